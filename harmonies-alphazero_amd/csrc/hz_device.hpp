@@ -1,0 +1,624 @@
+// hz_device.hpp — the Harmonies rules as CDNA4 device code.
+//
+// One lane owns one board ("lane-per-board"): every rule below is a handful
+// of 32/64-bit bitboard operations, so a wave advances 64 independent games
+// per instruction and the SoA state loads/stores are fully coalesced.
+//
+// Board state (48 B, six u64 words, stored SoA in HBM: word w of board b at
+// st[w * N + b]):
+//   pl[0..3]  bit-planes of the 4-bit stack code of every cell;
+//             player 0 in bits 0..22, player 1 in bits 32..54
+//             (cell = index into sorted(VALID_HEXES), constants.py:47-49)
+//   piles     5 piles x 3 tiles x 3 bits (7 = no tile), bits 45..47 = #piles
+//   misc      hand 3x3 bits | #hand 2 | bag 6x5 bits (TILE_TYPES order) |
+//             player 1 | phase 3 | game_over 1 | winner 2 | score0 8 | score1 8
+// Stack codes (every stack the placement rules can build,
+// harmonies_engine.py:183-194): 0 empty, 1+t a single tile t,
+// 7 wood+plant, 8 stone+stone, 9 stone x3, 10 wood+building,
+// 11 stone+building, 12 building+building.
+//
+// Chance: each board owns a CPython MT19937 stream (624 words SoA + a cursor)
+// seeded exactly like random.seed(int), consumed exactly like
+// random.sample(range(n), k) (Lib/random.py:239-249, :480-503).  The twist is
+// done lazily one word at a time (cursor in [624,1248) = "words below
+// cursor-624 are already twisted"), which is bit-identical to CPython's
+// batch twist for the consumed outputs; hz_mt_normalize turns it back into
+// CPython's (mt, index) form.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hz {
+
+constexpr int kCells = 23;
+constexpr uint32_t kAll23 = (1u << 23) - 1;
+constexpr int kActions = 143;
+enum { WATER = 0, PLANT = 1, WOOD = 2, STONE = 3, BUILDING = 4, FIELD = 5 };
+enum { PH_CHOOSE = 0, PH_P1 = 1, PH_P2 = 2, PH_P3 = 3, PH_OVER = 4 };
+enum {
+  ST_OK = 0, ST_BAD_PILE = 1, ST_BAD_FORMAT = 2, ST_NOT_IN_HAND = 3, ST_ILLEGAL_STACK = 4,
+  ST_BAD_PHASE = 5, ST_BAD_ACTION = 6, ST_NOOP = 7
+};
+
+// INITIAL_BAG (constants.py:41) in TILE_TYPES order.
+__host__ __device__ constexpr int initial_count(int t) {
+  return t == WATER ? 23 : t == PLANT ? 19 : t == WOOD ? 21 : t == STONE ? 23 : t == BUILDING ? 15 : 19;
+}
+
+struct State {
+  uint64_t pl[4];
+  uint64_t piles;
+  uint64_t misc;
+};
+
+// ------------------------------------------------------------------ fields
+__device__ __forceinline__ int hand_tile(uint64_t m, int j) { return (int)((m >> (3 * j)) & 7); }
+__device__ __forceinline__ int hand_n(uint64_t m) { return (int)((m >> 9) & 3); }
+__device__ __forceinline__ int bag_n(uint64_t m, int t) { return (int)((m >> (11 + 5 * t)) & 31); }
+__device__ __forceinline__ int player_of(uint64_t m) { return (int)((m >> 41) & 1); }
+__device__ __forceinline__ int phase_of(uint64_t m) { return (int)((m >> 42) & 7); }
+__device__ __forceinline__ int over_flag(uint64_t m) { return (int)((m >> 45) & 1); }
+__device__ __forceinline__ int winner_code(uint64_t m) { return (int)((m >> 46) & 3); }  // 0 None,1 P0,2 P1,3 draw
+__device__ __forceinline__ int score_of(uint64_t m, int p) { return (int)((m >> (48 + 8 * p)) & 255); }
+__device__ __forceinline__ int npiles_of(uint64_t piles) { return (int)((piles >> 45) & 7); }
+__device__ __forceinline__ int pile_tile(uint64_t piles, int i, int j) { return (int)((piles >> (9 * i + 3 * j)) & 7); }
+
+__device__ __forceinline__ uint64_t set_bits(uint64_t w, int lo, int width, uint64_t v) {
+  uint64_t mask = ((1ull << width) - 1) << lo;
+  return (w & ~mask) | ((v << lo) & mask);
+}
+
+__device__ __forceinline__ int bag_total(uint64_t m) {
+  int s = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) s += bag_n(m, t);
+  return s;
+}
+
+// is_game_over(): game_over and winner is not None (harmonies_engine.py:332-333)
+__device__ __forceinline__ bool game_done(uint64_t m) { return over_flag(m) && winner_code(m) != 0; }
+
+// ------------------------------------------------------------- bitboards
+__device__ __forceinline__ void planes_of(const State& s, int p, uint32_t b[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) b[k] = (uint32_t)(s.pl[k] >> (32 * p)) & kAll23;
+}
+
+template <int C>
+__device__ __forceinline__ uint32_t is_code(const uint32_t b[4]) {
+  uint32_t m = kAll23;
+  m &= (C & 1) ? b[0] : ~b[0];
+  m &= (C & 2) ? b[1] : ~b[1];
+  m &= (C & 4) ? b[2] : ~b[2];
+  m &= (C & 8) ? b[3] : ~b[3];
+  return m;
+}
+
+__device__ __forceinline__ int code_at(const State& s, int p, int c) {
+  int sh = 32 * p + c;
+  return (int)(((s.pl[0] >> sh) & 1) | (((s.pl[1] >> sh) & 1) << 1) | (((s.pl[2] >> sh) & 1) << 2) |
+               (((s.pl[3] >> sh) & 1) << 3));
+}
+
+__device__ __forceinline__ void set_code(State& s, int p, int c, int code) {
+  int sh = 32 * p + c;
+#pragma unroll
+  for (int k = 0; k < 4; k++) s.pl[k] = (s.pl[k] & ~(1ull << sh)) | ((uint64_t)((code >> k) & 1) << sh);
+}
+
+// New stack code after placing tile t on a stack, or -1 if illegal
+// (harmonies_engine.py:254-283; same rules as get_legal_moves :183-194).
+__device__ __forceinline__ int place_code(int code, int t) {
+  if (code == 0) return 1 + t;
+  if (t == PLANT && code == 3) return 7;
+  if (t == STONE && code == 4) return 8;
+  if (t == STONE && code == 8) return 9;
+  if (t == BUILDING && code == 3) return 10;
+  if (t == BUILDING && code == 4) return 11;
+  if (t == BUILDING && code == 5) return 12;
+  return -1;
+}
+
+// Tile at stack position pos (0 = bottom) for a code; 7 = none.
+__host__ __device__ constexpr uint64_t pack_tab(const int* v) {
+  uint64_t r = 0;
+  for (int i = 0; i < 13; i++) r |= (uint64_t)v[i] << (3 * i);
+  return r;
+}
+constexpr int kTab0[13] = {7, 0, 1, 2, 3, 4, 5, 2, 3, 3, 2, 3, 4};
+constexpr int kTab1[13] = {7, 7, 7, 7, 7, 7, 7, 1, 3, 3, 4, 4, 4};
+constexpr int kTab2[13] = {7, 7, 7, 7, 7, 7, 7, 7, 7, 3, 7, 7, 7};
+constexpr uint64_t kStackPos0 = pack_tab(kTab0);
+constexpr uint64_t kStackPos1 = pack_tab(kTab1);
+constexpr uint64_t kStackPos2 = pack_tab(kTab2);
+
+__device__ __forceinline__ int tile_at(int code, int pos) {
+  uint64_t t = pos == 0 ? kStackPos0 : pos == 1 ? kStackPos1 : kStackPos2;
+  return (int)((t >> (3 * code)) & 7);
+}
+
+// ----------------------------------------------------------- hex geometry
+// 5x7 grid layout for neighbour shifts: bit = (r+2)*7 + (q+3)
+// (process_game_state.py:9-12,36-37).  Axial direction (dq,dr) is a shift by
+// 7*dr + dq; every wrap-around lands on an invalid cell, masked by kValid35.
+__host__ __device__ constexpr int grid_bit(int c) {
+  // sorted(VALID_HEXES) -> (q, r)
+  constexpr int Q[23] = {-3, -2, -2, -2, -1, -1, -1, -1, -1, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 3};
+  constexpr int R[23] = {2, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, -2};
+  return (R[c] + 2) * 7 + (Q[c] + 3);
+}
+__host__ __device__ constexpr uint64_t valid35() {
+  uint64_t v = 0;
+  for (int c = 0; c < 23; c++) v |= 1ull << grid_bit(c);
+  return v;
+}
+constexpr uint64_t kValid35 = valid35();
+
+__device__ __forceinline__ uint64_t to35(uint32_t m) {
+  uint64_t g = 0;
+#pragma unroll
+  for (int c = 0; c < 23; c++) g |= (uint64_t)((m >> c) & 1u) << grid_bit(c);
+  return g;
+}
+
+__device__ __forceinline__ uint64_t nbr35(uint64_t s) {
+  return ((s << 1) | (s >> 1) | (s << 7) | (s >> 7) | (s << 6) | (s >> 6)) & kValid35;
+}
+
+// ------------------------------------------------------------------ scoring
+// calculate_score_for_player (harmonies_engine.py:357-523) on bitboards.
+__device__ __forceinline__ int water_points(int len) {  // :18-27
+  if (len <= 0) return 0;
+  if (len <= 6) return (int)((0x000F0B0805020000ull >> (8 * len)) & 0xFF);
+  return 15 + (len - 6) * 4;
+}
+
+struct ScoreParts { int grass, mount, field, bldg, water; };
+
+__device__ __forceinline__ ScoreParts score_parts(const uint32_t b23[4]) {
+  uint64_t b[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) b[k] = to35(b23[k]);
+  auto is = [&](int c) -> uint64_t {
+    uint64_t m = kValid35;
+    m &= (c & 1) ? b[0] : ~b[0];
+    m &= (c & 2) ? b[1] : ~b[1];
+    m &= (c & 4) ? b[2] : ~b[2];
+    m &= (c & 8) ? b[3] : ~b[3];
+    return m;
+  };
+  ScoreParts r;
+  // grass :369-390 (h1 plant 1; wood+plant 3; the h3 case is unreachable)
+  r.grass = __popcll(is(2)) + 3 * __popcll(is(7));
+  // mountains :392-422
+  uint64_t st1 = is(4), st2 = is(8), st3 = is(9);
+  uint64_t stone = st1 | st2 | st3;
+  uint64_t adj = stone & nbr35(stone);
+  r.mount = __popcll(adj & st1) + 3 * __popcll(adj & st2) + 7 * __popcll(adj & st3);
+  // fields :424-452 — +5 per connected component of size >= 2
+  uint64_t f = is(6);
+  uint64_t f2 = f & nbr35(f);
+  r.field = 0;
+  while (f2) {
+    uint64_t comp = f2 & (~f2 + 1);
+    for (;;) {
+      uint64_t nx = (comp | nbr35(comp)) & f2;
+      if (nx == comp) break;
+      comp = nx;
+    }
+    f2 &= ~comp;
+    r.field += 5;
+  }
+  // buildings :454-478 — building on top at height 2 with >= 3 distinct
+  // neighbouring top types
+  uint64_t tops[6];
+  tops[WATER] = is(1);
+  tops[PLANT] = is(2) | is(7);
+  tops[WOOD] = is(3);
+  tops[STONE] = stone;
+  tops[BUILDING] = is(5) | is(10) | is(11) | is(12);
+  tops[FIELD] = f;
+  uint64_t bh2 = is(10) | is(11) | is(12);
+  r.bldg = 0;
+  while (bh2) {
+    uint64_t cbit = bh2 & (~bh2 + 1);
+    bh2 &= ~cbit;
+    uint64_t nb = nbr35(cbit);
+    int types = 0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) types += (tops[t] & nb) ? 1 : 0;
+    if (types >= 3) r.bldg += 5;
+  }
+  // water :480-523 — per component of size >= 2, graph diameter d
+  // (max BFS eccentricity inside the component), get_water_score(d + 1)
+  uint64_t w = tops[WATER];
+  uint64_t w2 = w & nbr35(w);
+  r.water = 0;
+  while (w2) {
+    uint64_t comp = w2 & (~w2 + 1);
+    for (;;) {
+      uint64_t nx = (comp | nbr35(comp)) & w2;
+      if (nx == comp) break;
+      comp = nx;
+    }
+    w2 &= ~comp;
+    int diam = 0;
+    uint64_t todo = comp;
+    while (todo) {
+      uint64_t reach = todo & (~todo + 1);
+      todo &= ~reach;
+      int d = 0;
+      for (;;) {
+        uint64_t nx = (reach | nbr35(reach)) & comp;
+        if (nx == reach) break;
+        reach = nx;
+        d++;
+      }
+      diam = d > diam ? d : diam;
+    }
+    r.water += water_points(diam + 1);
+  }
+  return r;
+}
+
+__device__ __forceinline__ int score_player(const State& s, int p) {
+  uint32_t b[4];
+  planes_of(s, p, b);
+  ScoreParts r = score_parts(b);
+  return r.grass + r.mount + r.field + r.bldg + r.water;
+}
+
+// ------------------------------------------------------------------ MT19937
+struct MTRef {
+  uint32_t* mt;   // [624][N]
+  int32_t* pos;   // [N]
+  int n, b;
+  __device__ __forceinline__ uint32_t& w(int i) const { return mt[(size_t)i * n + b]; }
+};
+
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680U;
+  y ^= (y << 15) & 0xefc60000U;
+  y ^= (y >> 18);
+  return y;
+}
+
+__device__ __forceinline__ uint32_t twist_word(uint32_t cur, uint32_t next, uint32_t far) {
+  uint32_t y = (cur & 0x80000000U) | (next & 0x7fffffffU);
+  return far ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
+}
+
+// random.seed(int) for 0 <= seed < 2^64 (_randommodule.c random_seed +
+// init_by_array).  init_genrand(19650218) is regenerated on the fly.  The
+// caller sets its cursor to 624 (CPython: index = N after seeding).
+__device__ __forceinline__ void mt_seed(const MTRef& m, uint64_t seed) {
+  uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  int klen = key1 ? 2 : 1;
+  uint32_t init = 19650218U;  // init_genrand word i, generated in order
+  uint32_t prev = init;       // mt[i-1]
+  uint32_t mt0 = init;
+  int j = 0;
+  // first pass: i = 1..623, then mt[0] = mt[623] and one more step at i = 1
+  for (int i = 1; i < 624; i++) {
+    init = 1812433253U * (init ^ (init >> 30)) + (uint32_t)i;
+    uint32_t v = (init ^ ((prev ^ (prev >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
+    m.w(i) = v;
+    prev = v;
+    if (++j >= klen) j = 0;
+  }
+  mt0 = prev;
+  {
+    uint32_t v = (m.w(1) ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
+    m.w(1) = v;
+    prev = v;
+  }
+  // second pass: 623 steps starting at i = 2
+  for (int i = 2; i < 624; i++) {
+    uint32_t v = (m.w(i) ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    m.w(i) = v;
+    prev = v;
+  }
+  mt0 = prev;  // mt[0] = mt[623]
+  {
+    uint32_t v = (m.w(1) ^ ((mt0 ^ (mt0 >> 30)) * 1566083941U)) - 1U;
+    m.w(1) = v;
+  }
+  m.w(0) = 0x80000000U;
+}
+
+// genrand_uint32 with a lazy one-word twist.
+__device__ __forceinline__ uint32_t mt_next(const MTRef& m, int& pos) {
+  if (pos >= 1248) pos = 624;
+  if (pos < 624) return temper(m.w(pos++));
+  int i = pos - 624;
+  uint32_t nw;
+  if (i < 227) nw = twist_word(m.w(i), m.w(i + 1), m.w(i + 397));
+  else if (i < 623) nw = twist_word(m.w(i), m.w(i + 1), m.w(i - 227));
+  else nw = twist_word(m.w(623), m.w(0), m.w(396));
+  m.w(i) = nw;
+  pos++;
+  return temper(nw);
+}
+
+__device__ __forceinline__ uint32_t randbelow(const MTRef& m, int& pos, uint32_t n) {
+  if (!n) return 0;
+  int k = 32 - __clz(n);
+  uint32_t r = mt_next(m, pos) >> (32 - k);
+  while (r >= n) r = mt_next(m, pos) >> (32 - k);
+  return r;
+}
+
+// random.sample(range(n), k), k <= 3 (so setsize = 21, random.py:484-486).
+__device__ __forceinline__ void sample3(const MTRef& m, int& pos, uint32_t n, int k, uint32_t out[3]) {
+  if (n <= 21) {
+    // pool method; pool[x] == x except at <= 3 recorded positions
+    uint32_t mp[3], mv[3];
+    int nm = 0;
+    for (int i = 0; i < k; i++) {
+      uint32_t j = randbelow(m, pos, n - (uint32_t)i);
+      uint32_t last = n - (uint32_t)i - 1;
+      uint32_t vj = j, vl = last;
+      for (int q = 0; q < nm; q++) {
+        if (mp[q] == j) vj = mv[q];
+        if (mp[q] == last) vl = mv[q];
+      }
+      out[i] = vj;
+      mp[nm] = j;
+      mv[nm] = vl;
+      nm++;
+    }
+  } else {
+    for (int i = 0; i < k; i++) {
+      uint32_t j;
+      bool dup;
+      do {
+        j = randbelow(m, pos, n);
+        dup = (i > 0 && out[0] == j) || (i > 1 && out[1] == j);
+      } while (dup);
+      out[i] = j;
+    }
+  }
+}
+
+// _draw_tiles(3) (harmonies_engine.py:120-130): flat_bag follows the bag's
+// insertion order water, plant, wood, stone, field, building (constants.py:41).
+// Returns the pile as 3x3 bits (7 = none) and the number of tiles drawn.
+__device__ __forceinline__ int draw_pile(uint64_t& misc, const MTRef& m, int& pos, uint32_t& pile9) {
+  int cnt[6];
+#pragma unroll
+  for (int t = 0; t < 6; t++) cnt[t] = bag_n(misc, t);
+  uint32_t n = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) n += (uint32_t)cnt[t];
+  pile9 = 0x1FF;
+  if (!n) return 0;
+  int k = n < 3 ? (int)n : 3;
+  uint32_t idx[3];
+  sample3(m, pos, n, k, idx);
+  const int order[6] = {WATER, PLANT, WOOD, STONE, FIELD, BUILDING};
+  int drawn[3];
+  for (int i = 0; i < k; i++) {
+    uint32_t rem = idx[i];
+    int tile = -1;
+#pragma unroll
+    for (int o = 0; o < 6; o++) {
+      int tt = order[o];
+      if (tile < 0) {
+        if (rem < (uint32_t)cnt[tt]) tile = tt;
+        else rem -= (uint32_t)cnt[tt];
+      }
+    }
+    drawn[i] = tile;
+  }
+  // indices map against the pre-draw bag, then every drawn tile decrements
+  // the bag (:126-129)
+  for (int i = 0; i < k; i++) {
+    int t = drawn[i];
+    misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)(bag_n(misc, t) - 1));
+    pile9 = (pile9 & ~(7u << (3 * i))) | ((uint32_t)t << (3 * i));
+  }
+  return k;
+}
+
+// _replenish_piles (:132-137)
+__device__ __forceinline__ void replenish(State& s, const MTRef& m, int& pos) {
+  int np = npiles_of(s.piles);
+  while (np < 5) {
+    uint32_t pile9;
+    int k = draw_pile(s.misc, m, pos, pile9);
+    if (!k) break;
+    s.piles = set_bits(s.piles, 9 * np, 9, pile9);
+    np++;
+    s.piles = set_bits(s.piles, 45, 3, (uint64_t)np);
+  }
+}
+
+// HarmoniesGameState.__init__ (:66-79)
+__device__ __forceinline__ void reset_state(State& s, const MTRef& m, int& pos) {
+  s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
+  s.piles = (1ull << 45) - 1;  // every tile slot = 7 (none), 0 piles
+  uint64_t misc = 0x1FF;  // empty hand
+#pragma unroll
+  for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  s.misc = misc;  // player 0, choose_pile, not over, winner None, scores 0
+  replenish(s, m, pos);
+}
+
+// ------------------------------------------------------------- legal mask
+// get_legal_moves (:145-208) + get_action_index (process_game_state.py:156-179):
+// action = pile index during choose_pile, else 5 + tile*23 + cell.
+__device__ __forceinline__ void or_range(uint64_t mask[3], int lo, uint32_t m23) {
+  int w = lo >> 6, off = lo & 63;
+  uint64_t v = (uint64_t)m23;
+  mask[w] |= v << off;
+  if (off + 23 > 64) mask[w + 1] |= v >> (64 - off);
+}
+
+__device__ __forceinline__ int legal_mask(const State& s, uint64_t mask[3]) {
+  mask[0] = mask[1] = mask[2] = 0;
+  int ph = phase_of(s.misc);
+  if (ph == PH_CHOOSE) {
+    int np = npiles_of(s.piles);
+    mask[0] = (1ull << np) - 1;
+    return np;
+  }
+  if (ph < PH_P1 || ph > PH_P3) return 0;
+  int nh = hand_n(s.misc);
+  if (!nh) return 0;
+  uint32_t b[4];
+  planes_of(s, player_of(s.misc), b);
+  uint32_t empty = kAll23 & ~(b[0] | b[1] | b[2] | b[3]);
+  uint32_t wood1 = is_code<3>(b), stone1 = is_code<4>(b), stone2 = is_code<8>(b), bld1 = is_code<5>(b);
+  uint32_t has = 0;
+  for (int j = 0; j < nh; j++) has |= 1u << hand_tile(s.misc, j);
+  int count = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    if (!(has & (1u << t))) continue;
+    uint32_t m = empty;
+    if (t == PLANT) m |= wood1;
+    if (t == STONE) m |= stone1 | stone2;
+    if (t == BUILDING) m |= wood1 | stone1 | bld1;
+    or_range(mask, 5 + 23 * t, m);
+    count += __popc(m);
+  }
+  return count;
+}
+
+__device__ __forceinline__ int select64(uint64_t w, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    uint64_t lo = w & ((1ull << s) - 1);
+    int c = __popcll(lo);
+    if (k >= c) { k -= c; w >>= s; pos += s; }
+    else w = lo;
+  }
+  return pos;
+}
+
+// k-th (0-based) legal action in ascending action order.
+__device__ __forceinline__ int kth_action(const uint64_t mask[3], int k) {
+  int c0 = __popcll(mask[0]);
+  if (k < c0) return select64(mask[0], k);
+  k -= c0;
+  int c1 = __popcll(mask[1]);
+  if (k < c1) return 64 + select64(mask[1], k);
+  k -= c1;
+  return 128 + select64(mask[2], k);
+}
+
+// ------------------------------------------------------------------- step
+__device__ __forceinline__ void finish_game(State& s) {  // :344-354
+  int s0 = score_player(s, 0), s1 = score_player(s, 1);
+  uint64_t m = s.misc;
+  m = set_bits(m, 42, 3, PH_OVER);
+  m = set_bits(m, 48, 8, (uint64_t)s0);
+  m = set_bits(m, 56, 8, (uint64_t)s1);
+  m = set_bits(m, 46, 2, s0 > s1 ? 1 : s1 > s0 ? 2 : 3);
+  s.misc = m;
+}
+
+__device__ __forceinline__ void end_turn(State& s, const MTRef& mt, int& pos) {  // :301-329
+  int p = player_of(s.misc);
+  uint32_t b[4];
+  planes_of(s, p, b);
+  int filled = __popc(b[0] | b[1] | b[2] | b[3]);
+  bool player_trigger = (kCells - filled) <= 2;
+  bool bag_empty_before = bag_total(s.misc) == 0;
+  replenish(s, mt, pos);
+  bool bag_trigger = bag_empty_before && npiles_of(s.piles) == 0;
+  bool end = player_trigger || bag_trigger;
+  if (end && !over_flag(s.misc)) {
+    s.misc = set_bits(s.misc, 45, 1, 1);
+    if (p == 0) {
+      s.misc = set_bits(s.misc, 41, 1, 1);
+      s.misc = set_bits(s.misc, 42, 3, PH_CHOOSE);
+    } else {
+      finish_game(s);
+    }
+  } else if (over_flag(s.misc)) {
+    finish_game(s);
+  } else {
+    s.misc = set_bits(s.misc, 41, 1, (uint64_t)(1 - p));
+    s.misc = set_bits(s.misc, 42, 3, PH_CHOOSE);
+  }
+}
+
+// apply_move (:210-298) in place; returns a status (state untouched unless OK).
+__device__ __forceinline__ int step_state(State& s, int a, const MTRef& mt, int& pos) {
+  if (a < 0 || a >= kActions) return ST_BAD_ACTION;
+  int ph = phase_of(s.misc);
+  if (ph == PH_CHOOSE) {
+    int np = npiles_of(s.piles);
+    if (a >= 5 || a >= np) return ST_BAD_PILE;
+    uint32_t pile9 = (uint32_t)(s.piles >> (9 * a)) & 0x1FF;
+    int len = ((pile9 & 7) != 7) + (((pile9 >> 3) & 7) != 7) + (((pile9 >> 6) & 7) != 7);
+    uint64_t lower = s.piles & ((1ull << (9 * a)) - 1);
+    uint64_t upper = (s.piles & ((1ull << 45) - 1)) >> (9 * (a + 1));
+    uint64_t np_piles = lower | (upper << (9 * a));
+    np_piles |= 0x1FFull << 36;  // vacated top slot
+    s.piles = set_bits(np_piles, 45, 3, (uint64_t)(np - 1));
+    uint64_t m = set_bits(s.misc, 0, 9, pile9);
+    m = set_bits(m, 9, 2, (uint64_t)len);
+    s.misc = set_bits(m, 42, 3, PH_P1);
+    return ST_OK;
+  }
+  if (ph >= PH_P1 && ph <= PH_P3) {
+    if (a < 5) return ST_BAD_FORMAT;
+    int t = (a - 5) / 23, c = (a - 5) % 23;
+    int nh = hand_n(s.misc), j = -1;
+    for (int q = nh - 1; q >= 0; q--)
+      if (hand_tile(s.misc, q) == t) j = q;
+    if (j < 0) return ST_NOT_IN_HAND;
+    int p = player_of(s.misc);
+    int nc = place_code(code_at(s, p, c), t);
+    if (nc < 0) return ST_ILLEGAL_STACK;
+    // hand.remove(tile): drop entry j, shift the rest down
+    uint32_t h9 = (uint32_t)(s.misc & 0x1FF);
+    uint32_t low = h9 & ((1u << (3 * j)) - 1);
+    uint32_t high = h9 >> (3 * (j + 1));
+    uint32_t nh9 = (low | (high << (3 * j)) | (7u << 6)) & 0x1FF;
+    uint64_t m = set_bits(s.misc, 0, 9, nh9);
+    s.misc = set_bits(m, 9, 2, (uint64_t)(nh - 1));
+    set_code(s, p, c, nc);
+    if (ph < PH_P3) s.misc = set_bits(s.misc, 42, 3, (uint64_t)(ph + 1));
+    else end_turn(s, mt, pos);
+    return ST_OK;
+  }
+  return ST_BAD_PHASE;
+}
+
+// ------------------------------------------------------------ action rule
+__device__ __forceinline__ uint64_t rule_hash(uint64_t seed, uint64_t ply) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ULL + ply;
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int rule_pick(uint64_t seed, int ply, int n_legal) {
+  uint64_t z = rule_hash(seed, (uint64_t)ply);
+  return (int)(((z >> 32) * (uint64_t)n_legal) >> 32);
+}
+
+// ------------------------------------------------------------ SoA access
+__device__ __forceinline__ State load_state(const uint64_t* __restrict__ st, int n, int b) {
+  State s;
+#pragma unroll
+  for (int k = 0; k < 4; k++) s.pl[k] = st[(size_t)k * n + b];
+  s.piles = st[(size_t)4 * n + b];
+  s.misc = st[(size_t)5 * n + b];
+  return s;
+}
+
+__device__ __forceinline__ void store_state(uint64_t* __restrict__ st, int n, int b, const State& s) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) st[(size_t)k * n + b] = s.pl[k];
+  st[(size_t)4 * n + b] = s.piles;
+  st[(size_t)5 * n + b] = s.misc;
+}
+
+}  // namespace hz

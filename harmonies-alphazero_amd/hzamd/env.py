@@ -1,0 +1,174 @@
+"""BatchedEnv: N Harmonies boards resident in HBM, stepped by HIP kernels.
+
+This is the batched form of the reference env surface
+(harmonies_engine.py: HarmoniesGameState() :66-79, get_legal_moves :145-208,
+apply_move :210-298, calculate_score_for_player :357-367) and of the
+encoder (process_game_state.py:15-137).  Every method enqueues work on the
+current torch stream through libhz.so; nothing is computed on the host.
+"""
+import torch
+
+from . import _native as nat
+from .state import WORDS
+
+ACTION_SIZE = 143
+
+
+class BatchedEnv:
+    def __init__(self, n_boards, seed_base=0, device="cuda"):
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise nat.NativeError("BatchedEnv needs a GPU device (HIP); there is no CPU fallback")
+        self.n = int(n_boards)
+        L = nat.lib()
+        with torch.cuda.device(self.device):
+            self._h = L.hz_env_create(self.n, seed_base, nat.stream_ptr(self.device))
+        if not self._h:
+            raise nat.NativeError("hz_env_create failed")
+        self.seed_base = seed_base
+        self._mask = torch.zeros(self.n, 3, dtype=torch.int64, device=self.device)
+        self._count = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+        self._status = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+        self._score = torch.zeros(self.n, 2, dtype=torch.int32, device=self.device)
+
+    # -- plumbing ----------------------------------------------------------
+    def _sync_stream(self):
+        nat.lib().hz_env_set_stream(self._h, nat.stream_ptr(self.device))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            nat.lib().hz_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- env surface ---------------------------------------------------------
+    def reset(self, sel=None, seeds=None):
+        """HarmoniesGameState() on every board (or on boards where sel != 0)."""
+        self._sync_stream()
+        if sel is not None:
+            sel = sel.to(device=self.device, dtype=torch.uint8).contiguous()
+        if seeds is not None:
+            seeds = seeds.to(device=self.device, dtype=torch.int64).contiguous()
+        nat.check(nat.lib().hz_reset(self._h, nat.ptr(sel), nat.ptr(seeds)), "hz_reset")
+
+    def legal_mask(self, out=None, count=None):
+        """143-bit legal-action mask per board, int64 [n, 3] (bit i of word w
+        = action 64*w + i) and the number of legal actions int32 [n]."""
+        self._sync_stream()
+        out = self._mask if out is None else out
+        count = self._count if count is None else count
+        nat.check(nat.lib().hz_legal_mask(self._h, nat.ptr(out), nat.ptr(count)), "hz_legal_mask")
+        return out, count
+
+    def legal_actions(self):
+        """Boolean [n, 143] view of legal_mask (unpacked on the device)."""
+        mask, _ = self.legal_mask()
+        return unpack_mask(mask)
+
+    def step(self, actions, status=None):
+        """apply_move per board (actions int16 [n], <0 = no-op); int32 status."""
+        self._sync_stream()
+        actions = actions.to(device=self.device, dtype=torch.int16).contiguous()
+        status = self._status if status is None else status
+        nat.check(nat.lib().hz_step(self._h, nat.ptr(actions), nat.ptr(status)), "hz_step")
+        return status
+
+    def score(self, parts=False):
+        """calculate_score_for_player for both players: int32 [n, 2]
+        (and [n, 2, 5] per-habitat parts when parts=True)."""
+        self._sync_stream()
+        out = self._score
+        pt = torch.zeros(self.n, 2, 5, dtype=torch.int32, device=self.device) if parts else None
+        nat.check(nat.lib().hz_score(self._h, nat.ptr(out), nat.ptr(pt)), "hz_score")
+        return (out, pt) if parts else out
+
+    def encode(self, idx=None, board=None, glob=None):
+        """create_state_tensors for boards idx (default all): f32 [m,38,5,7], [m,42]."""
+        self._sync_stream()
+        if idx is not None:
+            idx = idx.to(device=self.device, dtype=torch.int32).contiguous()
+            m = idx.numel()
+        else:
+            m = self.n
+        if board is None:
+            board = torch.empty(m, 38, 5, 7, dtype=torch.float32, device=self.device)
+        if glob is None:
+            glob = torch.empty(m, 42, dtype=torch.float32, device=self.device)
+        nat.check(nat.lib().hz_encode(self._h, nat.ptr(idx), m, nat.ptr(board), nat.ptr(glob)), "hz_encode")
+        return board, glob
+
+    def rule_actions(self, mask=None, count=None, out=None):
+        """The build-defined deterministic policy (splitmix64 rule)."""
+        self._sync_stream()
+        if mask is None:
+            mask, count = self.legal_mask()
+        out = torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None else out
+        nat.check(nat.lib().hz_rule_actions(self._h, nat.ptr(mask), nat.ptr(count), nat.ptr(out)),
+                  "hz_rule_actions")
+        return out
+
+    def rollout(self, max_plies, auto_reset=False, record=False, games_done=None, steps_done=None):
+        """Fused rule-driven play of up to max_plies plies per board."""
+        self._sync_stream()
+        traj = None
+        if record:
+            traj = (torch.zeros(max_plies, WORDS, self.n, dtype=torch.int64, device=self.device),
+                    torch.zeros(max_plies, self.n, 3, dtype=torch.int64, device=self.device),
+                    torch.full((max_plies, self.n), -1, dtype=torch.int16, device=self.device))
+        games_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if games_done is None else games_done
+        steps_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if steps_done is None else steps_done
+        ts, tm, ta = traj if traj else (None, None, None)
+        nat.check(nat.lib().hz_rollout(self._h, int(max_plies), int(bool(auto_reset)), nat.ptr(ts), nat.ptr(tm),
+                                       nat.ptr(ta), nat.ptr(games_done), nat.ptr(steps_done)), "hz_rollout")
+        return games_done, steps_done, traj
+
+    # -- state transfer -------------------------------------------------------
+    def export_state(self, with_mt=False):
+        """int64 [6, n] state words (+ uint32-as-int32 [624, n] MT words and
+        int32 [n] CPython indices when with_mt)."""
+        self._sync_stream()
+        st = torch.empty(WORDS, self.n, dtype=torch.int64, device=self.device)
+        mt = idx = None
+        if with_mt:
+            mt = torch.empty(624, self.n, dtype=torch.int32, device=self.device)
+            idx = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        nat.check(nat.lib().hz_export_state(self._h, nat.ptr(st), nat.ptr(mt), nat.ptr(idx)), "hz_export_state")
+        return (st, mt, idx) if with_mt else st
+
+    def import_state(self, state, mt=None, mt_index=None):
+        self._sync_stream()
+        state = state.to(device=self.device, dtype=torch.int64).contiguous()
+        if mt is not None:
+            mt = mt.to(device=self.device, dtype=torch.int32).contiguous()
+            mt_index = mt_index.to(device=self.device, dtype=torch.int32).contiguous()
+        nat.check(nat.lib().hz_import_state(self._h, nat.ptr(state), nat.ptr(mt), nat.ptr(mt_index)),
+                  "hz_import_state")
+
+    def done(self):
+        """is_game_over() per board (bool [n]) from the state words."""
+        misc = self.export_state()[5]
+        over = (misc >> 45) & 1
+        win = (misc >> 46) & 3
+        return (over == 1) & (win != 0)
+
+
+_BIT = None
+
+
+def unpack_mask(mask):
+    """int64 [n, 3] packed mask -> bool [n, 143]."""
+    global _BIT
+    if _BIT is None or _BIT.device != mask.device:
+        _BIT = torch.arange(64, device=mask.device, dtype=torch.int64)
+    bits = (mask.unsqueeze(-1) >> _BIT) & 1  # [n, 3, 64]
+    return bits.reshape(mask.shape[0], 192)[:, :ACTION_SIZE].bool()

@@ -1,0 +1,117 @@
+/* hz_abi.h — C-ABI of libhz.so, the MI355X-native Harmonies self-play engine.
+ *
+ * The reference (IllyaArtemchuk/Harmonies-Alphazero) is pure Python with no
+ * FFI; its hot path is reached through duck-typed Python surfaces.  Each entry
+ * point below is the batched device form of one of those surfaces (cited as
+ * /root/reference file:line).  The Python package
+ * harmonies-alphazero_amd/hzamd binds them with ctypes; INTEGRATION.md shows
+ * the binding a maintainer would add.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer (e.g. torch tensor.data_ptr())
+ *    unless stated otherwise; it must stay valid until the work enqueued on
+ *    the handle's stream has run.  Calls are asynchronous, stream-ordered on
+ *    the handle's stream, and never allocate or synchronize.
+ *  - Return value: 0 = enqueued; <0 = invalid argument (nothing enqueued);
+ *    >0 = hipError_t of the failed launch.
+ *  - Per-board rule violations are not errors of the call: they come back as
+ *    per-board status codes (HZ_ST_*), where the reference raises ValueError.
+ *  - Board b's state is the structure-of-arrays record documented in
+ *    harmonies-alphazero_amd/csrc/hz_device.hpp (six u64 words, word w at
+ *    state[w * n + b]); its chance stream is a CPython MT19937 (624 words at
+ *    mt[i * n + b] plus a cursor).
+ */
+#ifndef HZ_ABI_H
+#define HZ_ABI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-board status codes (reference ValueError sites in parentheses) */
+enum {
+  HZ_ST_OK = 0,
+  HZ_ST_BAD_PILE = 1,        /* harmonies_engine.py:216-220 "Invalid pile index"      */
+  HZ_ST_BAD_FORMAT = 2,      /* :227-236 "Invalid move format for placement phase"     */
+  HZ_ST_NOT_IN_HAND = 3,     /* :244-248 "Illegal move attempted: Tile ... not in hand" */
+  HZ_ST_ILLEGAL_STACK = 4,   /* :281-283 "Cannot place ... on ... with stack"           */
+  HZ_ST_BAD_PHASE = 5,       /* :296-297 "Invalid turn phase"                           */
+  HZ_ST_BAD_ACTION = 6,      /* action id outside [0,143) (process_game_state.py:156-179) */
+  HZ_ST_NOOP = 7             /* negative action: board left untouched                    */
+};
+
+typedef struct hz_env hz_env;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* n_boards boards; board b's k-th game is seeded like
+ * random.seed(seed_base + b + (k << 32)) followed by HarmoniesGameState()
+ * (harmonies_engine.py:66-79).  stream: hipStream_t, NULL = null stream.
+ * The handle owns all device buffers (48 B state + 2.5 KB MT per board). */
+hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream);
+void hz_env_destroy(hz_env *env);
+int32_t hz_env_size(const hz_env *env);
+int hz_env_set_stream(hz_env *env, void *stream);
+/* device pointers of the handle's own buffers (for zero-copy views) */
+uint64_t *hz_env_state_ptr(hz_env *env);     /* [6][n]            */
+uint32_t *hz_env_mt_ptr(hz_env *env);        /* [624][n]          */
+int32_t *hz_env_mt_pos_ptr(hz_env *env);     /* [n]               */
+int32_t *hz_env_ply_ptr(hz_env *env);        /* [n] plies played in the current game */
+uint64_t *hz_env_seed_ptr(hz_env *env);      /* [n] seed of the current game */
+
+/* ---- env surface (step / reset / legal_actions / score) ----------------- */
+/* reset: HarmoniesGameState() for every board with sel[b] != 0 (sel NULL =
+ * all boards).  seeds (optional, [n]) overrides the per-board seed. */
+int hz_reset(hz_env *env, const uint8_t *sel, const uint64_t *seeds);
+
+/* legal_actions: get_legal_moves (harmonies_engine.py:145-208) mapped through
+ * get_action_index (process_game_state.py:156-179) to a 143-bit mask per
+ * board, mask[b*3 + w] bit i = action 64*w + i.  count[b] = #legal (may be
+ * NULL).  A finished board has an empty mask. */
+int hz_legal_mask(hz_env *env, uint64_t *mask, int32_t *count);
+
+/* step: apply_move (harmonies_engine.py:210-298) in place, including
+ * _end_turn_actions (:301-329) and chance draws.  action[b] < 0 = no-op.
+ * status[b] (may be NULL) gets an HZ_ST_* code; on a non-zero status the
+ * board is unchanged (the reference raises before committing its clone). */
+int hz_step(hz_env *env, const int16_t *action, int32_t *status);
+
+/* score: calculate_score_for_player(p) (:357-367) for both players of every
+ * board, out[b*2 + p].  parts (may be NULL): out_parts[(b*2+p)*5 + k] for
+ * grass, mountains, fields, buildings, water (:369-523). */
+int hz_score(hz_env *env, int32_t *out, int32_t *out_parts);
+
+/* encode: create_state_tensors (process_game_state.py:15-137) for boards
+ * idx[0..m) (idx NULL = boards 0..m-1): board[m][38][5][7], glob[m][42], f32. */
+int hz_encode(hz_env *env, const int32_t *idx, int32_t m, float *board, float *glob);
+
+/* Build-defined deterministic policy used by the env benchmark and the golden
+ * traces: pick legal action k = ((splitmix64(seed, ply) >> 32) * L) >> 32 in
+ * ascending action order.  Writes action[b] (-1 if no legal move). */
+int hz_rule_actions(hz_env *env, const uint64_t *mask, const int32_t *count, int16_t *action);
+
+/* Fused env loop: every board plays up to max_plies rule-driven plies
+ * (legal mask -> rule pick -> step), stopping at game end (auto_reset = 0) or
+ * starting its next game (auto_reset != 0).  Optional per-ply records
+ * (NULL = off): traj_state[(ply*6 + w)*n + b], traj_mask[(ply*n + b)*3 + w],
+ * traj_action[ply*n + b] (-1 after the game ended).  games_done[b] counts
+ * games finished during the call, steps_done[b] env steps taken. */
+int hz_rollout(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state,
+               uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done,
+               int32_t *steps_done);
+
+/* ---- state transfer (Python facade and tests) --------------------------- */
+/* export: state[6][n] and, optionally, the MT streams in CPython getstate()
+ * form (mt[624][n], mt_index[n] in [0, 624]).  Normalises the lazy twist in
+ * place (semantics unchanged). */
+int hz_export_state(hz_env *env, uint64_t *state, uint32_t *mt, int32_t *mt_index);
+/* import: the inverse; mt/mt_index may be NULL to keep the current streams. */
+int hz_import_state(hz_env *env, const uint64_t *state, const uint32_t *mt, const int32_t *mt_index);
+
+/* ---- build info ---------------------------------------------------------- */
+const char *hz_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,271 @@
+"""GPU parity of the HIP env kernels (libhz.so via hzamd.BatchedEnv) against
+the reference golden fixtures and the C oracle.  Bit-exact for every state,
+mask, action, score and encoder output."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+from hzamd.state import pack_ref, unpack_ref, words_to_array
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+@pytest.fixture(scope="module")
+def Env():
+    from hzamd.env import BatchedEnv
+    return BatchedEnv
+
+
+def states_of(env):
+    st = env.export_state().cpu().numpy()
+    return np.stack([unpack_ref(st[:, b]) for b in range(env.n)])
+
+
+def import_refstates(env, refs):
+    words = words_to_array([pack_ref(v) for v in refs])  # [n, 6]
+    env.import_state(torch.from_numpy(np.ascontiguousarray(words.T)))
+
+
+def mask_bits(mask_words):
+    """int64 [n,3] -> uint8 [n,143]"""
+    m = mask_words.view(np.uint64) if mask_words.dtype == np.int64 else mask_words
+    out = np.zeros((m.shape[0], 143), np.uint8)
+    for a in range(143):
+        out[:, a] = (m[:, a // 64] >> np.uint64(a % 64)) & np.uint64(1)
+    return out
+
+
+def test_reset_matches_reference(Env):
+    f = load("env_traces.npz")
+    env = Env(64, seed_base=0, device=DEV)
+    env.reset()
+    got = states_of(env)
+    first = f["states"][f["offsets"][:-1]]
+    assert (got == first).all()
+
+
+def test_stepwise_api_matches_traces(Env):
+    """legal_mask -> rule_actions -> step, ply by ply, against the traces."""
+    f = load("env_traces.npz")
+    off = f["offsets"]
+    n = len(f["seeds"])
+    env = Env(n, seed_base=0, device=DEV)
+    env.reset()
+    ply = 0
+    max_len = int(np.diff(off).max())
+    while ply < max_len:
+        live = np.array([off[g] + ply < off[g + 1] for g in range(n)])
+        mask, count = env.legal_mask()
+        acts = env.rule_actions(mask, count)
+        st = states_of(env)
+        mb = mask_bits(mask.cpu().numpy())
+        a = acts.cpu().numpy()
+        for g in range(n):
+            if live[g]:
+                p = off[g] + ply
+                assert (st[g] == f["states"][p]).all(), (g, ply)
+                assert (np.packbits(mb[g], bitorder="little") == f["masks"][p]).all(), (g, ply)
+                assert a[g] == f["actions"][p], (g, ply)
+            else:
+                assert a[g] == -1 and mb[g].sum() == 0
+        status = env.step(acts).cpu().numpy()
+        assert (status[live] == 0).all()
+        assert (status[~live] == 7).all()
+        ply += 1
+    st = states_of(env)
+    assert (st == f["finals"]).all()
+    assert env.done().all()
+
+
+def test_rollout_records_traces(Env):
+    f = load("env_traces.npz")
+    off = f["offsets"]
+    n = len(f["seeds"])
+    env = Env(n, seed_base=0, device=DEV)
+    env.reset()
+    games, steps, (ts, tm, ta) = env.rollout(max_plies=80, record=True)
+    ts, tm, ta = ts.cpu().numpy(), tm.cpu().numpy(), ta.cpu().numpy()
+    assert (steps.cpu().numpy() == f["plies"]).all()
+    assert (games.cpu().numpy() == 1).all()
+    for g in range(n):
+        L = off[g + 1] - off[g]
+        for ply in range(L):
+            p = off[g] + ply
+            assert (unpack_ref(ts[ply, :, g]) == f["states"][p]).all()
+            assert (np.packbits(mask_bits(tm[ply, g][None])[0], bitorder="little") == f["masks"][p]).all()
+            assert ta[ply, g] == f["actions"][p]
+        assert (ta[L:, g] == -1).all()
+    assert (states_of(env) == f["finals"]).all()
+
+
+def test_rollout_finals_and_rng_stream(Env):
+    f = load("env_finals.npz")
+    n = len(f["seeds"])
+    env = Env(n, seed_base=int(f["seeds"][0]), device=DEV)
+    env.reset()
+    games, steps, _ = env.rollout(max_plies=200)
+    assert (steps.cpu().numpy() == f["plies"]).all()
+    assert (states_of(env) == f["finals"]).all()
+    _, mt, idx = env.export_state(with_mt=True)
+    mt = mt.cpu().numpy().view(np.uint32)
+    idx = idx.cpu().numpy()
+    for b in range(n):
+        m = oracle.mt_from_words(mt[:, b], idx[b])
+        assert oracle.mt_next32(m) == f["next_word"][b], b
+
+
+def test_full_size_4096_vs_oracle(Env):
+    """BASELINE config 2 size: 4096 boards to game end, bit-exact vs the C oracle."""
+    n, base = 4096, 777
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    games, steps, _ = env.rollout(max_plies=200)
+    total, finals, plies, nxt = oracle.play_rule_games(n, base, nthreads=8)
+    assert (states_of(env) == finals).all()
+    assert (steps.cpu().numpy() == plies).all()
+    assert int(steps.sum()) == total
+    score = env.score().cpu().numpy()
+    assert (score[:, 0] == finals[:, 76]).all() and (score[:, 1] == finals[:, 77]).all()
+
+
+def test_auto_reset_steady_state(Env):
+    """auto_reset: board b's second game is seeded seed_base + b + 2^32."""
+    n, base = 256, 31
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    games, steps, _ = env.rollout(max_plies=150, auto_reset=True)
+    st = states_of(env)
+    g0 = oracle.play_rule_games(n, base)[2]
+    for b in range(0, n, 17):
+        m = oracle.mt_seed(base + b + (1 << 32))
+        s = oracle.reset(m)
+        seed = base + b + (1 << 32)
+        for ply in range(150 - int(g0[b])):
+            if oracle.is_game_over(s):
+                break
+            mask = oracle.legal(s)
+            L = int(mask.sum())
+            a = np.flatnonzero(mask)[((oracle.rule(seed, ply) >> 32) * L) >> 32]
+            s = oracle.step(s, int(a), m)[1]
+        assert (st[b] == s).all(), b
+    assert (games.cpu().numpy() >= 1).all()
+
+
+def test_scoring_known_answers(Env):
+    f = load("scoring.npz")
+    boards = f["boards"]
+    refs = np.zeros((len(boards), 78), np.int16)
+    refs[:, 0:23] = boards
+    refs[:, 23:46] = boards[::-1]
+    refs[:, 46:61] = -1
+    refs[:, 62:65] = -1
+    refs[:, 75] = -2
+    env = Env(len(boards), device=DEV)
+    import_refstates(env, refs)
+    total, parts = env.score(parts=True)
+    parts = parts.cpu().numpy()
+    assert (parts[:, 0, :] == f["scores"]).all()
+    assert (parts[:, 1, :] == f["scores"][::-1]).all()
+    assert (total.cpu().numpy()[:, 0] == f["scores"].sum(1)).all()
+    assert list(parts[0, 0]) == [4, 4, 5, 5, 5]
+
+
+def test_encoder_bit_exact(Env):
+    f = load("encoder.npz")
+    refs = f["states"]
+    env = Env(len(refs), device=DEV)
+    import_refstates(env, refs)
+    board, glob = env.encode()
+    b = board.cpu().numpy()
+    g = glob.cpu().numpy()
+    assert (b.view(np.uint32) == f["boards"].view(np.uint32)).all()
+    assert (g.view(np.uint32) == f["globs"].view(np.uint32)).all()
+    # gathered subset, reversed order
+    idx = torch.arange(len(refs) - 1, -1, -3, dtype=torch.int32)
+    board2, glob2 = env.encode(idx)
+    assert (board2.cpu().numpy() == f["boards"][idx.numpy()]).all()
+    assert (glob2.cpu().numpy() == f["globs"][idx.numpy()]).all()
+
+
+def test_encoder_game_over_states(Env):
+    f = load("env_finals.npz")
+    refs = f["finals"][:128]
+    env = Env(len(refs), device=DEV)
+    import_refstates(env, refs)
+    board, glob = env.encode()
+    for k in range(len(refs)):
+        ob, og = oracle.encode(refs[k])
+        assert (board[k].cpu().numpy() == ob).all() and (glob[k].cpu().numpy() == og).all()
+
+
+def test_status_codes_match_reference_errors(Env):
+    env = Env(8, seed_base=5, device=DEV)
+    env.reset()
+    before = env.export_state().clone()
+    # choose_pile phase: placement index -> bad pile (1), pile 5 -> bad pile (1),
+    # id 143 -> bad action (6), -1 -> no-op (7); the board must not change
+    acts = torch.tensor([7, 5, 143, -1, 0, 1, 2, 3], dtype=torch.int16)
+    st = env.step(acts).cpu().numpy()
+    assert list(st) == [1, 1, 6, 7, 0, 0, 0, 0]
+    after = env.export_state()
+    assert (after[:, :4] == before[:, :4]).all()
+    assert not (after[:, 4:] == before[:, 4:]).all()
+    # boards 4..7 are placing: pile index -> bad format (2), missing tile -> 3
+    ref = states_of(env)
+    acts = [-1, -1, -1, -1]
+    for b in range(4, 8):
+        hand = set(int(t) for t in ref[b, 62:62 + ref[b, 65]])
+        missing = [t for t in range(6) if t not in hand][0]
+        acts.append(0 if b < 6 else 5 + missing * 23 + 11)
+    st = env.step(torch.tensor(acts, dtype=torch.int16)).cpu().numpy()
+    assert list(st[4:]) == [2, 2, 3, 3]
+    # illegal stacking (4): second tile on the occupied centre cell when the
+    # oracle says so; game_over phase (5)
+    for seed in range(40):
+        m = oracle.mt_seed(seed)
+        s = oracle.reset(m)
+        s = oracle.step(s, 0, m)[1]
+        hand = [int(t) for t in s[62:65] if t >= 0]
+        s = oracle.step(s, 5 + hand[0] * 23 + 11, m)[1]
+        blocked = 5 + hand[1] * 23 + 11
+        expect, _ = oracle.step(s, blocked, oracle.mt_seed(seed))
+        if expect == 4:
+            break
+    assert expect == 4
+    env2 = Env(1, device=DEV)
+    import_refstates(env2, [s])
+    assert env2.step(torch.tensor([blocked], dtype=torch.int16)).cpu().numpy()[0] == 4
+    over = s.copy()
+    over[73] = 4
+    import_refstates(env2, [over])
+    assert env2.step(torch.tensor([0], dtype=torch.int16)).cpu().numpy()[0] == 5
+
+
+def test_mt_import_export_roundtrip_cpython(Env):
+    """A CPython random state imported mid-stream continues exactly like CPython."""
+    import random
+    r = random.Random(99)
+    for _ in range(700):
+        r.getrandbits(32)
+    ver, words, _ = r.getstate()
+    words = np.array(words, np.uint64)
+    env = Env(1, device=DEV)
+    m = oracle.mt_seed(0)
+    st = oracle.reset(m)
+    mt = torch.from_numpy(words[:624].astype(np.uint32).view(np.int32).reshape(624, 1).copy())
+    idx = torch.tensor([int(words[624])], dtype=torch.int32)
+    import_refstates(env, [st])
+    env.import_state(env.export_state(), mt, idx)
+    _, mt2, idx2 = env.export_state(with_mt=True)
+    assert (mt2.cpu().numpy().view(np.uint32)[:, 0] == words[:624]).all()
+    assert idx2.item() == int(words[624])
