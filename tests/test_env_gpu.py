@@ -139,26 +139,33 @@ def test_full_size_4096_vs_oracle(Env):
 
 
 def test_auto_reset_steady_state(Env):
-    """auto_reset: board b's second game is seeded seed_base + b + 2^32."""
-    n, base = 256, 31
+    """auto_reset: board b's k-th game is seeded seed_base + b + (k << 32)."""
+    n, base, plies = 256, 31, 150
     env = Env(n, seed_base=base, device=DEV)
     env.reset()
-    games, steps, _ = env.rollout(max_plies=150, auto_reset=True)
+    games, steps, _ = env.rollout(max_plies=plies, auto_reset=True)
     st = states_of(env)
-    g0 = oracle.play_rule_games(n, base)[2]
+    g = games.cpu().numpy()
     for b in range(0, n, 17):
-        m = oracle.mt_seed(base + b + (1 << 32))
-        s = oracle.reset(m)
-        seed = base + b + (1 << 32)
-        for ply in range(150 - int(g0[b])):
-            if oracle.is_game_over(s):
-                break
-            mask = oracle.legal(s)
-            L = int(mask.sum())
-            a = np.flatnonzero(mask)[((oracle.rule(seed, ply) >> 32) * L) >> 32]
-            s = oracle.step(s, int(a), m)[1]
+        left, e, done_games = plies, 0, 0
+        s = None
+        while left > 0:
+            seed = base + b + (e << 32)
+            m = oracle.mt_seed(seed)
+            s = oracle.reset(m)
+            ply = 0
+            while left > 0 and not oracle.is_game_over(s):
+                mask = oracle.legal(s)
+                L = int(mask.sum())
+                a = np.flatnonzero(mask)[((oracle.rule(seed, ply) >> 32) * L) >> 32]
+                s = oracle.step(s, int(a), m)[1]
+                ply += 1
+                left -= 1
+            done_games += int(oracle.is_game_over(s))
+            e += 1
         assert (st[b] == s).all(), b
-    assert (games.cpu().numpy() >= 1).all()
+        assert g[b] == done_games
+    assert (steps.cpu().numpy() == plies).all()
 
 
 def test_scoring_known_answers(Env):
