@@ -1,0 +1,232 @@
+"""Benchmark: BASELINE config 2 — 4096 concurrent boards per GPU, pure env
+step / legal_actions / score HIP kernels, bit-exact vs the CPU engine.
+
+One bench step = one batched pass of the env hot path over 4096 boards:
+hz_reset (HarmoniesGameState() x 4096, CPython-exact seeding) followed by
+hz_rollout, which plays every board to its end (legal mask -> build-defined
+splitmix rule pick -> apply_move, incl. chance draws and final scoring).
+Boards are seeded by their global id (rank * 4096 + b), so N GPUs run N
+independent shards (weak scaling, no data-path collective).
+
+Prints one JSON line (rank 0).  Usage:
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--boards 4096]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "harmonies-alphazero_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# SURVEY.md §8(d) algorithmic bytes per unit
+BYTES_PER_ENV_STEP = 152   # 64 B state read + 64 B state write + 18 B mask + ~6 B RNG
+BYTES_PER_RESET = 2564     # 624x4 B MT init + idx + 64 B state
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+MAX_PLIES = 96             # rule games end after 56-72 plies
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--boards", type=int, default=4096)
+    ap.add_argument("--seed-base", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--api-mode", action="store_true",
+                    help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(boards, seconds):
+    """The C oracle (oracle/hz_oracle.c, the bit-exact CPU port of the
+    reference engine) playing the same rule-driven 4096-board batches on the
+    host cores, for a bounded wall time."""
+    import oracle
+    nthreads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    oracle.play_rule_games(64, 10**9, nthreads=nthreads)  # warm the library / threads
+    steps = games = 0
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        total, _, _, _ = oracle.play_rule_games(boards, 10**9 + k * boards, nthreads=nthreads)
+        steps += total
+        games += boards
+        k += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
+            "games_per_s": games / dt,
+            "sample": f"{k} batches x {boards} rule-driven games ({steps} env steps) in {dt:.1f}s, "
+                      f"C oracle with OpenMP, {nthreads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from hzamd.env import BatchedEnv
+
+    n = args.boards
+    env = BatchedEnv(n, seed_base=args.seed_base + rank * n, device=dev)
+    games = torch.zeros(n, dtype=torch.int32, device=dev)
+    steps = torch.zeros(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def one_step(ev=None):
+        env.reset()
+        if ev:
+            ev[0].record(stream)
+        env.rollout(MAX_PLIES, games_done=games, steps_done=steps)
+        if ev:
+            ev[1].record(stream)
+
+    # first batch (episode 0: board b seeded seed_base + rank*n + b) doubles as
+    # the parity guard: its env-step count must equal the C oracle's
+    one_step()
+    torch.cuda.synchronize(dev)
+    first_steps = int(steps.sum().item())
+    for _ in range(max(0, args.warmup - 1)):
+        one_step()
+    torch.cuda.synchronize(dev)
+    env_steps_per_step = int(steps.sum().item())
+    games_per_step = int(games.sum().item())
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        c = torch.tensor([env_steps_per_step, games_per_step], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        env_steps_all, games_all = int(c[0]), int(c[1])
+    else:
+        env_steps_all, games_all = env_steps_per_step, games_per_step
+
+    value = env_steps_all * args.steps / elapsed
+    games_per_s = games_all * args.steps / elapsed
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    # roofline of the dominant kernel (hz_rollout / k_rollout), per launch
+    alg_bytes = env_steps_per_step * BYTES_PER_ENV_STEP
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("k_rollout_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    api = None
+    if args.api_mode and rank == 0:
+        api = api_mode(env, dev, stream)
+
+    if rank == 0:
+        import oracle  # test infrastructure: parity guard + cpu_baseline only
+        ref_total = oracle.play_rule_games(n, args.seed_base, nthreads=8)[0]
+        assert ref_total == first_steps, (ref_total, first_steps)
+        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(n, args.cpu_seconds)
+        out = {
+            "metric": "self-play env-steps/sec + games/sec @4096 boards, 1/2/4/8 GPUs; bit-exact vs CPU",
+            "value": value,
+            "unit": "env-steps/s",
+            "games_per_s": games_per_s,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: CPython-seeded games, seeds = global board id, build-defined splitmix rule policy",
+            "config": {"workload": "config2: 4096 concurrent boards/GPU, reset + rule-driven play to game end "
+                                   "(legal mask, step, chance draws, final scoring), fused hz_rollout",
+                       "boards_per_gpu": n, "env_steps_per_step": env_steps_per_step,
+                       "games_per_step": games_per_step, "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_rollout", "kernel_ms": kern_ms,
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "parity": f"first batch: {first_steps} env steps == C oracle ({ref_total})",
+        }
+        if api:
+            out["api_path"] = api
+        print(json.dumps(out))
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def api_mode(env, dev, stream, plies=MAX_PLIES, reps=5):
+    """Unfused path: per ply hz_legal_mask + hz_rule_actions + hz_step
+    (3 launches), then hz_score — captured once into a HIP graph."""
+    n = env.n
+    mask = torch.zeros(n, 3, dtype=torch.int64, device=dev)
+    count = torch.zeros(n, dtype=torch.int32, device=dev)
+    act = torch.zeros(n, dtype=torch.int16, device=dev)
+    status = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def body():
+        env.reset()
+        for _ in range(plies):
+            env.legal_mask(mask, count)
+            env.rule_actions(mask, count, act)
+            env.step(act, status)
+        env.score()
+
+    body()
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            body()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    return {"ms_per_batch": dt * 1e3, "launches_per_batch": 3 * plies + 2,
+            "note": "graph-captured per-ply launches over a 4096-board batch", "boards": n}
+
+
+if __name__ == "__main__":
+    main()
