@@ -269,12 +269,15 @@ __device__ __forceinline__ int score_player(const State& s, int p) {
 }
 
 // ------------------------------------------------------------------ MT19937
-struct MTRef {
-  uint32_t* mt;   // [624][N]
-  int32_t* pos;   // [N]
-  int n, b;
-  __device__ __forceinline__ uint32_t& w(int i) const { return mt[(size_t)i * n + b]; }
-};
+// A board's stream: 624 words at w[0..623] (board-major in HBM, or an LDS
+// copy) and a cursor packed as pos | tw << 16:
+//   pos = outputs consumed in the current generation (CPython's index),
+//   tw  = words of the current generation already twisted in place.
+// CPython twists all 624 words when index reaches N; we twist 8 at a time,
+// on demand, in one memory round trip per block.  The outputs are identical;
+// hz_mt_normalize finishes the twist (tw = 624) to recover CPython's state.
+constexpr int kMT = 624;
+constexpr int kMTSeeded = 624 | (624 << 16);  // CPython state right after seed()
 
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
   y ^= (y >> 11);
@@ -289,91 +292,126 @@ __device__ __forceinline__ uint32_t twist_word(uint32_t cur, uint32_t next, uint
   return far ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
 }
 
+template <int S>
+struct MTS {
+  uint32_t* w;  // word i at w[i * S]
+  int pos, tw;
+
+  __device__ __forceinline__ MTS(uint32_t* words, int cursor) : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
+  __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
+
+  // twist words [tw, tw + k), k <= 8: every source word is either already
+  // new (index < tw) or still old (index >= tw + k), so all 17 loads issue
+  // together.
+  __device__ __forceinline__ void advance() {
+    int k = kMT - tw < 8 ? kMT - tw : 8;
+    uint32_t cur[9], far[8];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      int i = tw + j;
+      cur[j] = (j <= k) ? w[(i < kMT ? i : 0) * S] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      int i = tw + j;
+      int fi = i < 227 ? i + 397 : (i < 623 ? i - 227 : 396);
+      far[j] = (j < k) ? w[fi * S] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (j < k) w[(tw + j) * S] = twist_word(cur[j], cur[j + 1], far[j]);
+    }
+    tw += k;
+  }
+
+  // genrand_uint32
+  __device__ __forceinline__ uint32_t next() {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    if (pos >= tw) advance();
+    return temper(w[(pos++) * S]);
+  }
+
+  // finish the current generation's twist (CPython form afterwards)
+  __device__ __forceinline__ void normalize() {
+    if (pos >= kMT) return;
+    while (tw < kMT) advance();
+  }
+};
+using MT = MTS<1>;
+
 // random.seed(int) for 0 <= seed < 2^64 (_randommodule.c random_seed +
-// init_by_array).  init_genrand(19650218) is regenerated on the fly.  The
-// caller sets its cursor to 624 (CPython: index = N after seeding).
-__device__ __forceinline__ void mt_seed(const MTRef& m, uint64_t seed) {
+// init_by_array) into w[i * stride]; init_genrand(19650218) is regenerated on
+// the fly.  The stream's cursor afterwards is kMTSeeded.
+__device__ __forceinline__ void mt_seed(uint32_t* w, int stride, uint64_t seed) {
   uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   int klen = key1 ? 2 : 1;
   uint32_t init = 19650218U;  // init_genrand word i, generated in order
   uint32_t prev = init;       // mt[i-1]
-  uint32_t mt0 = init;
   int j = 0;
   // first pass: i = 1..623, then mt[0] = mt[623] and one more step at i = 1
-  for (int i = 1; i < 624; i++) {
+  for (int i = 1; i < kMT; i++) {
     init = 1812433253U * (init ^ (init >> 30)) + (uint32_t)i;
     uint32_t v = (init ^ ((prev ^ (prev >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
-    m.w(i) = v;
+    w[i * stride] = v;
     prev = v;
     if (++j >= klen) j = 0;
   }
-  mt0 = prev;
-  {
-    uint32_t v = (m.w(1) ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
-    m.w(1) = v;
+  uint32_t mt0 = prev;
+  uint32_t nxt = w[1 * stride];
+  prev = (nxt ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
+  w[1 * stride] = prev;
+  // second pass: 623 steps starting at i = 2 (next word preloaded)
+  nxt = w[2 * stride];
+  for (int i = 2; i < kMT; i++) {
+    uint32_t after = i + 1 < kMT ? w[(i + 1) * stride] : 0u;
+    uint32_t v = (nxt ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    w[i * stride] = v;
     prev = v;
-  }
-  // second pass: 623 steps starting at i = 2
-  for (int i = 2; i < 624; i++) {
-    uint32_t v = (m.w(i) ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
-    m.w(i) = v;
-    prev = v;
+    nxt = after;
   }
   mt0 = prev;  // mt[0] = mt[623]
-  {
-    uint32_t v = (m.w(1) ^ ((mt0 ^ (mt0 >> 30)) * 1566083941U)) - 1U;
-    m.w(1) = v;
-  }
-  m.w(0) = 0x80000000U;
+  w[1 * stride] = (w[1 * stride] ^ ((mt0 ^ (mt0 >> 30)) * 1566083941U)) - 1U;
+  w[0] = 0x80000000U;
 }
 
-// genrand_uint32 with a lazy one-word twist.
-__device__ __forceinline__ uint32_t mt_next(const MTRef& m, int& pos) {
-  if (pos >= 1248) pos = 624;
-  if (pos < 624) return temper(m.w(pos++));
-  int i = pos - 624;
-  uint32_t nw;
-  if (i < 227) nw = twist_word(m.w(i), m.w(i + 1), m.w(i + 397));
-  else if (i < 623) nw = twist_word(m.w(i), m.w(i + 1), m.w(i - 227));
-  else nw = twist_word(m.w(623), m.w(0), m.w(396));
-  m.w(i) = nw;
-  pos++;
-  return temper(nw);
-}
-
-__device__ __forceinline__ uint32_t randbelow(const MTRef& m, int& pos, uint32_t n) {
+template <class M>
+__device__ __forceinline__ uint32_t randbelow(M& m, uint32_t n) {
   if (!n) return 0;
   int k = 32 - __clz(n);
-  uint32_t r = mt_next(m, pos) >> (32 - k);
-  while (r >= n) r = mt_next(m, pos) >> (32 - k);
+  uint32_t r = m.next() >> (32 - k);
+  while (r >= n) r = m.next() >> (32 - k);
   return r;
 }
 
 // random.sample(range(n), k), k <= 3 (so setsize = 21, random.py:484-486).
-__device__ __forceinline__ void sample3(const MTRef& m, int& pos, uint32_t n, int k, uint32_t out[3]) {
+template <class M>
+__device__ __forceinline__ void sample3(M& m, uint32_t n, int k, uint32_t out[3]) {
   if (n <= 21) {
     // pool method; pool[x] == x except at <= 3 recorded positions
-    uint32_t mp[3], mv[3];
-    int nm = 0;
-    for (int i = 0; i < k; i++) {
-      uint32_t j = randbelow(m, pos, n - (uint32_t)i);
+    uint32_t mp[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mv[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (i >= k) break;
+      uint32_t j = randbelow(m, n - (uint32_t)i);
       uint32_t last = n - (uint32_t)i - 1;
       uint32_t vj = j, vl = last;
-      for (int q = 0; q < nm; q++) {
-        if (mp[q] == j) vj = mv[q];
-        if (mp[q] == last) vl = mv[q];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        if (q < i && mp[q] == j) vj = mv[q];
+        if (q < i && mp[q] == last) vl = mv[q];
       }
       out[i] = vj;
-      mp[nm] = j;
-      mv[nm] = vl;
-      nm++;
+      mp[i] = j;
+      mv[i] = vl;
     }
   } else {
-    for (int i = 0; i < k; i++) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (i >= k) break;
       uint32_t j;
       bool dup;
       do {
-        j = randbelow(m, pos, n);
+        j = randbelow(m, n);
         dup = (i > 0 && out[0] == j) || (i > 1 && out[1] == j);
       } while (dup);
       out[i] = j;
@@ -383,8 +421,10 @@ __device__ __forceinline__ void sample3(const MTRef& m, int& pos, uint32_t n, in
 
 // _draw_tiles(3) (harmonies_engine.py:120-130): flat_bag follows the bag's
 // insertion order water, plant, wood, stone, field, building (constants.py:41).
-// Returns the pile as 3x3 bits (7 = none) and the number of tiles drawn.
-__device__ __forceinline__ int draw_pile(uint64_t& misc, const MTRef& m, int& pos, uint32_t& pile9) {
+// Produces the pile as 3x3 bits (7 = none); returns the number of tiles drawn.
+// The bag itself is decremented by the caller (apply_pile).
+template <class M>
+__device__ __forceinline__ int draw_pile(uint64_t misc, M& m, uint32_t& pile9) {
   int cnt[6];
 #pragma unroll
   for (int t = 0; t < 6; t++) cnt[t] = bag_n(misc, t);
@@ -394,11 +434,12 @@ __device__ __forceinline__ int draw_pile(uint64_t& misc, const MTRef& m, int& po
   pile9 = 0x1FF;
   if (!n) return 0;
   int k = n < 3 ? (int)n : 3;
-  uint32_t idx[3];
-  sample3(m, pos, n, k, idx);
+  uint32_t idx[3] = {0, 0, 0};
+  sample3(m, n, k, idx);
   const int order[6] = {WATER, PLANT, WOOD, STONE, FIELD, BUILDING};
-  int drawn[3];
-  for (int i = 0; i < k; i++) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (i >= k) break;
     uint32_t rem = idx[i];
     int tile = -1;
 #pragma unroll
@@ -409,40 +450,71 @@ __device__ __forceinline__ int draw_pile(uint64_t& misc, const MTRef& m, int& po
         else rem -= (uint32_t)cnt[tt];
       }
     }
-    drawn[i] = tile;
-  }
-  // indices map against the pre-draw bag, then every drawn tile decrements
-  // the bag (:126-129)
-  for (int i = 0; i < k; i++) {
-    int t = drawn[i];
-    misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)(bag_n(misc, t) - 1));
-    pile9 = (pile9 & ~(7u << (3 * i))) | ((uint32_t)t << (3 * i));
+    pile9 = (pile9 & ~(7u << (3 * i))) | ((uint32_t)tile << (3 * i));
   }
   return k;
 }
 
-// _replenish_piles (:132-137)
-__device__ __forceinline__ void replenish(State& s, const MTRef& m, int& pos) {
-  int np = npiles_of(s.piles);
-  while (np < 5) {
-    uint32_t pile9;
-    int k = draw_pile(s.misc, m, pos, pile9);
-    if (!k) break;
-    s.piles = set_bits(s.piles, 9 * np, 9, pile9);
-    np++;
-    s.piles = set_bits(s.piles, 45, 3, (uint64_t)np);
+// Every drawn tile decrements the bag (:126-129).
+__device__ __forceinline__ void apply_pile(uint64_t& misc, uint32_t pile9) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    int t = (int)((pile9 >> (3 * i)) & 7);
+    if (t != 7) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)(bag_n(misc, t) - 1));
   }
 }
 
+// Sources of piles for _replenish_piles: the live stream ...
+template <class M>
+struct StreamDraw {
+  M& m;
+  __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
+    uint32_t p9;
+    return draw_pile(misc, m, p9) ? p9 : 0x1FFu;
+  }
+};
+// ... or a recorded script of up to 5 piles (9 bits each, 0x1FF = stop),
+// used when an MCTS expansion replays the draws its children made in the
+// reference's child order.
+struct ScriptDraw {
+  uint64_t script;
+  __device__ __forceinline__ uint32_t operator()(uint64_t) {
+    uint32_t p9 = (uint32_t)(script & 0x1FF);
+    script = (script >> 9) | (0x1FFull << 36);
+    return p9;
+  }
+};
+
+// _replenish_piles (:132-137); returns the piles drawn as a script.
+template <class Draw>
+__device__ __forceinline__ uint64_t replenish(State& s, Draw& draw) {
+  int np = npiles_of(s.piles);
+  uint64_t script = (1ull << 45) - 1;
+  int d = 0;
+  while (np < 5) {
+    uint32_t pile9 = draw(s.misc);
+    if (pile9 == 0x1FFu) break;
+    apply_pile(s.misc, pile9);
+    s.piles = set_bits(s.piles, 9 * np, 9, pile9);
+    script = set_bits(script, 9 * d, 9, pile9);
+    np++;
+    d++;
+    s.piles = set_bits(s.piles, 45, 3, (uint64_t)np);
+  }
+  return script;
+}
+
 // HarmoniesGameState.__init__ (:66-79)
-__device__ __forceinline__ void reset_state(State& s, const MTRef& m, int& pos) {
+template <class M>
+__device__ __forceinline__ void reset_state(State& s, M& m) {
   s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
   s.piles = (1ull << 45) - 1;  // every tile slot = 7 (none), 0 piles
-  uint64_t misc = 0x1FF;  // empty hand
+  uint64_t misc = 0x1FF;        // empty hand
 #pragma unroll
   for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
   s.misc = misc;  // player 0, choose_pile, not over, winner None, scores 0
-  replenish(s, m, pos);
+  StreamDraw<M> d{m};
+  replenish(s, d);
 }
 
 // ------------------------------------------------------------- legal mask
@@ -520,14 +592,15 @@ __device__ __forceinline__ void finish_game(State& s) {  // :344-354
   s.misc = m;
 }
 
-__device__ __forceinline__ void end_turn(State& s, const MTRef& mt, int& pos) {  // :301-329
+template <class Draw>
+__device__ __forceinline__ void end_turn(State& s, Draw& draw) {  // :301-329
   int p = player_of(s.misc);
   uint32_t b[4];
   planes_of(s, p, b);
   int filled = __popc(b[0] | b[1] | b[2] | b[3]);
   bool player_trigger = (kCells - filled) <= 2;
   bool bag_empty_before = bag_total(s.misc) == 0;
-  replenish(s, mt, pos);
+  replenish(s, draw);
   bool bag_trigger = bag_empty_before && npiles_of(s.piles) == 0;
   bool end = player_trigger || bag_trigger;
   if (end && !over_flag(s.misc)) {
@@ -547,7 +620,8 @@ __device__ __forceinline__ void end_turn(State& s, const MTRef& mt, int& pos) { 
 }
 
 // apply_move (:210-298) in place; returns a status (state untouched unless OK).
-__device__ __forceinline__ int step_state(State& s, int a, const MTRef& mt, int& pos) {
+template <class Draw>
+__device__ __forceinline__ int step_state(State& s, int a, Draw& draw) {
   if (a < 0 || a >= kActions) return ST_BAD_ACTION;
   int ph = phase_of(s.misc);
   if (ph == PH_CHOOSE) {
@@ -584,10 +658,112 @@ __device__ __forceinline__ int step_state(State& s, int a, const MTRef& mt, int&
     s.misc = set_bits(m, 9, 2, (uint64_t)(nh - 1));
     set_code(s, p, c, nc);
     if (ph < PH_P3) s.misc = set_bits(s.misc, 42, 3, (uint64_t)(ph + 1));
-    else end_turn(s, mt, pos);
+    else end_turn(s, draw);
     return ST_OK;
   }
   return ST_BAD_PHASE;
+}
+
+// ------------------------------------------------------- transposition key
+// MCTS.py keys its DAG by hash(state) (MCTS.py:14,177,185) of
+// get_canonical_tuple() (harmonies_engine.py:81-110).  Because CPython hashes
+// the int -1 like -2, two canonical tuples collide exactly when they agree
+// after mapping every axial coordinate component -1 to -2, with board items
+// still listed in sorted real-coordinate order.  The key below encodes that
+// equivalence exactly (pyhash = true); pyhash = false gives the true
+// canonical tuple.
+//   w0: player | phase<<1 | #hand<<4 | sorted hand<<6 | #piles<<15 | bag<<18
+//   w1: the piles in order, each sorted (5 x 9 bits)
+//   w2..w4 / w5..w7: player 0 / 1 board: one byte (class << 4 | stack code)
+//   per occupied cell in cell order (pyhash), or 23 stack-code nibbles.
+struct CKey {
+  uint64_t w[8];
+};
+
+// cell -> coordinate class under (-1 -> -2): {1,6} {2,7} {3,8} {4,5} {9,10}
+// {14,15} {19,20} collide; classes numbered 0..15 in order of first cell.
+constexpr int kHashClass[23] = {0, 1, 2, 3, 4, 4, 1, 2, 3, 5, 5, 6, 7, 8, 9, 9, 10, 11, 12, 13, 13, 14, 15};
+__host__ __device__ constexpr uint64_t pack_class(int lo) {
+  uint64_t r = 0;
+  for (int c = lo; c < 23 && c < lo + 16; c++) r |= (uint64_t)kHashClass[c] << (4 * (c - lo));
+  return r;
+}
+constexpr uint64_t kClassLo = pack_class(0), kClassHi = pack_class(16);
+
+__device__ __forceinline__ void sort3(uint32_t& a, uint32_t& b, uint32_t& c) {
+  uint32_t t;
+  if (b < a) { t = a; a = b; b = t; }
+  if (c < b) { t = b; b = c; c = t; }
+  if (b < a) { t = a; a = b; b = t; }
+}
+
+__device__ __forceinline__ uint32_t sorted9(uint32_t v9) {
+  uint32_t a = v9 & 7, b = (v9 >> 3) & 7, c = (v9 >> 6) & 7;
+  sort3(a, b, c);
+  return a | (b << 3) | (c << 6);
+}
+
+__device__ __forceinline__ CKey canon_key(const State& s, bool pyhash) {
+  CKey k;
+  uint64_t m = s.misc;
+  k.w[0] = (uint64_t)player_of(m) | ((uint64_t)phase_of(m) << 1) | ((uint64_t)hand_n(m) << 4) |
+           ((uint64_t)sorted9((uint32_t)(m & 0x1FF)) << 6) | ((uint64_t)npiles_of(s.piles) << 15) |
+           (((m >> 11) & ((1ull << 30) - 1)) << 18);
+  uint64_t pw = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) pw |= (uint64_t)sorted9((uint32_t)(s.piles >> (9 * i)) & 0x1FF) << (9 * i);
+  k.w[1] = pw;
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    uint64_t a0 = 0, a1 = 0, a2 = 0;
+    if (pyhash) {
+      int cnt = 0;
+#pragma unroll
+      for (int c = 0; c < 23; c++) {
+        int code = code_at(s, p, c);
+        uint64_t cls = c < 16 ? (kClassLo >> (4 * c)) & 15 : (kClassHi >> (4 * (c - 16))) & 15;
+        uint64_t byte = (cls << 4) | (uint64_t)code;
+        int sh = (cnt & 7) * 8;
+        if (code) {
+          if (cnt < 8) a0 |= byte << sh;
+          else if (cnt < 16) a1 |= byte << sh;
+          else a2 |= byte << sh;
+          cnt++;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 23; c++) {
+        uint64_t code = (uint64_t)code_at(s, p, c);
+        if (c < 16) a0 |= code << (4 * c);
+        else a1 |= code << (4 * (c - 16));
+      }
+    }
+    k.w[2 + 3 * p] = a0;
+    k.w[3 + 3 * p] = a1;
+    k.w[4 + 3 * p] = a2;
+  }
+  return k;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t key_hash(const CKey& k) {
+  uint64_t h = 0x243F6A8885A308D3ULL;
+#pragma unroll
+  for (int i = 0; i < 8; i++) h = mix64(h ^ (k.w[i] + 0x9E3779B97F4A7C15ULL * (uint64_t)(i + 1)));
+  return h;
+}
+
+__device__ __forceinline__ bool key_eq(const CKey& a, const CKey& b) {
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq = eq && (a.w[i] == b.w[i]);
+  return eq;
 }
 
 // ------------------------------------------------------------ action rule

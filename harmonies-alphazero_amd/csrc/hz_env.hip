@@ -11,6 +11,7 @@
 
 #include "../../include/hz_abi.h"
 #include "hz_device.hpp"
+#include "hz_encode.hpp"
 
 using namespace hz;
 
@@ -19,8 +20,8 @@ struct hz_env {
   uint64_t seed_base;
   hipStream_t stream;
   uint64_t *state;   // [6][n]
-  uint32_t *mt;      // [624][n]
-  int32_t *pos;      // [n]
+  uint32_t *mt;      // [n][624] board-major MT19937 words
+  int32_t *pos;      // [n] MT cursor (pos | tw << 16, see hz_device.hpp)
   int32_t *ply;      // [n]
   int32_t *episode;  // [n]
   uint64_t *seed;    // [n]
@@ -33,31 +34,50 @@ constexpr int kBlock = 64;  // one wave per workgroup: 4096 boards -> 64 waves
 inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 
 // ------------------------------------------------------------------ reset
+// Lane-per-board with the 64 boards' MT arrays staged in LDS as [624][65]
+// words (stride 65: the per-lane seeding writes and the board-major write-out
+// reads are both bank-conflict free).  Seeding (two serial 623-step passes)
+// and the 15 opening draws run at LDS latency; one coalesced pass then writes
+// the block's contiguous 64 x 2,496 B of HBM.
+constexpr int kLdsStride = 65;
+constexpr size_t kResetLds = (size_t)kMT * kLdsStride * sizeof(uint32_t);  // 162,240 B
+
 __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                   int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                   int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
                                                   int n, uint64_t seed_base, const uint8_t *__restrict__ sel,
                                                   const uint64_t *__restrict__ seeds) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  if (sel && !sel[b]) return;
-  uint64_t sd;
-  if (seeds) {
-    sd = seeds[b];
-  } else {
-    int e = episode[b];
-    sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
-    episode[b] = e + 1;
+  extern __shared__ uint32_t lds[];
+  int lane = threadIdx.x;
+  int b0 = blockIdx.x * kBlock;
+  int b = b0 + lane;
+  bool act = b < n && (!sel || sel[b]);
+  if (act) {
+    uint64_t sd;
+    if (seeds) {
+      sd = seeds[b];
+    } else {
+      int e = episode[b];
+      sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+      episode[b] = e + 1;
+    }
+    mt_seed(lds + lane, kLdsStride, sd);
+    MTS<kLdsStride> m(lds + lane, kMTSeeded);
+    State s;
+    reset_state(s, m);
+    store_state(st, n, b, s);
+    pos[b] = m.cursor();
+    ply[b] = 0;
+    seed[b] = sd;
   }
-  MTRef m{mt, pos, n, b};
-  mt_seed(m, sd);
-  int p = 624;
-  State s;
-  reset_state(s, m, p);
-  store_state(st, n, b, s);
-  pos[b] = p;
-  ply[b] = 0;
-  seed[b] = sd;
+  uint64_t actmask = __ballot(act);
+  __syncthreads();
+  int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  uint32_t *g = mt + (size_t)b0 * kMT;
+  for (int o = lane; o < nb * kMT; o += kBlock) {
+    int bl = o / kMT, i = o - bl * kMT;
+    if ((actmask >> bl) & 1) g[o] = lds[i * kLdsStride + bl];
+  }
 }
 
 // ------------------------------------------------------------- legal mask
@@ -87,12 +107,12 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
     return;
   }
   State s = load_state(st, n, b);
-  MTRef m{mt, pos, n, b};
-  int p = pos[b];
-  int r = step_state(s, a, m, p);
+  MT m(mt + (size_t)b * kMT, pos[b]);
+  StreamDraw<MT> d{m};
+  int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
-    pos[b] = p;
+    pos[b] = m.cursor();
     ply[b] += 1;
   }
   if (status) status[b] = r;
@@ -137,9 +157,10 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
                                                     int32_t *__restrict__ steps_done) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
-  MTRef m{mt, pos, n, b};
+  MT m(mt + (size_t)b * kMT, pos[b]);
+  StreamDraw<MT> draw{m};
   State s = load_state(st, n, b);
-  int p = pos[b], g_ply = ply[b], games = 0, steps = 0;
+  int g_ply = ply[b], games = 0, steps = 0;
   uint64_t sd = seed[b];
   for (int i = 0; i < max_plies; i++) {
     if (game_done(s.misc)) {
@@ -152,9 +173,10 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
       int e = episode[b];
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       episode[b] = e + 1;
-      mt_seed(m, sd);
-      p = 624;
-      reset_state(s, m, p);
+      mt_seed(m.w, 1, sd);
+      m.pos = kMT;
+      m.tw = kMT;
+      reset_state(s, m);
       g_ply = 0;
     }
     uint64_t mk[3];
@@ -174,126 +196,35 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
     }
     int a = kth_action(mk, rule_pick(sd, g_ply, L));
     if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
-    step_state(s, a, m, p);
+    step_state(s, a, draw);
     g_ply++;
     steps++;
     if (game_done(s.misc)) games++;
   }
   store_state(st, n, b, s);
-  pos[b] = p;
+  pos[b] = m.cursor();
   ply[b] = g_ply;
   seed[b] = sd;
   if (games_done) games_done[b] = games;
   if (steps_done) steps_done[b] = steps;
 }
 
-// ----------------------------------------------------------------- encode
-// Column-major (x-major) valid-cell mask: sorted(VALID_HEXES) order is
-// (q, r) lexicographic = column-major over the 5x7 grid, so a cell's index is
-// the number of valid cells before it in this order.
-__host__ __device__ constexpr uint64_t valid_cm() {
-  uint64_t v = 0;
-  for (int c = 0; c < 23; c++) {
-    int g = grid_bit(c);
-    int y = g / 7, x = g % 7;
-    v |= 1ull << (x * 5 + y);
-  }
-  return v;
-}
-constexpr uint64_t kValidCM = valid_cm();
-
-__global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, int n,
-                                                      const int32_t *__restrict__ idx, int m,
-                                                      float *__restrict__ board) {
-  // one thread per float2 of the [m][38][5][7] output (1330 floats / board)
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t total = (size_t)m * 665;
-  if (i >= total) return;
-  int j = (int)(i / 665);
-  int e0 = (int)(i - (size_t)j * 665) * 2;
-  int b = idx ? idx[j] : j;
-  float v[2];
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    int e = e0 + q;
-    int ch = e / 35, yx = e - ch * 35;
-    int y = yx / 7, x = yx - y * 7;
-    int cm = x * 5 + y;
-    float val = 0.f;
-    if ((kValidCM >> cm) & 1) {
-      int cell = __popcll(kValidCM & ((1ull << cm) - 1));
-      if (ch < 36) {
-        int p = ch >= 18 ? 1 : 0;
-        int r = ch - 18 * p;
-        int t = r / 3, sp = r - 3 * t;
-        int sh = 32 * p + cell;
-        int code = (int)(((st[b] >> sh) & 1) | (((st[(size_t)n + b] >> sh) & 1) << 1) |
-                         (((st[(size_t)2 * n + b] >> sh) & 1) << 2) | (((st[(size_t)3 * n + b] >> sh) & 1) << 3));
-        val = tile_at(code, sp) == t ? 1.f : 0.f;
-      } else {
-        uint64_t misc = st[(size_t)5 * n + b];
-        if (ch == 36) {
-          val = (float)player_of(misc);
-        } else {
-          int ph = phase_of(misc);
-          val = ph <= PH_P3 ? (float)((double)ph / 3.0) : 0.f;
-        }
-      }
-    }
-    v[q] = val;
-  }
-  reinterpret_cast<float2 *>(board)[i] = make_float2(v[0], v[1]);
-}
-
-__global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict__ st, int n,
-                                                     const int32_t *__restrict__ idx, int m,
-                                                     float *__restrict__ glob) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m * 42) return;
-  int j = i / 42, f = i - j * 42;
-  int b = idx ? idx[j] : j;
-  uint64_t misc = st[(size_t)5 * n + b];
-  float val = 0.f;
-  if (f < 30) {
-    uint64_t piles = st[(size_t)4 * n + b];
-    int pi = f / 6, t = f - pi * 6;
-    if (pi < npiles_of(piles)) {
-      int cnt = (pile_tile(piles, pi, 0) == t) + (pile_tile(piles, pi, 1) == t) + (pile_tile(piles, pi, 2) == t);
-      val = (float)((double)cnt / 3.0);
-    }
-  } else if (f < 36) {
-    int t = f - 30, nh = hand_n(misc), cnt = 0;
-    for (int q = 0; q < nh; q++) cnt += hand_tile(misc, q) == t;
-    val = (float)((double)cnt / 3.0);
-  } else {
-    int t = f - 36;
-    val = (float)((double)bag_n(misc, t) / (double)initial_count(t));
-  }
-  glob[i] = val;
-}
-
 // ---------------------------------------------------------- state transfer
 __global__ void __launch_bounds__(kBlock) k_mt_normalize(uint32_t *__restrict__ mt, int32_t *__restrict__ pos,
-                                                         int n) {
+                                                         int n, int32_t *__restrict__ index) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
-  int p = pos[b];
-  if (p >= 1248) p = 624;
-  pos[b] = p;
-  // p < 624: already CPython form.  p == 624: CPython's "index = N" (the next
-  // call twists), identical representation.
-  if (p <= 624) return;
-  MTRef m{mt, pos, n, b};
-  int start = p - 624;
-  for (int i = start; i < 624; i++) {
-    uint32_t nw;
-    if (i < 227) nw = twist_word(m.w(i), m.w(i + 1), m.w(i + 397));
-    else if (i < 623) nw = twist_word(m.w(i), m.w(i + 1), m.w(i - 227));
-    else nw = twist_word(m.w(623), m.w(0), m.w(396));
-    m.w(i) = nw;
-  }
-  // all 624 words are now the current generation, as after CPython's twist
-  pos[b] = start;
+  MT m(mt + (size_t)b * kMT, pos[b]);
+  m.normalize();
+  pos[b] = m.cursor();
+  if (index) index[b] = m.pos;
+}
+
+__global__ void __launch_bounds__(kBlock) k_mt_import(int32_t *__restrict__ pos, int n,
+                                                      const int32_t *__restrict__ index) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  pos[b] = index[b] | (kMT << 16);  // CPython states are fully twisted
 }
 
 inline int launch_err() {
@@ -314,6 +245,12 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   e->seed_base = seed_base;
   e->stream = (hipStream_t)stream;
   size_t n = (size_t)n_boards;
+  // k_reset stages 64 boards' MT words in 158 KiB of LDS
+  if (hipFuncSetAttribute((const void *)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
+      hipSuccess) {
+    free(e);
+    return nullptr;
+  }
   bool ok = hipMalloc(&e->state, n * 6 * sizeof(uint64_t)) == hipSuccess &&
             hipMalloc(&e->mt, n * 624 * sizeof(uint32_t)) == hipSuccess &&
             hipMalloc(&e->pos, n * sizeof(int32_t)) == hipSuccess &&
@@ -361,7 +298,7 @@ uint64_t *hz_env_seed_ptr(hz_env *e) { return e ? e->seed : nullptr; }
 
 int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   if (!e) return -1;
-  hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos,
+  hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
   return launch_err();
 }
@@ -389,15 +326,7 @@ int hz_encode(hz_env *e, const int32_t *idx, int32_t m, float *board, float *glo
   if (!e || m < 0 || (!board && !glob)) return -1;
   if (!idx && m > e->n) return -2;
   if (m == 0) return 0;
-  if (board) {
-    size_t total = (size_t)m * 665;
-    hipLaunchKernelGGL(k_encode_board, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, e->state,
-                       e->n, idx, m, board);
-  }
-  if (glob) {
-    hipLaunchKernelGGL(k_encode_glob, dim3((unsigned)((m * 42 + 255) / 256)), dim3(256), 0, e->stream, e->state,
-                       e->n, idx, m, glob);
-  }
+  launch_encode(e->state, (long)e->n, 1, idx, m, board, glob, e->stream);
   return launch_err();
 }
 
@@ -421,14 +350,13 @@ int hz_export_state(hz_env *e, uint64_t *state, uint32_t *mt, int32_t *mt_index)
   if (!e) return -1;
   size_t n = (size_t)e->n;
   if (state && hipMemcpyAsync(state, e->state, n * 6 * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream))
-    return launch_err() ? launch_err() : 1;
+    return 1;
   if (mt || mt_index) {
-    hipLaunchKernelGGL(k_mt_normalize, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->mt, e->pos, e->n);
+    hipLaunchKernelGGL(k_mt_normalize, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->mt, e->pos, e->n,
+                       mt_index);
     int r = launch_err();
     if (r) return r;
-    if (mt && hipMemcpyAsync(mt, e->mt, n * 624 * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
-    if (mt_index && hipMemcpyAsync(mt_index, e->pos, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream))
-      return 1;
+    if (mt && hipMemcpyAsync(mt, e->mt, n * kMT * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
   }
   return 0;
 }
@@ -440,8 +368,9 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
   if (state && hipMemcpyAsync(e->state, state, n * 6 * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream))
     return 1;
   if (mt) {
-    if (hipMemcpyAsync(e->mt, mt, n * 624 * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
-    if (hipMemcpyAsync(e->pos, mt_index, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
+    if (hipMemcpyAsync(e->mt, mt, n * kMT * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
+    hipLaunchKernelGGL(k_mt_import, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->pos, e->n, mt_index);
+    return launch_err();
   }
   return 0;
 }

@@ -1,0 +1,510 @@
+// hz_mcts.hip — batched PUCT MCTS over the boards of an hz_env.
+//
+// Reference: MCTS.py (Node :8-20, Edge :23-39, move_to_leaf :63-149,
+// expand_leaf :151-218, back_fill :220-266, get_best_action_and_pi :272-441).
+// Every board runs its own single-tree search; all boards advance one
+// simulation per "sim step" in lock-step, so the leaf evaluations of all
+// boards form one PyTorch batch.  Boards are independent, so lock-stepping
+// preserves each board's sequential semantics exactly (no virtual loss).
+//
+// One wave (64 lanes) owns one board in every tree kernel: lanes are edges
+// in selection and backup, children in expansion.  Per board, in HBM:
+//   node pool  [max_nodes] : 48 B state, 64-bit key digest, first edge, #edges
+//   edge pool  [max_edges] : action, child node, N (int), W (f64), P (f32), player
+//   hash table [hcap] u64  : search generation << 32 | node id (linear probing;
+//                            entries of older searches read as empty, so the
+//                            table is never cleared)
+// Arithmetic follows the reference's NumPy/Python types exactly (see select
+// and expand) so that visit counts are bit-identical to the CPU engine.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "../../include/hz_abi.h"
+#include "hz_device.hpp"
+#include "hz_encode.hpp"
+
+using namespace hz;
+
+struct hz_env;  // defined in hz_env.hip; accessed through the ABI getters
+
+struct hz_mcts {
+  int32_t n, max_nodes, max_edges, hcap, max_depth;
+  int32_t exact_keys;
+  hipStream_t stream;
+  uint64_t *node_state;  // [n][max_nodes][6]
+  uint64_t *node_hash;   // [n][max_nodes]
+  int32_t *node_e0;      // [n][max_nodes]
+  int32_t *node_ne;      // [n][max_nodes]
+  int16_t *edge_action;  // [n][max_edges]
+  int32_t *edge_child;   // [n][max_edges]
+  int32_t *edge_n;       // [n][max_edges]
+  double *edge_w;        // [n][max_edges]
+  float *edge_p;         // [n][max_edges]
+  uint8_t *edge_player;  // [n][max_edges]
+  uint64_t *ht;          // [n][hcap]
+  int32_t *counts;       // [n][4]: nodes, edges, generation, overflow
+  int32_t *path;         // [n][max_depth]
+  int32_t *depth;        // [n]
+  int32_t *leaf;         // [n]  leaf node of the current simulation, -1 = inactive
+  int32_t *leaf_gidx;    // [n]  b*max_nodes + leaf for the encoder, -1 = no eval
+};
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kMaxChildren = 69;  // measured max legal moves
+constexpr int kChildSlots = 128;  // two per lane
+
+inline int launch_err() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+__device__ __forceinline__ uint64_t ht_entry(int gen, int node) {
+  return ((uint64_t)(uint32_t)gen << 32) | (uint32_t)node;
+}
+
+__device__ __forceinline__ State load_node(const uint64_t *ns) {
+  State s;
+#pragma unroll
+  for (int k = 0; k < 4; k++) s.pl[k] = ns[k];
+  s.piles = ns[4];
+  s.misc = ns[5];
+  return s;
+}
+
+__device__ __forceinline__ void store_node(uint64_t *ns, const State &s) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) ns[k] = s.pl[k];
+  ns[4] = s.piles;
+  ns[5] = s.misc;
+}
+
+// ------------------------------------------------------------------- begin
+// Fresh tree per move (MCTS.py:288-289): node 0 = the board's game state.
+__global__ void __launch_bounds__(kWave) k_begin(hz_mcts m, const uint64_t *__restrict__ game, int n_env,
+                                                 const uint8_t *__restrict__ active) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.n) return;
+  int32_t *cnt = m.counts + (size_t)b * 4;
+  bool act = !active || active[b];
+  if (!act) {
+    m.leaf[b] = -1;
+    m.leaf_gidx[b] = -1;
+    cnt[0] = 0;
+    cnt[1] = 0;
+    return;
+  }
+  State s = load_state(game, n_env, b);
+  size_t nb = (size_t)b * m.max_nodes;
+  store_node(m.node_state + nb * 6, s);
+  CKey key = canon_key(s, !m.exact_keys);
+  uint64_t h = key_hash(key);
+  m.node_hash[nb] = h;
+  m.node_e0[nb] = 0;
+  m.node_ne[nb] = 0;
+  int gen = cnt[2] + 1;
+  cnt[0] = 1;
+  cnt[1] = 0;
+  cnt[2] = gen;
+  cnt[3] = 0;
+  uint64_t *ht = m.ht + (size_t)b * m.hcap;
+  ht[h & (uint64_t)(m.hcap - 1)] = ht_entry(gen, 0);
+}
+
+// ------------------------------------------------------------------ select
+// move_to_leaf (MCTS.py:63-149).  Per node: U = cpuct*P*sqrt(max(1,sum N))/(1+N)
+// with NumPy promotion: cpuct*P in float32, the rest float64; Q = W/N
+// (0 while N == 0); the first edge (insertion = ascending action order)
+// with the largest Q+U by strict '>' wins.
+__global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__restrict__ active, float cpuct) {
+  int b = blockIdx.x;
+  int lane = threadIdx.x;
+  int32_t *cnt = m.counts + (size_t)b * 4;
+  if ((active && !active[b]) || cnt[0] == 0) {
+    if (lane == 0) {
+      m.leaf[b] = -1;
+      m.leaf_gidx[b] = -1;
+    }
+    return;
+  }
+  size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
+  int node = 0, d = 0;
+  int32_t *path = m.path + (size_t)b * m.max_depth;
+  for (;;) {
+    int ne = m.node_ne[nb + node];
+    if (ne <= 0) break;
+    int e0 = m.node_e0[nb + node];
+    int n0 = 0, n1 = 0;
+    double w0 = 0, w1 = 0;
+    float p0 = 0, p1 = 0;
+    if (lane < ne) {
+      n0 = m.edge_n[eb + e0 + lane];
+      w0 = m.edge_w[eb + e0 + lane];
+      p0 = m.edge_p[eb + e0 + lane];
+    }
+    if (lane + kWave < ne) {
+      n1 = m.edge_n[eb + e0 + lane + kWave];
+      w1 = m.edge_w[eb + e0 + lane + kWave];
+      p1 = m.edge_p[eb + e0 + lane + kWave];
+    }
+    int ns = n0 + n1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+    double sqrt_ns = __dsqrt_rn(ns > 1 ? (double)ns : 1.0);
+    double best = -INFINITY;
+    int bi = 0x7fffffff;
+    if (lane < ne) {
+      double u = __ddiv_rn(__dmul_rn((double)__fmul_rn(cpuct, p0), sqrt_ns), (double)(1 + n0));
+      double q = n0 ? __ddiv_rn(w0, (double)n0) : 0.0;
+      best = __dadd_rn(q, u);
+      bi = lane;
+    }
+    if (lane + kWave < ne) {
+      double u = __ddiv_rn(__dmul_rn((double)__fmul_rn(cpuct, p1), sqrt_ns), (double)(1 + n1));
+      double q = n1 ? __ddiv_rn(w1, (double)n1) : 0.0;
+      double v = __dadd_rn(q, u);
+      if (v > best) { best = v; bi = lane + kWave; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      double ob = __shfl_xor(best, o);
+      int oi = __shfl_xor(bi, o);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    int sel = e0 + bi;
+    if (d >= m.max_depth) {
+      if (lane == 0) cnt[3] = 1;
+      break;
+    }
+    if (lane == 0) path[d] = sel;
+    d++;
+    node = m.edge_child[eb + sel];
+  }
+  if (lane == 0) {
+    m.leaf[b] = node;
+    m.depth[b] = d;
+    State s = load_node(m.node_state + (nb + node) * 6);
+    m.leaf_gidx[b] = game_done(s.misc) ? -1 : (int)(nb + node);
+  }
+}
+
+// ---------------------------------------------------------- expand + backup
+struct ExpandLds {
+  uint32_t mt[kMT];
+  uint64_t script[kChildSlots];
+  uint64_t state[kChildSlots][6];
+  uint64_t key[kChildSlots][8];
+  uint64_t hash[kChildSlots];
+  int32_t child[kChildSlots];
+  int32_t flag[kChildSlots];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
+};
+
+// expand_leaf (MCTS.py:151-218) + back_fill (:220-266) + the root Dirichlet
+// mix (:308-327).  noise[b*69 + i] is the i-th legal move's Dirichlet sample.
+__global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
+                                                         int32_t *__restrict__ mtcur,
+                                                         const float *__restrict__ policy,
+                                                         const float *__restrict__ value,
+                                                         const double *__restrict__ noise, double eps,
+                                                         float one_minus_eps, int testing) {
+  __shared__ ExpandLds L;
+  int b = blockIdx.x;
+  int lane = threadIdx.x;
+  int leaf = m.leaf[b];
+  if (leaf < 0) return;
+  int32_t *cnt = m.counts + (size_t)b * 4;
+  size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
+  State ls = load_node(m.node_state + (nb + leaf) * 6);
+  int leaf_player = player_of(ls.misc);
+  double v;
+  if (game_done(ls.misc)) {
+    // MCTS.py:333-341: outcome from the leaf player's perspective
+    int wc = winner_code(ls.misc);
+    double outcome = wc == 1 ? 1.0 : wc == 2 ? -1.0 : 0.0;
+    v = (wc == 3) ? 0.0 : (leaf_player == 0 ? outcome : -outcome);
+  } else {
+    v = (double)value[b];
+    uint64_t mk[3];
+    int nl = legal_mask(ls, mk);
+    bool noisy = leaf == 0 && !testing && noise;
+    if (nl > 0 && nl <= kMaxChildren && m.node_ne[nb + leaf] == 0) {
+      bool turn_end = phase_of(ls.misc) == PH_P3;
+      if (turn_end) {
+        // the children's _end_turn_actions draw from the board's stream in
+        // child order (MCTS.py:171-176): replay that sequence once, serially,
+        // on an LDS copy of the stream
+        uint32_t *g = mtw + (size_t)b * kMT;
+        for (int i = lane; i < kMT; i += kWave) L.mt[i] = g[i];
+        __syncthreads();
+        if (lane == 0) {
+          MT mt(L.mt, mtcur[b]);
+          StreamDraw<MT> draw{mt};
+          for (int c = 0; c < nl; c++) {
+            State tmp = ls;
+            L.script[c] = replenish(tmp, draw);
+          }
+          mtcur[b] = mt.cursor();
+        }
+        __syncthreads();
+        for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];
+      }
+      // children: lane handles child c = lane and lane + 64
+      for (int c = lane; c < kChildSlots; c += kWave) {
+        if (c < nl) {
+          int a = kth_action(mk, c);
+          State ch = ls;
+          ScriptDraw sd{turn_end ? L.script[c] : ~0ull};
+          step_state(ch, a, sd);
+          CKey k = canon_key(ch, !m.exact_keys);
+#pragma unroll
+          for (int w = 0; w < 8; w++) L.key[c][w] = k.w[w];
+#pragma unroll
+          for (int w = 0; w < 4; w++) L.state[c][w] = ch.pl[w];
+          L.state[c][4] = ch.piles;
+          L.state[c][5] = ch.misc;
+          L.hash[c] = key_hash(k);
+          L.child[c] = -1;
+          L.flag[c] = 0;
+        }
+      }
+      __syncthreads();
+      // transpositions (MCTS.py:177-204): a child whose key is already in the
+      // tree reuses that node (flag 1), or is skipped if it is the leaf itself
+      // (flag 2) ...
+      int gen = cnt[2];
+      uint64_t *ht = m.ht + (size_t)b * m.hcap;
+      uint64_t hmask = (uint64_t)(m.hcap - 1);
+      for (int c = lane; c < kChildSlots; c += kWave) {
+        if (c >= nl) continue;
+        uint64_t h = L.hash[c];
+        CKey k;
+#pragma unroll
+        for (int w = 0; w < 8; w++) k.w[w] = L.key[c][w];
+        for (uint64_t slot = h & hmask;; slot = (slot + 1) & hmask) {
+          uint64_t e = ht[slot];
+          if ((int)(e >> 32) != gen) break;
+          int nid = (int)(uint32_t)e;
+          if (m.node_hash[nb + nid] != h) continue;
+          State os = load_node(m.node_state + (nb + nid) * 6);
+          if (key_eq(canon_key(os, !m.exact_keys), k)) {
+            L.flag[c] = nid == leaf ? 2 : 1;
+            L.child[c] = nid;
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      // ... and among the remaining children the first of equal keys creates
+      // the node, later siblings reuse it (flag 3: child[c] = that sibling)
+      for (int c = lane; c < kChildSlots; c += kWave) {
+        if (c >= nl || L.flag[c] != 0) continue;
+        uint64_t h = L.hash[c];
+        for (int c2 = 0; c2 < c; c2++) {
+          if (L.flag[c2] != 0 || L.hash[c2] != h) continue;
+          bool eq = true;
+#pragma unroll
+          for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c][w];
+          if (eq) {
+            L.flag[c] = 3;
+            L.child[c] = c2;
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      // new nodes get consecutive ids in child order; edges keep child order
+      int base_n = cnt[0], base_e = cnt[1];
+      int n_new = 0, n_edges = 0;
+      for (int r = 0; r < 2; r++) {
+        int c = lane + r * kWave;
+        bool isnew = c < nl && L.flag[c] == 0;
+        bool hasedge = c < nl && L.flag[c] != 2;
+        uint64_t bn = __ballot(isnew), be = __ballot(hasedge);
+        uint64_t below = (1ull << lane) - 1;
+        if (isnew) L.child[c] = base_n + n_new + __popcll(bn & below);
+        if (hasedge) L.flag[c] |= (n_edges + __popcll(be & below)) << 4;  // edge rank
+        n_new += __popcll(bn);
+        n_edges += __popcll(be);
+      }
+      __syncthreads();
+      if (base_n + n_new > m.max_nodes || base_e + n_edges > m.max_edges) {
+        if (lane == 0) cnt[3] = 1;  // capacity exhausted: leave the leaf unexpanded
+      } else {
+        for (int c = lane; c < kChildSlots; c += kWave) {
+          if (c >= nl) continue;
+          int f = L.flag[c] & 15;
+          int node_id = f == 3 ? L.child[L.child[c]] : L.child[c];
+          if (f == 0) {
+            uint64_t *ns = m.node_state + (nb + node_id) * 6;
+#pragma unroll
+            for (int w = 0; w < 6; w++) ns[w] = L.state[c][w];
+            m.node_hash[nb + node_id] = L.hash[c];
+            m.node_e0[nb + node_id] = 0;
+            m.node_ne[nb + node_id] = 0;
+            for (uint64_t slot = L.hash[c] & hmask;; slot = (slot + 1) & hmask) {
+              unsigned long long old = ht[slot];
+              if ((int)(old >> 32) == gen) continue;
+              unsigned long long prev =
+                  atomicCAS((unsigned long long *)&ht[slot], old, (unsigned long long)ht_entry(gen, node_id));
+              if (prev == old) break;
+            }
+          }
+          if (f != 2) {
+            int a = kth_action(mk, c);
+            float p = policy[(size_t)b * kActions + a];
+            if (noisy) p = __double2float_rn(__dadd_rn((double)__fmul_rn(one_minus_eps, p),
+                                                       __dmul_rn(eps, noise[(size_t)b * kMaxChildren + c])));
+            int e = base_e + (L.flag[c] >> 4);
+            m.edge_action[eb + e] = (int16_t)a;
+            m.edge_child[eb + e] = node_id;
+            m.edge_n[eb + e] = 0;
+            m.edge_w[eb + e] = 0.0;
+            m.edge_p[eb + e] = p;
+            m.edge_player[eb + e] = (uint8_t)leaf_player;
+          }
+        }
+        if (lane == 0) {
+          m.node_e0[nb + leaf] = base_e;
+          m.node_ne[nb + leaf] = n_edges;
+          cnt[0] = base_n + n_new;
+          cnt[1] = base_e + n_edges;
+        }
+      }
+    } else if (nl > kMaxChildren && lane == 0) {
+      cnt[3] = 2;
+    }
+  }
+  // back_fill: every path edge gets N += 1, W += v * (+1 if the edge's mover
+  // is the leaf's player else -1)
+  int d = m.depth[b];
+  const int32_t *path = m.path + (size_t)b * m.max_depth;
+  for (int i = lane; i < d; i += kWave) {
+    int e = path[i];
+    double dir = m.edge_player[eb + e] == leaf_player ? 1.0 : -1.0;
+    m.edge_n[eb + e] += 1;
+    m.edge_w[eb + e] = __dadd_rn(m.edge_w[eb + e], v * dir);
+  }
+}
+
+// root visit counts by action (MCTS.py:355-376)
+__global__ void __launch_bounds__(kWave) k_result(hz_mcts m, int32_t *__restrict__ visits) {
+  int b = blockIdx.x;
+  int lane = threadIdx.x;
+  int32_t *out = visits + (size_t)b * kActions;
+  for (int a = lane; a < kActions; a += kWave) out[a] = 0;
+  __syncthreads();
+  if (m.counts[(size_t)b * 4] == 0) return;
+  size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
+  int ne = m.node_ne[nb], e0 = m.node_e0[nb];
+  for (int i = lane; i < ne; i += kWave) out[m.edge_action[eb + e0 + i]] = m.edge_n[eb + e0 + i];
+}
+
+template <class T>
+bool alloc(T **p, size_t count) {
+  return hipMalloc((void **)p, count * sizeof(T)) == hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream) {
+  if (n_boards <= 0 || max_nodes < 2 || max_depth < 1) return nullptr;
+  hz_mcts *m = (hz_mcts *)calloc(1, sizeof(hz_mcts));
+  if (!m) return nullptr;
+  m->n = n_boards;
+  m->max_nodes = max_nodes;
+  m->max_edges = max_nodes;
+  int h = 1;
+  while (h < 2 * max_nodes) h <<= 1;
+  m->hcap = h;
+  m->max_depth = max_depth;
+  m->exact_keys = exact_keys;
+  m->stream = (hipStream_t)stream;
+  size_t n = (size_t)n_boards, N = n * max_nodes, E = n * m->max_edges;
+  bool ok = alloc(&m->node_state, N * 6) && alloc(&m->node_hash, N) && alloc(&m->node_e0, N) &&
+            alloc(&m->node_ne, N) && alloc(&m->edge_action, E) && alloc(&m->edge_child, E) &&
+            alloc(&m->edge_n, E) && alloc(&m->edge_w, E) && alloc(&m->edge_p, E) && alloc(&m->edge_player, E) &&
+            alloc(&m->ht, n * m->hcap) && alloc(&m->counts, n * 4) && alloc(&m->path, n * max_depth) &&
+            alloc(&m->depth, n) && alloc(&m->leaf, n) && alloc(&m->leaf_gidx, n);
+  if (ok) {
+    ok = hipMemset(m->ht, 0, n * m->hcap * sizeof(uint64_t)) == hipSuccess &&
+         hipMemset(m->counts, 0, n * 4 * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(m->depth, 0, n * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(m->leaf, 0xff, n * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(m->leaf_gidx, 0xff, n * sizeof(int32_t)) == hipSuccess;
+  }
+  if (!ok) {
+    hz_mcts_destroy(m);
+    return nullptr;
+  }
+  return m;
+}
+
+void hz_mcts_destroy(hz_mcts *m) {
+  if (!m) return;
+  void *ptrs[] = {m->node_state, m->node_hash, m->node_e0,   m->node_ne, m->edge_action, m->edge_child,
+                  m->edge_n,     m->edge_w,    m->edge_p,    m->edge_player, m->ht, m->counts,
+                  m->path,       m->depth,     m->leaf,      m->leaf_gidx};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  free(m);
+}
+
+int hz_mcts_set_stream(hz_mcts *m, void *stream) {
+  if (!m) return -1;
+  m->stream = (hipStream_t)stream;
+  return 0;
+}
+
+int hz_mcts_begin(hz_mcts *m, hz_env *env, const uint8_t *active) {
+  if (!m || !env || hz_env_size(env) != m->n) return -1;
+  hipLaunchKernelGGL(k_begin, dim3((m->n + kWave - 1) / kWave), dim3(kWave), 0, m->stream, *m,
+                     hz_env_state_ptr(env), m->n, active);
+  return launch_err();
+}
+
+int hz_mcts_select(hz_mcts *m, const uint8_t *active, float cpuct) {
+  if (!m) return -1;
+  hipLaunchKernelGGL(k_select, dim3(m->n), dim3(kWave), 0, m->stream, *m, active, cpuct);
+  return launch_err();
+}
+
+int hz_mcts_encode_leaves(hz_mcts *m, float *board, float *glob) {
+  if (!m || (!board && !glob)) return -1;
+  launch_encode(m->node_state, 1, 6, m->leaf_gidx, m->n, board, glob, m->stream);
+  return launch_err();
+}
+
+int hz_mcts_expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
+                          double eps, int32_t testing) {
+  if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
+  float ome = (float)(1.0 - eps);
+  hipLaunchKernelGGL(k_expand_backup, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
+                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing);
+  return launch_err();
+}
+
+int hz_mcts_result(hz_mcts *m, int32_t *visits) {
+  if (!m || !visits) return -1;
+  hipLaunchKernelGGL(k_result, dim3(m->n), dim3(kWave), 0, m->stream, *m, visits);
+  return launch_err();
+}
+
+int hz_mcts_stats(hz_mcts *m, int32_t *counts) {
+  if (!m || !counts) return -1;
+  return hipMemcpyAsync(counts, m->counts, (size_t)m->n * 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, m->stream)
+             ? 1
+             : 0;
+}
+
+int hz_mcts_leaf_ptrs(hz_mcts *m, int32_t **leaf, int32_t **leaf_gidx) {
+  if (!m) return -1;
+  if (leaf) *leaf = m->leaf;
+  if (leaf_gidx) *leaf_gidx = m->leaf_gidx;
+  return 0;
+}
+
+}  // extern "C"

@@ -36,6 +36,16 @@ _SIGS = {
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_export_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_import_state": ([_vp, _vp, _vp, _vp], _c.c_int),
+    "hz_mcts_create": ([_c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _vp], _vp),
+    "hz_mcts_destroy": ([_vp], None),
+    "hz_mcts_set_stream": ([_vp, _vp], _c.c_int),
+    "hz_mcts_begin": ([_vp, _vp, _vp], _c.c_int),
+    "hz_mcts_select": ([_vp, _vp, _c.c_float], _c.c_int),
+    "hz_mcts_encode_leaves": ([_vp, _vp, _vp], _c.c_int),
+    "hz_mcts_expand_backup": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
+    "hz_mcts_result": ([_vp, _vp], _c.c_int),
+    "hz_mcts_stats": ([_vp, _vp], _c.c_int),
+    "hz_mcts_leaf_ptrs": ([_vp, _vp, _vp], _c.c_int),
     "hz_version": ([], _c.c_char_p),
 }
 

@@ -134,13 +134,14 @@ class BatchedEnv:
 
     # -- state transfer -------------------------------------------------------
     def export_state(self, with_mt=False):
-        """int64 [6, n] state words (+ uint32-as-int32 [624, n] MT words and
-        int32 [n] CPython indices when with_mt)."""
+        """int64 [6, n] state words (+ uint32-as-int32 [n, 624] MT words and
+        int32 [n] CPython indices when with_mt: random.setstate((3, tuple(mt[b]) +
+        (idx[b],), None)) continues board b's stream)."""
         self._sync_stream()
         st = torch.empty(WORDS, self.n, dtype=torch.int64, device=self.device)
         mt = idx = None
         if with_mt:
-            mt = torch.empty(624, self.n, dtype=torch.int32, device=self.device)
+            mt = torch.empty(self.n, 624, dtype=torch.int32, device=self.device)
             idx = torch.empty(self.n, dtype=torch.int32, device=self.device)
         nat.check(nat.lib().hz_export_state(self._h, nat.ptr(st), nat.ptr(mt), nat.ptr(idx)), "hz_export_state")
         return (st, mt, idx) if with_mt else st

@@ -1,0 +1,158 @@
+"""BatchedMCTS: one PUCT search per board of a BatchedEnv, all boards advancing
+in lock-step so that every simulation's leaf evaluations form one PyTorch
+batch (the reference evaluates one leaf at a time: MCTS.py:291-352).
+
+    select (HIP) -> encode leaves (HIP) -> evaluator(board, glob) (PyTorch)
+    -> expand + backup (HIP)
+
+The evaluator is any callable (board f32[n,38,5,7], glob f32[n,42]) ->
+(policy f32[n,143] probabilities, value f32[n]) on the same device, e.g.
+`BatchedPredictor(model)` wrapping model.py's AlphaZeroModel the way
+ModelManager.predict does (softmax over all 143 logits, model.py:81-110).
+"""
+import torch
+
+from . import _native as nat
+from .env import ACTION_SIZE
+
+MAX_CHILDREN = 69
+
+
+class BatchedMCTS:
+    def __init__(self, env, num_simulations, max_nodes=None, max_depth=192, exact_keys=False):
+        self.env = env
+        self.n = env.n
+        self.device = env.device
+        self.num_simulations = int(num_simulations)
+        self.max_nodes = int(max_nodes or 1 + MAX_CHILDREN * self.num_simulations)
+        L = nat.lib()
+        self._h = L.hz_mcts_create(self.n, self.max_nodes, int(max_depth), int(bool(exact_keys)),
+                                   nat.stream_ptr(self.device))
+        if not self._h:
+            raise nat.NativeError("hz_mcts_create failed (out of device memory?)")
+        d = self.device
+        self.board = torch.zeros(self.n, 38, 5, 7, dtype=torch.float32, device=d)
+        self.glob = torch.zeros(self.n, 42, dtype=torch.float32, device=d)
+        self.visits = torch.zeros(self.n, ACTION_SIZE, dtype=torch.int32, device=d)
+        self.counts = torch.zeros(self.n, 4, dtype=torch.int32, device=d)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            nat.lib().hz_mcts_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _sync(self):
+        nat.lib().hz_mcts_set_stream(self._h, nat.stream_ptr(self.device))
+        self.env._sync_stream()
+
+    # -- the four device stages ----------------------------------------------
+    def begin(self, active=None):
+        self._sync()
+        nat.check(nat.lib().hz_mcts_begin(self._h, self.env.handle, nat.ptr(active)), "hz_mcts_begin")
+
+    def select(self, cpuct, active=None):
+        nat.check(nat.lib().hz_mcts_select(self._h, nat.ptr(active), float(cpuct)), "hz_mcts_select")
+
+    def encode_leaves(self):
+        nat.check(nat.lib().hz_mcts_encode_leaves(self._h, nat.ptr(self.board), nat.ptr(self.glob)),
+                  "hz_mcts_encode_leaves")
+        return self.board, self.glob
+
+    def expand_backup(self, policy, value, noise=None, eps=0.25, testing=True):
+        policy = policy.to(dtype=torch.float32).contiguous()
+        value = value.reshape(-1).to(dtype=torch.float32).contiguous()
+        if noise is not None:
+            noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
+        nat.check(nat.lib().hz_mcts_expand_backup(self._h, self.env.handle, nat.ptr(policy), nat.ptr(value),
+                                                  nat.ptr(noise), float(eps), int(bool(testing))),
+                  "hz_mcts_expand_backup")
+
+    def result(self):
+        nat.check(nat.lib().hz_mcts_result(self._h, nat.ptr(self.visits)), "hz_mcts_result")
+        return self.visits
+
+    def stats(self):
+        nat.check(nat.lib().hz_mcts_stats(self._h, nat.ptr(self.counts)), "hz_mcts_stats")
+        return self.counts
+
+    # -- one full search per board -------------------------------------------
+    def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None):
+        """get_best_action_and_pi's simulation loop (MCTS.py:288-352) for every
+        active board; returns root visit counts int32 [n, 143]."""
+        if active is not None:
+            active = active.to(device=self.device, dtype=torch.uint8).contiguous()
+        self.begin(active)
+        for _ in range(self.num_simulations if sims is None else int(sims)):
+            self.select(cpuct, active)
+            board, glob = self.encode_leaves()
+            policy, value = evaluator(board, glob)
+            self.expand_backup(policy, value, noise, eps, testing)
+        return self.result()
+
+
+def choose_actions(visits, explore, u):
+    """Move choice of get_best_action_and_pi (MCTS.py:394-423) from root visit
+    counts (edges are in ascending action order, as the search inserts them):
+    explore[b] -> sample proportional to N with the uniform u[b] (first action
+    whose cumulative count exceeds u * total); else the first action with the
+    most visits.  Returns int64 [n] (-1 when a board has no visits)."""
+    v = visits.to(torch.int64)
+    total = v.sum(1)
+    greedy = torch.argmax(v, dim=1)
+    cum = v.cumsum(1)
+    target = u.to(torch.float64) * total.to(torch.float64)
+    sampled = torch.argmax((target.unsqueeze(1) < cum.to(torch.float64)).to(torch.int32), dim=1)
+    act = torch.where(explore.to(torch.bool), sampled, greedy)
+    return torch.where(total > 0, act, torch.full_like(act, -1))
+
+
+def pi_from_visits(visits):
+    """pi_target = N / sum(N) in float64, stored as float32 by the trainer
+    (MCTS.py:378-381, trainer.py:531)."""
+    v = visits.to(torch.float64)
+    tot = v.sum(1, keepdim=True)
+    return torch.where(tot > 0, v / tot.clamp_min(1), torch.zeros_like(v)).to(torch.float32)
+
+
+class BatchedPredictor:
+    """ModelManager.predict (model.py:81-110) for a whole batch: eval mode,
+    no grad, softmax over all 143 logits (illegal moves are not masked)."""
+
+    def __init__(self, model, dtype=None):
+        self.model = model
+        self.dtype = dtype
+
+    @torch.no_grad()
+    def __call__(self, board, glob):
+        self.model.eval()
+        if self.dtype is not None and self.dtype != torch.float32:
+            with torch.autocast(device_type="cuda", dtype=self.dtype):
+                logits, value = self.model(board, glob)
+        else:
+            logits, value = self.model(board, glob)
+        return torch.softmax(logits.float(), dim=1), value.float().reshape(-1)
+
+
+def stub_evaluator(board, glob):
+    """Deterministic integer-valued evaluator used by the parity tests; the
+    same formula as tests/golden/make_golden.py:stub_predict_np, so the GPU
+    search and the reference search see identical priors and values."""
+    n0 = torch.round(board[:, 0:18].double().sum((1, 2, 3))).long()
+    n1 = torch.round(board[:, 18:36].double().sum((1, 2, 3))).long()
+    cp = torch.round(board[:, 36].amax((1, 2))).long()
+    ph3 = torch.round(board[:, 37].amax((1, 2)) * 3.0).long()
+    pc = torch.round(glob[:, 0:36].double() * 3.0).long()
+    w = (pc * torch.arange(1, 37, device=board.device, dtype=torch.int64)).sum(1)
+    K = (n0 * 73 + n1 * 151 + ph3 * 7 + cp * 3 + w * 13) % (1 << 31)
+    a = torch.arange(ACTION_SIZE, device=board.device, dtype=torch.int64)
+    h = (a.unsqueeze(0) * 2654435761 + K.unsqueeze(1) * 40503) % (1 << 32)
+    pol = ((h >> 22) + 1).to(torch.float32) / 1024.0
+    val = ((K % 255) - 127).to(torch.float64) / 128.0
+    return pol, val.to(torch.float32)

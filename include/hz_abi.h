@@ -19,7 +19,7 @@
  *  - Board b's state is the structure-of-arrays record documented in
  *    harmonies-alphazero_amd/csrc/hz_device.hpp (six u64 words, word w at
  *    state[w * n + b]); its chance stream is a CPython MT19937 (624 words at
- *    mt[i * n + b] plus a cursor).
+ *    mt[b * 624 + i] plus a cursor).
  */
 #ifndef HZ_ABI_H
 #define HZ_ABI_H
@@ -54,7 +54,7 @@ int32_t hz_env_size(const hz_env *env);
 int hz_env_set_stream(hz_env *env, void *stream);
 /* device pointers of the handle's own buffers (for zero-copy views) */
 uint64_t *hz_env_state_ptr(hz_env *env);     /* [6][n]            */
-uint32_t *hz_env_mt_ptr(hz_env *env);        /* [624][n]          */
+uint32_t *hz_env_mt_ptr(hz_env *env);        /* [n][624]          */
 int32_t *hz_env_mt_pos_ptr(hz_env *env);     /* [n]               */
 int32_t *hz_env_ply_ptr(hz_env *env);        /* [n] plies played in the current game */
 uint64_t *hz_env_seed_ptr(hz_env *env);      /* [n] seed of the current game */
@@ -102,11 +102,47 @@ int hz_rollout(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *tra
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
 /* export: state[6][n] and, optionally, the MT streams in CPython getstate()
- * form (mt[624][n], mt_index[n] in [0, 624]).  Normalises the lazy twist in
- * place (semantics unchanged). */
+ * form (mt[n][624], mt_index[n] in [0, 624]).  Finishes any partially
+ * twisted generation in place (the stream's future outputs are unchanged). */
 int hz_export_state(hz_env *env, uint64_t *state, uint32_t *mt, int32_t *mt_index);
 /* import: the inverse; mt/mt_index may be NULL to keep the current streams. */
 int hz_import_state(hz_env *env, const uint64_t *state, const uint32_t *mt, const int32_t *mt_index);
+
+/* ---- batched MCTS (MCTS.py) ---------------------------------------------- */
+/* One single-tree PUCT search per board of an hz_env, all boards advancing
+ * one simulation per call sequence select -> encode_leaves -> (caller's
+ * policy/value inference, e.g. PyTorch) -> expand_backup.  Semantics follow
+ * get_best_action_and_pi (MCTS.py:272-441) with moves in ascending action
+ * order (the reference's order is set iteration order).
+ * Transpositions are keyed like the reference's hash(state) (exact_keys = 0)
+ * or by the exact canonical tuple (exact_keys = 1).  max_nodes bounds nodes
+ * and edges per board per search (1 + sims * 69 never overflows). */
+typedef struct hz_mcts hz_mcts;
+hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream);
+void hz_mcts_destroy(hz_mcts *mcts);
+int hz_mcts_set_stream(hz_mcts *mcts, void *stream);
+/* new tree per board with root = the env board's current state (MCTS.py:288);
+ * active[b] == 0 (or NULL = all active) leaves board b out of this search */
+int hz_mcts_begin(hz_mcts *mcts, hz_env *env, const uint8_t *active);
+/* move_to_leaf (MCTS.py:63-149) for every active board */
+int hz_mcts_select(hz_mcts *mcts, const uint8_t *active, float cpuct);
+/* create_state_tensors of every board's selected leaf into board[n][38][5][7],
+ * glob[n][42]; rows of terminal leaves / inactive boards are zero */
+int hz_mcts_encode_leaves(hz_mcts *mcts, float *board, float *glob);
+/* expand_leaf (MCTS.py:151-218) with policy[n][143] (probabilities, as
+ * ModelManager.predict returns them, model.py:81-110), root Dirichlet mix
+ * (MCTS.py:308-327) when !testing using noise[n][69] (i-th legal move), then
+ * back_fill (MCTS.py:220-266) with value[n] (terminal leaves use the game
+ * outcome, MCTS.py:333-341).  Children's chance draws consume the env
+ * board's MT stream in child order, like the reference's apply_move calls. */
+int hz_mcts_expand_backup(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
+                          const double *noise, double eps, int32_t testing);
+/* root visit counts by action id: visits[n][143] (MCTS.py:355-376) */
+int hz_mcts_result(hz_mcts *mcts, int32_t *visits);
+/* per-board [nodes, edges, search generation, overflow flag] -> counts[n][4] */
+int hz_mcts_stats(hz_mcts *mcts, int32_t *counts);
+/* host pointers to the device arrays leaf[n] / leaf_gidx[n] (debugging) */
+int hz_mcts_leaf_ptrs(hz_mcts *mcts, int32_t **leaf, int32_t **leaf_gidx);
 
 /* ---- build info ---------------------------------------------------------- */
 const char *hz_version(void);

@@ -120,7 +120,7 @@ def test_rollout_finals_and_rng_stream(Env):
     mt = mt.cpu().numpy().view(np.uint32)
     idx = idx.cpu().numpy()
     for b in range(n):
-        m = oracle.mt_from_words(mt[:, b], idx[b])
+        m = oracle.mt_from_words(mt[b], idx[b])
         assert oracle.mt_next32(m) == f["next_word"][b], b
 
 
@@ -269,10 +269,16 @@ def test_mt_import_export_roundtrip_cpython(Env):
     env = Env(1, device=DEV)
     m = oracle.mt_seed(0)
     st = oracle.reset(m)
-    mt = torch.from_numpy(words[:624].astype(np.uint32).view(np.int32).reshape(624, 1).copy())
+    mt = torch.from_numpy(words[:624].astype(np.uint32).view(np.int32).reshape(1, 624).copy())
     idx = torch.tensor([int(words[624])], dtype=torch.int32)
     import_refstates(env, [st])
     env.import_state(env.export_state(), mt, idx)
     _, mt2, idx2 = env.export_state(with_mt=True)
-    assert (mt2.cpu().numpy().view(np.uint32)[:, 0] == words[:624]).all()
+    assert (mt2.cpu().numpy().view(np.uint32)[0] == words[:624]).all()
     assert idx2.item() == int(words[624])
+    # and the next draws continue CPython's stream
+    acts = torch.tensor([0], dtype=torch.int16)
+    m = oracle.mt_from_words(words[:624], int(words[624]))
+    s1 = oracle.step(st, 0, m)[1]
+    env.step(acts)
+    assert (states_of(env)[0] == s1).all()

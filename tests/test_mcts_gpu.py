@@ -1,0 +1,121 @@
+"""GPU parity of the batched HIP MCTS (hzamd.mcts) against the reference's
+own get_best_action_and_pi (golden fixtures, canonical move order, stub
+evaluator) and against the C oracle at full batch size.  Visit counts, the
+chosen move, tree sizes and the RNG stream must match exactly."""
+import os
+from collections import defaultdict
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN
+from hzamd.state import pack_ref, unpack_ref, words_to_array
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def make_env(refs, mt_seeds):
+    from hzamd.env import BatchedEnv
+    env = BatchedEnv(len(refs), device=DEV)
+    words = words_to_array([pack_ref(v) for v in refs])
+    mts = np.zeros((len(refs), 624), np.uint32)
+    idx = np.zeros(len(refs), np.int32)
+    for i, s in enumerate(mt_seeds):
+        w, k = oracle.mt_seed(int(s)).words()
+        mts[i], idx[i] = w, k
+    env.import_state(torch.from_numpy(np.ascontiguousarray(words.T)),
+                     torch.from_numpy(mts.view(np.int32)), torch.from_numpy(idx))
+    return env
+
+
+def test_mcts_matches_reference_fixtures():
+    from hzamd.mcts import BatchedMCTS, choose_actions, stub_evaluator
+    f = load("mcts.npz")
+    groups = defaultdict(list)
+    for k in range(len(f["sims"])):
+        groups[(int(f["sims"][k]), float(f["cpuct"][k]), int(f["testing"][k]), float(f["eps"][k]))].append(k)
+    checked = 0
+    for (sims, cpuct, testing, eps), ks in groups.items():
+        env = make_env(f["state"][ks], f["mt_seed"][ks])
+        mcts = BatchedMCTS(env, sims)
+        noise = torch.from_numpy(np.ascontiguousarray(f["noise"][ks][:, :69]))
+        visits = mcts.search(stub_evaluator, cpuct, noise=noise, eps=eps, testing=bool(testing))
+        explore = torch.tensor([(not testing) and f["ply"][k] < f["tau0"][k] for k in ks])
+        u = torch.tensor([f["u"][k] for k in ks], dtype=torch.float64)
+        act = choose_actions(visits.cpu(), explore, u).numpy()
+        counts = mcts.stats().cpu().numpy()
+        v = visits.cpu().numpy()
+        _, mt, mti = env.export_state(with_mt=True)
+        mt = mt.cpu().numpy().view(np.uint32)
+        mti = mti.cpu().numpy()
+        for j, k in enumerate(ks):
+            assert (v[j] == f["visits"][k]).all(), (k, v[j][v[j] > 0], f["visits"][k][f["visits"][k] > 0])
+            assert act[j] == f["action"][k], k
+            assert counts[j, 0] == f["n_nodes"][k] and counts[j, 1] == f["n_edges"][k], k
+            assert counts[j, 3] == 0
+            m = oracle.mt_from_words(mt[j], mti[j])
+            assert oracle.mt_next32(m) == f["next_word"][k], k
+            checked += 1
+        mcts.close()
+        env.close()
+    assert checked == len(f["sims"])
+
+
+def test_mcts_4096_boards_vs_oracle():
+    """Full batch: 4096 boards at assorted game positions, 24 simulations,
+    testing mode, stub evaluator; every board is searched by the C oracle."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, base, sims, cpuct = 4096, 500, 24, 2.0
+    env = BatchedEnv(n, seed_base=base, device=DEV)
+    env.reset()
+    # advance board b by (b % 61) rule plies to spread positions over the game
+    plies = torch.arange(n, device=DEV) % 61
+    for p in range(61):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        act = torch.where(plies > p, act, torch.full_like(act, -1))
+        env.step(act)
+    st0, mt0, idx0 = env.export_state(with_mt=True)
+    st0, mt0, idx0 = st0.cpu().numpy(), mt0.cpu().numpy().view(np.uint32), idx0.cpu().numpy()
+    active = torch.from_numpy(np.array([not oracle.is_game_over(unpack_ref(st0[:, b])) for b in range(n)]))
+    mcts = BatchedMCTS(env, sims)
+    visits = mcts.search(stub_evaluator, cpuct, active=active).cpu().numpy()
+    counts = mcts.stats().cpu().numpy()
+    _, mt1, idx1 = env.export_state(with_mt=True)
+    mt1, idx1 = mt1.cpu().numpy().view(np.uint32), idx1.cpu().numpy()
+    for b in range(n):
+        if not active[b]:
+            assert visits[b].sum() == 0
+            continue
+        m = oracle.mt_from_words(mt0[b], idx0[b])
+        a, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, cpuct, testing=True)
+        assert (visits[b] == ov).all(), b
+        assert (counts[b, 0], counts[b, 1]) == (nn, ne), b
+        m2 = oracle.mt_from_words(mt1[b], idx1[b])
+        assert oracle.mt_next32(m2) == oracle.mt_next32(m), b
+
+
+def test_mcts_exact_keys_mode():
+    """exact_keys=1 keys transpositions by the true canonical tuple."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, sims = 128, 16
+    env = BatchedEnv(n, seed_base=77, device=DEV)
+    env.reset()
+    st0, mt0, idx0 = env.export_state(with_mt=True)
+    st0, mt0, idx0 = st0.cpu().numpy(), mt0.cpu().numpy().view(np.uint32), idx0.cpu().numpy()
+    mcts = BatchedMCTS(env, sims, exact_keys=True)
+    visits = mcts.search(stub_evaluator, 1.5).cpu().numpy()
+    counts = mcts.stats().cpu().numpy()
+    for b in range(n):
+        m = oracle.mt_from_words(mt0[b], idx0[b])
+        _, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, 1.5, testing=True, exact_keys=True)
+        assert (visits[b] == ov).all() and (counts[b, 0], counts[b, 1]) == (nn, ne), b
