@@ -375,6 +375,14 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
   return 0;
 }
 
+int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_stride, const int32_t *idx, int32_t m,
+                     float *board, float *glob, void *stream) {
+  if (!states || m < 0 || (!board && !glob)) return -1;
+  if (m == 0) return 0;
+  launch_encode(states, (long)word_stride, (long)item_stride, idx, m, board, glob, (hipStream_t)stream);
+  return launch_err();
+}
+
 const char *hz_version(void) { return "hz 0.1 gfx950"; }
 
 }  // extern "C"

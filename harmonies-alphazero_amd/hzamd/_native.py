@@ -33,6 +33,7 @@ _SIGS = {
     "hz_score": ([_vp, _vp, _vp], _c.c_int),
     "hz_encode": ([_vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_rule_actions": ([_vp, _vp, _vp, _vp], _c.c_int),
+    "hz_encode_states": ([_vp, _c.c_int64, _c.c_int64, _vp, _c.c_int32, _vp, _vp, _vp], _c.c_int),
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_export_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_import_state": ([_vp, _vp, _vp, _vp], _c.c_int),

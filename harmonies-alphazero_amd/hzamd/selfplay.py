@@ -1,0 +1,142 @@
+"""Batched self-play: `self_play_worker` (trainer.py:434-541) for n boards at
+once on one GPU.
+
+Per ply, for every board still playing: record the state and the player to
+move, run get_best_action_and_pi's search (BatchedMCTS, one PyTorch leaf
+batch per simulation), choose the move (tau = 1 sampling for the first
+`turns_until_tau0` plies unless testing, else the first most-visited move),
+apply it (HIP step, chance draws from the board's CPython stream).  When a
+board's game ends its examples get z = outcome from the recorded player's
+perspective (trainer.py:517-538).
+
+Records stay on the device in compact form: state words int64 [T, 6, n],
+player int8 [T, n], visit counts int32 [T, n, 143], valid bool [T, n].
+`examples()` turns them into the reference's example tuples
+(board f32[38,5,7], glob f32[42], pi f32[143], z f32[1]).
+"""
+import torch
+
+from . import _native as nat
+from .env import BatchedEnv
+from .mcts import MAX_CHILDREN, BatchedMCTS, choose_actions, pi_from_visits
+
+MCTS_DEFAULT = {  # config.py:53-65 (the self-play config)
+    "num_simulations": 400, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+    "fpu_value": 0.25, "turns_until_tau0": 15, "action_size": 143, "testing": False,
+}
+
+
+class NoiseSource:
+    """Root Dirichlet noise (MCTS.py:314-316) and the tau=1 uniforms, drawn on
+    the device from a generator seeded by (seed, first global board id, move
+    counter): a rank's 4096 boards get the same draws whatever the GPU count."""
+
+    def __init__(self, seed, device):
+        self.seed = int(seed)
+        self.device = device
+        self.gen = torch.Generator(device=device)
+
+    def draw(self, step, counts, alpha):
+        self.gen.manual_seed((self.seed * 1000003 + step) & ((1 << 63) - 1))
+        n = counts.numel()
+        conc = torch.full((n, MAX_CHILDREN), float(alpha), dtype=torch.float64, device=self.device)
+        g = torch._standard_gamma(conc, generator=self.gen)
+        live = torch.arange(MAX_CHILDREN, device=self.device).unsqueeze(0) < counts.unsqueeze(1)
+        g = torch.where(live, g, torch.zeros_like(g))
+        noise = g / g.sum(1, keepdim=True).clamp_min(1e-300)
+        u = torch.rand(n, dtype=torch.float64, device=self.device, generator=self.gen)
+        return noise, u
+
+
+class SelfPlay:
+    def __init__(self, n_boards, evaluator, mcts_config=None, seed_base=0, device="cuda", max_plies=200,
+                 env=None, exact_keys=False):
+        self.cfg = dict(MCTS_DEFAULT, **(mcts_config or {}))
+        self.device = torch.device(device)
+        self.env = env or BatchedEnv(n_boards, seed_base=seed_base, device=self.device)
+        self.n = self.env.n
+        self.evaluator = evaluator
+        self.mcts = BatchedMCTS(self.env, self.cfg["num_simulations"], exact_keys=exact_keys)
+        self.max_plies = int(max_plies)
+        self.noise = NoiseSource(seed_base, self.device)
+        self.keep_noise = False
+        self.noise_log = []
+        self.step_counter = 0
+
+    def play(self, reset=True):
+        """Play one game on every board; returns the device records."""
+        env, n, d, cfg = self.env, self.n, self.device, self.cfg
+        if reset:
+            env.reset()
+        T = self.max_plies
+        states = torch.zeros(T, 6, n, dtype=torch.int64, device=d)
+        players = torch.zeros(T, n, dtype=torch.int8, device=d)
+        visits = torch.zeros(T, n, 143, dtype=torch.int32, device=d)
+        valid = torch.zeros(T, n, dtype=torch.bool, device=d)
+        testing = bool(cfg.get("testing", False))
+        done = env.done()
+        ply = 0
+        while ply < T and not bool(done.all()):
+            active = ~done
+            st = env.export_state()
+            states[ply] = st
+            players[ply] = ((st[5] >> 41) & 1).to(torch.int8)
+            valid[ply] = active
+            _, count = env.legal_mask()
+            noise, u = self.noise.draw(self.step_counter, count, cfg["dirichlet_alpha"])
+            self.step_counter += 1
+            v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
+                                 eps=cfg["dirichlet_epsilon"], testing=testing)
+            explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
+            act = choose_actions(v, explore, u)
+            if self.keep_noise:
+                self.noise_log.append((noise.clone(), u.clone(), act.clone()))
+            visits[ply] = v
+            act = torch.where(active, act, torch.full_like(act, -1)).to(torch.int16)
+            status = env.step(act)
+            bad = active & (status != 0)
+            if bool(bad.any()):
+                raise RuntimeError(f"self-play step failed on boards {torch.nonzero(bad).flatten().tolist()[:8]}")
+            done = env.done()
+            ply += 1
+        final = env.export_state()
+        return {"states": states[:ply], "players": players[:ply], "visits": visits[:ply],
+                "valid": valid[:ply], "final": final, "plies": ply}
+
+    @staticmethod
+    def outcomes(final):
+        """get_game_outcome per board (+1 P0 won, -1 P1 won, 0 draw)."""
+        win = (final[5] >> 46) & 3
+        return torch.where(win == 1, 1, torch.where(win == 2, -1, 0)).to(torch.float32)
+
+    def compact(self, rec):
+        """Flatten the valid records: states int64 [M, 6], pi f32 [M, 143],
+        z f32 [M] (trainer.py:517-538), board id int32 [M]."""
+        out = self.outcomes(rec["final"])                       # [n]
+        T = rec["plies"]
+        mask = rec["valid"]                                      # [T, n]
+        player = rec["players"].to(torch.float32)
+        z = torch.where(player == 0, out.unsqueeze(0), -out.unsqueeze(0))  # 0 stays 0 for draws
+        states = rec["states"].permute(0, 2, 1)[mask]            # [M, 6]
+        pi = pi_from_visits(rec["visits"][mask])                 # [M, 143]
+        board_id = torch.arange(self.n, device=self.device).expand(T, self.n)[mask].to(torch.int32)
+        return {"states": states.contiguous(), "pi": pi, "z": z[mask].contiguous(), "board": board_id}
+
+    def examples(self, compact):
+        """The reference's replay-buffer tuples (trainer.py:529-538), on CPU."""
+        board, glob = encode_states(compact["states"])
+        b, g, p, z = board.cpu(), glob.cpu(), compact["pi"].cpu(), compact["z"].cpu()
+        return [(b[i], g[i], p[i], z[i:i + 1]) for i in range(b.shape[0])]
+
+
+def encode_states(states):
+    """create_state_tensors for an int64 [M, 6] array of state words."""
+    m = states.shape[0]
+    dev = states.device
+    board = torch.empty(m, 38, 5, 7, dtype=torch.float32, device=dev)
+    glob = torch.empty(m, 42, dtype=torch.float32, device=dev)
+    if m:
+        st = states.contiguous()
+        nat.check(nat.lib().hz_encode_states(nat.ptr(st), 1, 6, None, m, nat.ptr(board), nat.ptr(glob),
+                                             nat.stream_ptr(dev)), "hz_encode_states")
+    return board, glob

@@ -85,6 +85,12 @@ int hz_score(hz_env *env, int32_t *out, int32_t *out_parts);
  * idx[0..m) (idx NULL = boards 0..m-1): board[m][38][5][7], glob[m][42], f32. */
 int hz_encode(hz_env *env, const int32_t *idx, int32_t m, float *board, float *glob);
 
+/* Stateless encoder over any state array (replay records, tree nodes): item j
+ * is idx[j] (idx NULL = j); its word w is states[item * item_stride +
+ * w * word_stride].  idx[j] < 0 yields zeros.  Enqueued on `stream`. */
+int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_stride, const int32_t *idx,
+                     int32_t m, float *board, float *glob, void *stream);
+
 /* Build-defined deterministic policy used by the env benchmark and the golden
  * traces: pick legal action k = ((splitmix64(seed, ply) >> 32) * L) >> 32 in
  * ascending action order.  Writes action[b] (-1 if no legal move). */
