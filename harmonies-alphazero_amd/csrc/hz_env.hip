@@ -118,6 +118,21 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
   if (status) status[b] = r;
 }
 
+// -------------------------------------------- replenish / end-turn (facade)
+__global__ void __launch_bounds__(kBlock) k_turn_op(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
+                                                    int32_t *__restrict__ pos, int n, const uint8_t *__restrict__ sel,
+                                                    int op) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n || (sel && !sel[b])) return;
+  State s = load_state(st, n, b);
+  MT m(mt + (size_t)b * kMT, pos[b]);
+  StreamDraw<MT> d{m};
+  if (op == 0) replenish(s, d);
+  else end_turn(s, d);
+  store_state(st, n, b, s);
+  pos[b] = m.cursor();
+}
+
 // ------------------------------------------------------------------ score
 __global__ void __launch_bounds__(kBlock) k_score(const uint64_t *__restrict__ st, int n, int32_t *__restrict__ out,
                                                   int32_t *__restrict__ parts) {
@@ -373,6 +388,20 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
     return launch_err();
   }
   return 0;
+}
+
+int hz_replenish(hz_env *e, const uint8_t *sel) {
+  if (!e) return -1;
+  hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,
+                     0);
+  return launch_err();
+}
+
+int hz_end_turn(hz_env *e, const uint8_t *sel) {
+  if (!e) return -1;
+  hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,
+                     1);
+  return launch_err();
 }
 
 int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_stride, const int32_t *idx, int32_t m,

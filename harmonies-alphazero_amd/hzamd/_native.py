@@ -31,6 +31,8 @@ _SIGS = {
     "hz_legal_mask": ([_vp, _vp, _vp], _c.c_int),
     "hz_step": ([_vp, _vp, _vp], _c.c_int),
     "hz_score": ([_vp, _vp, _vp], _c.c_int),
+    "hz_replenish": ([_vp, _vp], _c.c_int),
+    "hz_end_turn": ([_vp, _vp], _c.c_int),
     "hz_encode": ([_vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_rule_actions": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_encode_states": ([_vp, _c.c_int64, _c.c_int64, _vp, _c.c_int32, _vp, _vp, _vp], _c.c_int),

@@ -61,6 +61,18 @@ class BatchedEnv:
             seeds = seeds.to(device=self.device, dtype=torch.int64).contiguous()
         nat.check(nat.lib().hz_reset(self._h, nat.ptr(sel), nat.ptr(seeds)), "hz_reset")
 
+    def replenish(self, sel=None):
+        """_replenish_piles on every (selected) board."""
+        self._sync_stream()
+        sel = None if sel is None else sel.to(device=self.device, dtype=torch.uint8).contiguous()
+        nat.check(nat.lib().hz_replenish(self._h, nat.ptr(sel)), "hz_replenish")
+
+    def end_turn(self, sel=None):
+        """_end_turn_actions on every (selected) board."""
+        self._sync_stream()
+        sel = None if sel is None else sel.to(device=self.device, dtype=torch.uint8).contiguous()
+        nat.check(nat.lib().hz_end_turn(self._h, nat.ptr(sel)), "hz_end_turn")
+
     def legal_mask(self, out=None, count=None):
         """143-bit legal-action mask per board, int64 [n, 3] (bit i of word w
         = action 64*w + i) and the number of legal actions int32 [n]."""

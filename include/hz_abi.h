@@ -76,6 +76,13 @@ int hz_legal_mask(hz_env *env, uint64_t *mask, int32_t *count);
  * board is unchanged (the reference raises before committing its clone). */
 int hz_step(hz_env *env, const int16_t *action, int32_t *status);
 
+/* _replenish_piles (harmonies_engine.py:132-137) / _end_turn_actions
+ * (:301-329) on the selected boards (sel NULL = all), drawing from each
+ * board's stream.  The Python facade uses them for HarmoniesGameState() and
+ * for callers that invoke _end_turn_actions directly (text_game.py:212). */
+int hz_replenish(hz_env *env, const uint8_t *sel);
+int hz_end_turn(hz_env *env, const uint8_t *sel);
+
 /* score: calculate_score_for_player(p) (:357-367) for both players of every
  * board, out[b*2 + p].  parts (may be NULL): out_parts[(b*2+p)*5 + k] for
  * grass, mountains, fields, buildings, water (:369-523). */
