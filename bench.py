@@ -1,10 +1,11 @@
 """Benchmark: BASELINE config 2 — 4096 concurrent boards per GPU, pure env
 step / legal_actions / score HIP kernels, bit-exact vs the CPU engine.
 
-One bench step = one batched pass of the env hot path over 4096 boards:
-hz_reset (HarmoniesGameState() x 4096, CPython-exact seeding) followed by
-hz_rollout, which plays every board to its end (legal mask -> build-defined
-splitmix rule pick -> apply_move, incl. chance draws and final scoring).
+One bench step = one batched pass of the env hot path over 4096 boards, a
+single hz_play launch: HarmoniesGameState() on every board (CPython-exact
+seeding and opening draws), then play to the end of every game (legal mask ->
+build-defined splitmix rule pick -> apply_move, incl. chance draws and final
+scoring).
 Boards are seeded by their global id (rank * 4096 + b), so N GPUs run N
 independent shards (weak scaling, no data-path collective).
 
@@ -46,6 +47,10 @@ def parse():
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3],
+                    help="2: env kernels (default, the headline); 3: MCTS self-play moves with the network")
+    ap.add_argument("--sims", type=int, default=200, help="config 3: MCTS simulations per move")
+    ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     return ap.parse_args()
 
 
@@ -73,6 +78,76 @@ def cpu_baseline(boards, seconds):
                       f"C oracle with OpenMP, {nthreads} threads"}
 
 
+def bench_selfplay(args, dev, rank, world):
+    """BASELINE config 3: 4096 boards x `sims` MCTS simulations per move with
+    the default 128-filter x 8-block network (random init, torch.manual_seed(0),
+    BatchedPredictor = ModelManager.predict batched).  One step = one move of
+    every board (full search + choice + env step)."""
+    from hzamd.mcts import BatchedPredictor
+    from hzamd.net import HarmoniesNet, flops_per_eval
+    from hzamd.selfplay import SelfPlay
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = True
+    net = HarmoniesNet().to(dev).eval()
+    dtype = torch.bfloat16 if args.nn_dtype == "bf16" else None
+    pred = BatchedPredictor(net, dtype=dtype)
+    nn_ev = []
+
+    def evaluator(board, glob):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = pred(board, glob)
+        b.record()
+        nn_ev.append((a, b))
+        return out
+
+    n = args.boards
+    cfg = {"num_simulations": args.sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+           "turns_until_tau0": 15, "testing": False}
+    sp = SelfPlay(n, evaluator, cfg, seed_base=args.seed_base + rank * n, device=dev)
+    sp.env.reset()
+    for w in range(args.warmup):
+        sp.move(w)
+    torch.cuda.synchronize(dev)
+    nn_ev.clear()
+    edges = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        _, v, active = sp.move(args.warmup + k)
+        edges += int(sp.mcts.stats()[:, 1].sum().item())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    nn_ms = sum(a.elapsed_time(b) for a, b in nn_ev)
+    sims_done = n * args.sims * args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    sims_all = sims_done * world
+    per_move = elapsed / args.steps
+    avg_plies = 62.4  # SURVEY §6: mean game length
+    fl = flops_per_eval()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "self-play MCTS simulations/sec (= NN leaf evals/s) @4096 boards x 200 sims",
+            "value": sims_all / elapsed, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": per_move * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
+            "config": {"workload": f"config3: {n} boards x {args.sims} sims/move, default 128fx8 net",
+                       "boards_per_gpu": n, "sims": args.sims, "parallelism": f"shard{world}"},
+            "games_per_s_est": world * n / (per_move * avg_plies),
+            "env_steps_per_s": (edges + n * args.steps) * world / elapsed,
+            "nn_ms_per_move": nn_ms / args.steps, "tree_ms_per_move": per_move * 1e3 - nn_ms / args.steps,
+            "nn_tflops": fl * n * args.sims * args.steps / (nn_ms * 1e-3) / 1e12,
+            "note": "games/s estimated from ms per move x mean game length 62.4 plies",
+        }))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,6 +158,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+    if args.config == 3:
+        bench_selfplay(args, dev, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from hzamd.env import BatchedEnv
 
@@ -93,10 +173,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def one_step(ev=None):
-        env.reset()
+        # hz_play: HarmoniesGameState() on every board fused with rule-driven
+        # play to the end of the game, one launch
         if ev:
             ev[0].record(stream)
-        env.rollout(MAX_PLIES, games_done=games, steps_done=steps)
+        env.rollout(MAX_PLIES, games_done=games, steps_done=steps, reset=True)
         if ev:
             ev[1].record(stream)
 
@@ -139,8 +220,8 @@ def main():
     games_per_s = games_all * args.steps / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
 
-    # roofline of the dominant kernel (hz_rollout / k_rollout), per launch
-    alg_bytes = env_steps_per_step * BYTES_PER_ENV_STEP
+    # roofline of the dominant kernel (hz_play = k_rollout with reset), per launch
+    alg_bytes = env_steps_per_step * BYTES_PER_ENV_STEP + games_per_step * BYTES_PER_RESET
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -173,7 +254,7 @@ def main():
             "dtype": "u64",
             "data": "synthetic: CPython-seeded games, seeds = global board id, build-defined splitmix rule policy",
             "config": {"workload": "config2: 4096 concurrent boards/GPU, reset + rule-driven play to game end "
-                                   "(legal mask, step, chance draws, final scoring), fused hz_rollout",
+                                   "(legal mask, step, chance draws, final scoring), one hz_play launch",
                        "boards_per_gpu": n, "env_steps_per_step": env_steps_per_step,
                        "games_per_step": games_per_step, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

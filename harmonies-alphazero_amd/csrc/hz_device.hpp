@@ -295,46 +295,131 @@ __device__ __forceinline__ uint32_t twist_word(uint32_t cur, uint32_t next, uint
 template <int S>
 struct MTS {
   uint32_t* w;  // word i at w[i * S]
-  int pos, tw;
+  int pos, tw;  // CPython index; words of this generation twisted in place
+  // Register window of TEMPERED outputs in three 8-word blocks A, B, C:
+  // slot t holds word base + t, slots [0, nw) are filled (blocks fill in
+  // order; only the generation's last block is short) and off = pos - base
+  // of them are consumed.  prefetch() tops the window up to 24 words at the
+  // start of every draw, where all lanes of the wave are together, so the
+  // wave pays one memory round trip for everybody's refill; a draw needs more
+  // than 24 words with probability ~1e-5 per lane.  Only static register
+  // indices are used (a dynamic index would move the stream to scratch), and
+  // a stored word is never re-read (vmcnt counts stores on CDNA).
+  uint32_t a0, a1, a2, a3, a4, a5, a6, a7;
+  uint32_t b0, b1, b2, b3, b4, b5, b6, b7;
+  uint32_t c0, c1, c2, c3, c4, c5, c6, c7;
+  int nw, off;
 
-  __device__ __forceinline__ MTS(uint32_t* words, int cursor) : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
+  __device__ __forceinline__ MTS(uint32_t* words, int cursor)
+      : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16), a0(0), a1(0), a2(0), a3(0), a4(0), a5(0), a6(0),
+        a7(0), b0(0), b1(0), b2(0), b3(0), b4(0), b5(0), b6(0), b7(0), c0(0), c1(0), c2(0), c3(0), c4(0), c5(0),
+        c6(0), c7(0), nw(0), off(0) {}
   __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
 
-  // twist words [tw, tw + k), k <= 8: every source word is either already
-  // new (index < tw) or still old (index >= tw + k), so all 17 loads issue
-  // together.
-  __device__ __forceinline__ void advance() {
-    int k = kMT - tw < 8 ? kMT - tw : 8;
+  // Raw words [start, start + k), k = min(8, 624 - start), start <= tw: words
+  // below tw are loaded, the rest twisted (their sources are new below tw,
+  // old from tw on) and stored.  All 17 loads issue together.  Returns the
+  // tempered outputs in o[].
+  __device__ __forceinline__ int fill(int start, uint32_t o[8]) {
+    int k = kMT - start < 8 ? kMT - start : 8;
     uint32_t cur[9], far[8];
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      int i = tw + j;
+      int i = start + j;
       cur[j] = (j <= k) ? w[(i < kMT ? i : 0) * S] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      int i = tw + j;
+      int i = start + j;
       int fi = i < 227 ? i + 397 : (i < 623 ? i - 227 : 396);
-      far[j] = (j < k) ? w[fi * S] : 0u;
+      far[j] = (j < k && i >= tw) ? w[fi * S] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      if (j < k) w[(tw + j) * S] = twist_word(cur[j], cur[j + 1], far[j]);
+      int i = start + j;
+      o[j] = (i < tw) ? cur[j] : twist_word(cur[j], cur[j + 1], far[j]);
     }
-    tw += k;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      int i = start + j;
+      if (j < k && i >= tw) w[i * S] = o[j];
+    }
+    if (start + k > tw) tw = start + k;
+#pragma unroll
+    for (int j = 0; j < 8; j++) o[j] = temper(o[j]);
+    return k;
   }
 
-  // genrand_uint32
+  // drop fully consumed leading blocks
+  __device__ __forceinline__ void compact() {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      if (off >= 8 && nw >= 8) {
+        a0 = b0; a1 = b1; a2 = b2; a3 = b3; a4 = b4; a5 = b5; a6 = b6; a7 = b7;
+        b0 = c0; b1 = c1; b2 = c2; b3 = c3; b4 = c4; b5 = c5; b6 = c6; b7 = c7;
+        off -= 8;
+        nw -= 8;
+      }
+    }
+    if (off >= nw) { off = 0; nw = 0; }
+  }
+
+  __device__ __forceinline__ void prefetch() {
+    compact();
+    if (pos >= kMT) { pos = 0; tw = 0; nw = off = 0; }  // the window is empty here
+    uint32_t o[8];
+    int base = pos - off;
+    if (nw == 0) {
+      nw = fill(base, o);
+      a0 = o[0]; a1 = o[1]; a2 = o[2]; a3 = o[3]; a4 = o[4]; a5 = o[5]; a6 = o[6]; a7 = o[7];
+    }
+    if (nw == 8 && base + 8 < kMT) {
+      nw += fill(base + 8, o);
+      b0 = o[0]; b1 = o[1]; b2 = o[2]; b3 = o[3]; b4 = o[4]; b5 = o[5]; b6 = o[6]; b7 = o[7];
+    }
+    if (nw == 16 && base + 16 < kMT) {
+      nw += fill(base + 16, o);
+      c0 = o[0]; c1 = o[1]; c2 = o[2]; c3 = o[3]; c4 = o[4]; c5 = o[5]; c6 = o[6]; c7 = o[7];
+    }
+  }
+
+  __device__ __forceinline__ uint32_t win(int t) const {  // t is a compile-time constant after unrolling
+    switch (t) {
+      case 0: return a0; case 1: return a1; case 2: return a2; case 3: return a3;
+      case 4: return a4; case 5: return a5; case 6: return a6; case 7: return a7;
+      case 8: return b0; case 9: return b1; case 10: return b2; case 11: return b3;
+      case 12: return b4; case 13: return b5; case 14: return b6; case 15: return b7;
+      case 16: return c0; case 17: return c1; case 18: return c2; case 19: return c3;
+      case 20: return c4; case 21: return c5; case 22: return c6; default: return c7;
+    }
+  }
+
+  __device__ __forceinline__ bool live(int t) const { return t >= off && t < nw; }
+
+  __device__ __forceinline__ void consume(int c) {
+    pos += c;
+    off += c;
+  }
+
+  // genrand_uint32 one word at a time (slow path; drops the window)
   __device__ __forceinline__ uint32_t next() {
+    nw = off = 0;
     if (pos >= kMT) { pos = 0; tw = 0; }
-    if (pos >= tw) advance();
+    if (pos >= tw) {
+      uint32_t o[8];
+      fill(pos, o);
+      pos++;
+      return o[0];
+    }
     return temper(w[(pos++) * S]);
   }
 
   // finish the current generation's twist (CPython form afterwards)
   __device__ __forceinline__ void normalize() {
     if (pos >= kMT) return;
-    while (tw < kMT) advance();
+    uint32_t o[8];
+    while (tw < kMT) fill(tw, o);
+    nw = off = 0;
   }
 };
 using MT = MTS<1>;
@@ -357,17 +442,17 @@ __device__ __forceinline__ void mt_seed(uint32_t* w, int stride, uint64_t seed) 
     if (++j >= klen) j = 0;
   }
   uint32_t mt0 = prev;
-  uint32_t nxt = w[1 * stride];
-  prev = (nxt ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
+  uint32_t m1 = w[1 * stride];
+  prev = (m1 ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
   w[1 * stride] = prev;
-  // second pass: 623 steps starting at i = 2 (next word preloaded)
-  nxt = w[2 * stride];
+  // second pass: 623 steps starting at i = 2, reading 4 words ahead
+  uint32_t r0 = w[2 * stride], r1 = w[3 * stride], r2 = w[4 * stride], r3 = w[5 * stride];
   for (int i = 2; i < kMT; i++) {
-    uint32_t after = i + 1 < kMT ? w[(i + 1) * stride] : 0u;
-    uint32_t v = (nxt ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    uint32_t after = i + 4 < kMT ? w[(i + 4) * stride] : 0u;
+    uint32_t v = (r0 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
     w[i * stride] = v;
     prev = v;
-    nxt = after;
+    r0 = r1; r1 = r2; r2 = r3; r3 = after;
   }
   mt0 = prev;  // mt[0] = mt[623]
   w[1 * stride] = (w[1 * stride] ^ ((mt0 ^ (mt0 >> 30)) * 1566083941U)) - 1U;
@@ -383,40 +468,69 @@ __device__ __forceinline__ uint32_t randbelow(M& m, uint32_t n) {
   return r;
 }
 
-// random.sample(range(n), k), k <= 3 (so setsize = 21, random.py:484-486).
+// random.sample(range(n), k), k <= 3 (so setsize = 21, random.py:484-486),
+// one word at a time (slow path); resumes after `got` picks.
 template <class M>
-__device__ __forceinline__ void sample3(M& m, uint32_t n, int k, uint32_t out[3]) {
+__device__ __forceinline__ void sample3_serial(M& m, uint32_t n, int k, uint32_t j[3], int got) {
   if (n <= 21) {
-    // pool method; pool[x] == x except at <= 3 recorded positions
-    uint32_t mp[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mv[3] = {0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      if (i >= k) break;
-      uint32_t j = randbelow(m, n - (uint32_t)i);
-      uint32_t last = n - (uint32_t)i - 1;
-      uint32_t vj = j, vl = last;
-#pragma unroll
-      for (int q = 0; q < 3; q++) {
-        if (q < i && mp[q] == j) vj = mv[q];
-        if (q < i && mp[q] == last) vl = mv[q];
-      }
-      out[i] = vj;
-      mp[i] = j;
-      mv[i] = vl;
-    }
+    for (int i = got; i < k; i++) j[i] = randbelow(m, n - (uint32_t)i);
   } else {
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      if (i >= k) break;
-      uint32_t j;
+    for (int i = got; i < k; i++) {
+      uint32_t v;
       bool dup;
       do {
-        j = randbelow(m, n);
-        dup = (i > 0 && out[0] == j) || (i > 1 && out[1] == j);
+        v = randbelow(m, n);
+        dup = (i > 0 && j[0] == v) || (i > 1 && j[1] == v);
       } while (dup);
-      out[i] = j;
+      j[i] = v;
     }
   }
+}
+
+// The raw picks of random.sample(range(n), k): the set method (n > 21) keeps
+// every value < n not already taken; the pool method (n <= 21) takes the
+// i-th value < n - i.  A word whose value is out of range is rejected
+// (_randbelow, random.py:239-249).  Branch-free scan of the register window
+// (the wave leaves early once every lane has its picks).
+template <class M>
+__device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[3]) {
+  uint32_t j0 = 0, j1 = 0, j2 = 0;
+  int got = 0, used = 0;
+  if (__all(n > 21)) {
+    int sh = __clz(n);
+#pragma unroll
+    for (int t = 0; t < 24; t++) {
+      if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
+      bool lv = m.live(t) && got < k;
+      uint32_t v = m.win(t) >> sh;  // getrandbits(bit_length(n))
+      bool ok = lv && v < n && (got < 1 || v != j0) && (got < 2 || v != j1);
+      j0 = (ok && got == 0) ? v : j0;
+      j1 = (ok && got == 1) ? v : j1;
+      j2 = (ok && got == 2) ? v : j2;
+      used += lv ? 1 : 0;
+      got += ok ? 1 : 0;
+    }
+  } else {
+    bool pool = n <= 21;
+    int sh0 = __clz(n), sh1 = __clz(n > 1 ? n - 1 : 1), sh2 = __clz(n > 2 ? n - 2 : 1);
+#pragma unroll
+    for (int t = 0; t < 24; t++) {
+      if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
+      bool lv = m.live(t) && got < k;
+      int sh = pool ? (got == 0 ? sh0 : got == 1 ? sh1 : sh2) : sh0;
+      uint32_t lim = pool ? n - (uint32_t)got : n;
+      uint32_t v = m.win(t) >> sh;
+      bool ok = lv && v < lim && (pool || ((got < 1 || v != j0) && (got < 2 || v != j1)));
+      j0 = (ok && got == 0) ? v : j0;
+      j1 = (ok && got == 1) ? v : j1;
+      j2 = (ok && got == 2) ? v : j2;
+      used += lv ? 1 : 0;
+      got += ok ? 1 : 0;
+    }
+  }
+  m.consume(used);
+  j[0] = j0; j[1] = j1; j[2] = j2;
+  if (got < k) sample3_serial(m, n, k, j, got);  // window exhausted (rare)
 }
 
 // _draw_tiles(3) (harmonies_engine.py:120-130): flat_bag follows the bag's
@@ -434,8 +548,28 @@ __device__ __forceinline__ int draw_pile(uint64_t misc, M& m, uint32_t& pile9) {
   pile9 = 0x1FF;
   if (!n) return 0;
   int k = n < 3 ? (int)n : 3;
-  uint32_t idx[3] = {0, 0, 0};
-  sample3(m, n, k, idx);
+  uint32_t j[3] = {0, 0, 0};
+  sample3_raw(m, n, k, j);
+  uint32_t idx[3];
+  if (n <= 21) {
+    // pool method bookkeeping: result[i] = pool[j_i]; pool[j_i] = pool[n-i-1];
+    // pool[x] == x except at <= 3 recorded positions (random.py:488-493)
+    uint32_t mp0 = 0xffffffffu, mp1 = 0xffffffffu, mv0 = 0, mv1 = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      uint32_t ji = j[i], last = n - (uint32_t)i - 1;
+      uint32_t vj = ji, vl = last;
+      if (i > 0 && mp0 == ji) vj = mv0;
+      if (i > 1 && mp1 == ji) vj = mv1;
+      if (i > 0 && mp0 == last) vl = mv0;
+      if (i > 1 && mp1 == last) vl = mv1;
+      idx[i] = vj;
+      if (i == 0) { mp0 = ji; mv0 = vl; }
+      if (i == 1) { mp1 = ji; mv1 = vl; }
+    }
+  } else {
+    idx[0] = j[0]; idx[1] = j[1]; idx[2] = j[2];
+  }
   const int order[6] = {WATER, PLANT, WOOD, STONE, FIELD, BUILDING};
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -465,10 +599,13 @@ __device__ __forceinline__ void apply_pile(uint64_t& misc, uint32_t pile9) {
 }
 
 // Sources of piles for _replenish_piles: the live stream ...
+// (holds the stream by value: a reference member would force the stream
+// state out of registers into scratch)
 template <class M>
 struct StreamDraw {
-  M& m;
+  M m;
   __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
+    m.prefetch();  // the one point where the wave's refills line up
     uint32_t p9;
     return draw_pile(misc, m, p9) ? p9 : 0x1FFu;
   }
@@ -506,14 +643,13 @@ __device__ __forceinline__ uint64_t replenish(State& s, Draw& draw) {
 
 // HarmoniesGameState.__init__ (:66-79)
 template <class M>
-__device__ __forceinline__ void reset_state(State& s, M& m) {
+__device__ __forceinline__ void reset_state(State& s, StreamDraw<M>& d) {
   s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
   s.piles = (1ull << 45) - 1;  // every tile slot = 7 (none), 0 piles
   uint64_t misc = 0x1FF;        // empty hand
 #pragma unroll
   for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
   s.misc = misc;  // player 0, choose_pile, not over, winner None, scores 0
-  StreamDraw<M> d{m};
   replenish(s, d);
 }
 

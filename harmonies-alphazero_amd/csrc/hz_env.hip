@@ -27,6 +27,32 @@ struct hz_env {
   uint64_t *seed;    // [n]
 };
 
+#ifdef HZ_DIAG
+// diagnostic build only (tools/diag.py): per-lane phase clocks
+__device__ uint64_t *g_stamps;
+#define HZ_STAMP(slot)                                                    \
+  do {                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                    \
+    if (g_stamps) g_stamps[(size_t)b * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                    \
+  } while (0)
+#define HZ_ACC(slot, t0)                                                  \
+  do {                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                    \
+    uint64_t _t = __builtin_amdgcn_s_memtime();                           \
+    acc##slot += _t - (t0);                                               \
+    t0 = _t;                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                    \
+  } while (0)
+#else
+#define HZ_STAMP(slot) \
+  do {                 \
+  } while (0)
+#define HZ_ACC(slot, t0) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int kBlock = 64;  // one wave per workgroup: 4096 boards -> 64 waves
@@ -61,12 +87,15 @@ __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uin
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       episode[b] = e + 1;
     }
+    HZ_STAMP(0);
     mt_seed(lds + lane, kLdsStride, sd);
-    MTS<kLdsStride> m(lds + lane, kMTSeeded);
+    HZ_STAMP(1);
+    StreamDraw<MTS<kLdsStride>> d{MTS<kLdsStride>(lds + lane, kMTSeeded)};
     State s;
-    reset_state(s, m);
+    reset_state(s, d);
+    HZ_STAMP(2);
     store_state(st, n, b, s);
-    pos[b] = m.cursor();
+    pos[b] = d.m.cursor();
     ply[b] = 0;
     seed[b] = sd;
   }
@@ -74,10 +103,25 @@ __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uin
   __syncthreads();
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
   uint32_t *g = mt + (size_t)b0 * kMT;
-  for (int o = lane; o < nb * kMT; o += kBlock) {
-    int bl = o / kMT, i = o - bl * kMT;
-    if ((actmask >> bl) & 1) g[o] = lds[i * kLdsStride + bl];
+  HZ_STAMP(3);
+  // board by board: lanes copy words lane, lane + 64, ... (LDS banks distinct,
+  // 256 B coalesced stores, ten LDS reads in flight per board)
+  for (int bl = 0; bl < nb; bl++) {
+    if (!((actmask >> bl) & 1)) continue;
+    uint32_t v[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      int i = lane + kBlock * k;
+      v[k] = i < kMT ? lds[i * kLdsStride + bl] : 0u;
+    }
+    uint32_t *gb = g + (size_t)bl * kMT;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      int i = lane + kBlock * k;
+      if (i < kMT) gb[i] = v[k];
+    }
   }
+  HZ_STAMP(4);
 }
 
 // ------------------------------------------------------------- legal mask
@@ -107,12 +151,11 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
     return;
   }
   State s = load_state(st, n, b);
-  MT m(mt + (size_t)b * kMT, pos[b]);
-  StreamDraw<MT> d{m};
+  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
-    pos[b] = m.cursor();
+    pos[b] = d.m.cursor();
     ply[b] += 1;
   }
   if (status) status[b] = r;
@@ -125,12 +168,11 @@ __global__ void __launch_bounds__(kBlock) k_turn_op(uint64_t *__restrict__ st, u
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n || (sel && !sel[b])) return;
   State s = load_state(st, n, b);
-  MT m(mt + (size_t)b * kMT, pos[b]);
-  StreamDraw<MT> d{m};
+  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
   if (op == 0) replenish(s, d);
   else end_turn(s, d);
   store_state(st, n, b, s);
-  pos[b] = m.cursor();
+  pos[b] = d.m.cursor();
 }
 
 // ------------------------------------------------------------------ score
@@ -163,65 +205,148 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 }
 
 // ---------------------------------------------------------------- rollout
+// Lane-per-board with the block's 64 MT streams resident in LDS for the
+// whole call ([624][65] words, as in k_reset): every draw reads and twists at
+// LDS latency instead of paying a scattered HBM round trip per draw.  The
+// streams are staged in (or seeded in place when reset_first) and written
+// back once.
+__device__ __forceinline__ void stage_mt(uint32_t *__restrict__ lds, uint32_t *__restrict__ g, int nb, int lane,
+                                         uint64_t actmask, bool to_lds) {
+  // the block's streams are one contiguous span of nb * 624 words in HBM
+  int total4 = nb * (kMT / 4);
+  for (int q0 = 0; q0 < total4; q0 += kBlock * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int q = q0 + u * kBlock + lane;
+      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
+      if (q < total4 && ((actmask >> bl) & 1)) {
+        if (to_lds) {
+          v[u] = reinterpret_cast<const uint4 *>(g)[q];
+        } else {
+          v[u].x = lds[i * kLdsStride + bl];
+          v[u].y = lds[(i + 1) * kLdsStride + bl];
+          v[u].z = lds[(i + 2) * kLdsStride + bl];
+          v[u].w = lds[(i + 3) * kLdsStride + bl];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int q = q0 + u * kBlock + lane;
+      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
+      if (q < total4 && ((actmask >> bl) & 1)) {
+        if (to_lds) {
+          lds[i * kLdsStride + bl] = v[u].x;
+          lds[(i + 1) * kLdsStride + bl] = v[u].y;
+          lds[(i + 2) * kLdsStride + bl] = v[u].z;
+          lds[(i + 3) * kLdsStride + bl] = v[u].w;
+        } else {
+          reinterpret_cast<uint4 *>(g)[q] = v[u];
+        }
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                     int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                     int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
                                                     int n, uint64_t seed_base, int max_plies, int auto_reset,
-                                                    uint64_t *__restrict__ traj_state, uint64_t *__restrict__ traj_mask,
+                                                    int reset_first, uint64_t *__restrict__ traj_state,
+                                                    uint64_t *__restrict__ traj_mask,
                                                     int16_t *__restrict__ traj_action, int32_t *__restrict__ games_done,
                                                     int32_t *__restrict__ steps_done) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  MT m(mt + (size_t)b * kMT, pos[b]);
-  StreamDraw<MT> draw{m};
-  State s = load_state(st, n, b);
-  int g_ply = ply[b], games = 0, steps = 0;
-  uint64_t sd = seed[b];
-  for (int i = 0; i < max_plies; i++) {
-    if (game_done(s.misc)) {
-      if (!auto_reset) {
-        if (traj_action) {
-          for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
-        }
-        break;
-      }
+  extern __shared__ uint32_t lds[];
+  int lane = threadIdx.x;
+  int b0 = blockIdx.x * kBlock;
+  int b = b0 + lane;
+  bool act = b < n;
+  uint64_t actmask = __ballot(act);
+  int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  uint32_t *g = mt + (size_t)b0 * kMT;
+  if (!reset_first) stage_mt(lds, g, nb, lane, actmask, true);
+  __syncthreads();
+  if (act) {
+    StreamDraw<MTS<kLdsStride>> draw{MTS<kLdsStride>(lds + lane, reset_first ? kMTSeeded : pos[b])};
+    State s;
+    int g_ply, games = 0, steps = 0;
+    uint64_t sd;
+    if (reset_first) {
       int e = episode[b];
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       episode[b] = e + 1;
-      mt_seed(m.w, 1, sd);
-      m.pos = kMT;
-      m.tw = kMT;
-      reset_state(s, m);
+      mt_seed(lds + lane, kLdsStride, sd);
+      reset_state(s, draw);
       g_ply = 0;
+    } else {
+      s = load_state(st, n, b);
+      g_ply = ply[b];
+      sd = seed[b];
     }
-    uint64_t mk[3];
-    int L = legal_mask(s, mk);
-    if (traj_state) {
-      uint64_t *o = traj_state + (size_t)i * 6 * n + b;
-      o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
-      o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+#ifdef HZ_DIAG
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    uint64_t acc8 = 0, acc9 = 0, acc10 = 0, acc11 = 0, acc12 = 0;
+#endif
+    for (int i = 0; i < max_plies; i++) {
+      if (game_done(s.misc)) {
+        if (!auto_reset) {
+          if (traj_action) {
+            for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
+          }
+          break;
+        }
+        int e = episode[b];
+        sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+        episode[b] = e + 1;
+        mt_seed(lds + lane, kLdsStride, sd);
+        draw.m = MTS<kLdsStride>(lds + lane, kMTSeeded);
+        reset_state(s, draw);
+        g_ply = 0;
+      }
+      uint64_t mk[3];
+      HZ_ACC(8, t0);
+      int L = legal_mask(s, mk);
+      HZ_ACC(9, t0);
+      if (traj_state) {
+        uint64_t *o = traj_state + (size_t)i * 6 * n + b;
+        o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
+        o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+      }
+      if (traj_mask) {
+        uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
+        o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+      }
+      if (L == 0) {  // stuck board (unreachable from HarmoniesGameState())
+        if (traj_action) traj_action[(size_t)i * n + b] = -1;
+        break;
+      }
+      int a = kth_action(mk, rule_pick(sd, g_ply, L));
+      if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
+      HZ_ACC(10, t0);
+      bool te = phase_of(s.misc) == PH_P3;
+      step_state(s, a, draw);
+      if (te) HZ_ACC(12, t0);
+      else HZ_ACC(11, t0);
+      g_ply++;
+      steps++;
+      if (game_done(s.misc)) games++;
     }
-    if (traj_mask) {
-      uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
-      o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+    store_state(st, n, b, s);
+    pos[b] = draw.m.cursor();
+    ply[b] = g_ply;
+    seed[b] = sd;
+#ifdef HZ_DIAG
+    if (g_stamps) {
+      uint64_t *o = g_stamps + (size_t)b * 16;
+      o[8] = acc8; o[9] = acc9; o[10] = acc10; o[11] = acc11; o[12] = acc12;
     }
-    if (L == 0) {  // stuck board (unreachable from HarmoniesGameState())
-      if (traj_action) traj_action[(size_t)i * n + b] = -1;
-      break;
-    }
-    int a = kth_action(mk, rule_pick(sd, g_ply, L));
-    if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
-    step_state(s, a, draw);
-    g_ply++;
-    steps++;
-    if (game_done(s.misc)) games++;
+#endif
+    if (games_done) games_done[b] = games;
+    if (steps_done) steps_done[b] = steps;
   }
-  store_state(st, n, b, s);
-  pos[b] = m.cursor();
-  ply[b] = g_ply;
-  seed[b] = sd;
-  if (games_done) games_done[b] = games;
-  if (steps_done) steps_done[b] = steps;
+  __syncthreads();
+  stage_mt(lds, g, nb, lane, actmask, false);
 }
 
 // ---------------------------------------------------------- state transfer
@@ -260,9 +385,11 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   e->seed_base = seed_base;
   e->stream = (hipStream_t)stream;
   size_t n = (size_t)n_boards;
-  // k_reset stages 64 boards' MT words in 158 KiB of LDS
+  // k_reset / k_rollout stage 64 boards' MT words in 158 KiB of LDS
   if (hipFuncSetAttribute((const void *)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
-      hipSuccess) {
+          hipSuccess ||
+      hipFuncSetAttribute((const void *)k_rollout, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
+          hipSuccess) {
     free(e);
     return nullptr;
   }
@@ -352,13 +479,23 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
   return launch_err();
 }
 
+static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
+                          uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
+  if (!e || max_plies < 0) return -1;
+  hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kBlock), kResetLds, e->stream, e->state, e->mt, e->pos,
+                     e->ply, e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
+                     traj_mask, traj_action, games_done, steps_done);
+  return launch_err();
+}
+
 int hz_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state, uint64_t *traj_mask,
                int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
-  if (!e || max_plies < 0) return -1;
-  hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
-                     e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, traj_state, traj_mask,
-                     traj_action, games_done, steps_done);
-  return launch_err();
+  return launch_rollout(e, max_plies, auto_reset, 0, traj_state, traj_mask, traj_action, games_done, steps_done);
+}
+
+int hz_play(hz_env *e, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state, uint64_t *traj_mask,
+            int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
+  return launch_rollout(e, max_plies, auto_reset, 1, traj_state, traj_mask, traj_action, games_done, steps_done);
 }
 
 int hz_export_state(hz_env *e, uint64_t *state, uint32_t *mt, int32_t *mt_index) {
@@ -413,5 +550,11 @@ int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_s
 }
 
 const char *hz_version(void) { return "hz 0.1 gfx950"; }
+
+#ifdef HZ_DIAG
+int hz_diag_set_stamps(uint64_t *p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 }  // extern "C"

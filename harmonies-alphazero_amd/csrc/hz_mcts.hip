@@ -239,13 +239,12 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
         for (int i = lane; i < kMT; i += kWave) L.mt[i] = g[i];
         __syncthreads();
         if (lane == 0) {
-          MT mt(L.mt, mtcur[b]);
-          StreamDraw<MT> draw{mt};
+          StreamDraw<MT> draw{MT(L.mt, mtcur[b])};
           for (int c = 0; c < nl; c++) {
             State tmp = ls;
             L.script[c] = replenish(tmp, draw);
           }
-          mtcur[b] = mt.cursor();
+          mtcur[b] = draw.m.cursor();
         }
         __syncthreads();
         for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libhz.so")
+LIB_PATH = os.environ.get("HZ_LIB") or os.path.join(PKG_DIR, "libhz.so")  # HZ_LIB: diagnostic builds
 
 _lib = None
 
@@ -37,6 +37,7 @@ _SIGS = {
     "hz_rule_actions": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_encode_states": ([_vp, _c.c_int64, _c.c_int64, _vp, _c.c_int32, _vp, _vp, _vp], _c.c_int),
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
+    "hz_play": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_export_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_import_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_mcts_create": ([_c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _vp], _vp),

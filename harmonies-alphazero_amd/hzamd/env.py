@@ -129,8 +129,9 @@ class BatchedEnv:
                   "hz_rule_actions")
         return out
 
-    def rollout(self, max_plies, auto_reset=False, record=False, games_done=None, steps_done=None):
-        """Fused rule-driven play of up to max_plies plies per board."""
+    def rollout(self, max_plies, auto_reset=False, record=False, games_done=None, steps_done=None, reset=False):
+        """Fused rule-driven play of up to max_plies plies per board
+        (reset=True: start every board's next game first, in the same launch)."""
         self._sync_stream()
         traj = None
         if record:
@@ -140,8 +141,9 @@ class BatchedEnv:
         games_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if games_done is None else games_done
         steps_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if steps_done is None else steps_done
         ts, tm, ta = traj if traj else (None, None, None)
-        nat.check(nat.lib().hz_rollout(self._h, int(max_plies), int(bool(auto_reset)), nat.ptr(ts), nat.ptr(tm),
-                                       nat.ptr(ta), nat.ptr(games_done), nat.ptr(steps_done)), "hz_rollout")
+        fn = nat.lib().hz_play if reset else nat.lib().hz_rollout
+        nat.check(fn(self._h, int(max_plies), int(bool(auto_reset)), nat.ptr(ts), nat.ptr(tm), nat.ptr(ta),
+                     nat.ptr(games_done), nat.ptr(steps_done)), "hz_play" if reset else "hz_rollout")
         return games_done, steps_done, traj
 
     # -- state transfer -------------------------------------------------------

@@ -63,9 +63,33 @@ class SelfPlay:
         self.noise_log = []
         self.step_counter = 0
 
+    def move(self, ply, done=None):
+        """One ply for every board that is still playing: search, choose,
+        step.  Returns (state words before the move, visits, active mask)."""
+        env, n, d, cfg = self.env, self.n, self.device, self.cfg
+        testing = bool(cfg.get("testing", False))
+        done = env.done() if done is None else done
+        active = ~done
+        st = env.export_state()
+        _, count = env.legal_mask()
+        noise, u = self.noise.draw(self.step_counter, count, cfg["dirichlet_alpha"])
+        self.step_counter += 1
+        v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
+                             eps=cfg["dirichlet_epsilon"], testing=testing)
+        explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
+        act = choose_actions(v, explore, u)
+        if self.keep_noise:
+            self.noise_log.append((noise.clone(), u.clone(), act.clone()))
+        act = torch.where(active, act, torch.full_like(act, -1)).to(torch.int16)
+        status = env.step(act)
+        bad = active & (status != 0)
+        if bool(bad.any()):
+            raise RuntimeError(f"self-play step failed on boards {torch.nonzero(bad).flatten().tolist()[:8]}")
+        return st, v, active
+
     def play(self, reset=True):
         """Play one game on every board; returns the device records."""
-        env, n, d, cfg = self.env, self.n, self.device, self.cfg
+        env, n, d = self.env, self.n, self.device
         if reset:
             env.reset()
         T = self.max_plies
@@ -73,30 +97,14 @@ class SelfPlay:
         players = torch.zeros(T, n, dtype=torch.int8, device=d)
         visits = torch.zeros(T, n, 143, dtype=torch.int32, device=d)
         valid = torch.zeros(T, n, dtype=torch.bool, device=d)
-        testing = bool(cfg.get("testing", False))
         done = env.done()
         ply = 0
         while ply < T and not bool(done.all()):
-            active = ~done
-            st = env.export_state()
+            st, v, active = self.move(ply, done)
             states[ply] = st
             players[ply] = ((st[5] >> 41) & 1).to(torch.int8)
             valid[ply] = active
-            _, count = env.legal_mask()
-            noise, u = self.noise.draw(self.step_counter, count, cfg["dirichlet_alpha"])
-            self.step_counter += 1
-            v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
-                                 eps=cfg["dirichlet_epsilon"], testing=testing)
-            explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
-            act = choose_actions(v, explore, u)
-            if self.keep_noise:
-                self.noise_log.append((noise.clone(), u.clone(), act.clone()))
             visits[ply] = v
-            act = torch.where(active, act, torch.full_like(act, -1)).to(torch.int16)
-            status = env.step(act)
-            bad = active & (status != 0)
-            if bool(bad.any()):
-                raise RuntimeError(f"self-play step failed on boards {torch.nonzero(bad).flatten().tolist()[:8]}")
             done = env.done()
             ply += 1
         final = env.export_state()
@@ -110,17 +118,35 @@ class SelfPlay:
         return torch.where(win == 1, 1, torch.where(win == 2, -1, 0)).to(torch.float32)
 
     def compact(self, rec):
-        """Flatten the valid records: states int64 [M, 6], pi f32 [M, 143],
-        z f32 [M] (trainer.py:517-538), board id int32 [M]."""
+        """Flatten the valid records: states int64 [M, 6], visits int32
+        [M, 143], pi f32 [M, 143], z f32 [M] (trainer.py:517-538), player
+        int8 [M], board id int32 [M]."""
         out = self.outcomes(rec["final"])                       # [n]
         T = rec["plies"]
         mask = rec["valid"]                                      # [T, n]
         player = rec["players"].to(torch.float32)
         z = torch.where(player == 0, out.unsqueeze(0), -out.unsqueeze(0))  # 0 stays 0 for draws
         states = rec["states"].permute(0, 2, 1)[mask]            # [M, 6]
-        pi = pi_from_visits(rec["visits"][mask])                 # [M, 143]
+        visits = rec["visits"][mask]
+        pi = pi_from_visits(visits)                              # [M, 143]
         board_id = torch.arange(self.n, device=self.device).expand(T, self.n)[mask].to(torch.int32)
-        return {"states": states.contiguous(), "pi": pi, "z": z[mask].contiguous(), "board": board_id}
+        return {"states": states.contiguous(), "visits": visits, "pi": pi, "z": z[mask].contiguous(),
+                "player": rec["players"][mask], "board": board_id}
+
+    def iteration(self, buffer=None, group=None):
+        """One self-play phase: every board plays a game; with torch.distributed
+        initialised the packed records of all ranks are all-gathered (RCCL)
+        into `buffer` (a distributed.ReplayBuffer) on every rank."""
+        from . import distributed as hd
+        import torch.distributed as dist
+        rec = self.play()
+        comp = self.compact(rec)
+        packed = hd.pack_records(comp["states"], comp["visits"], comp["z"], comp["player"])
+        if dist.is_available() and dist.is_initialized():
+            packed = hd.all_gather_records(packed, group)
+        if buffer is not None:
+            buffer.extend(packed)
+        return packed, rec
 
     def examples(self, compact):
         """The reference's replay-buffer tuples (trainer.py:529-538), on CPU."""

@@ -112,6 +112,11 @@ int hz_rule_actions(hz_env *env, const uint64_t *mask, const int32_t *count, int
 int hz_rollout(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state,
                uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done,
                int32_t *steps_done);
+/* hz_reset (all boards) fused with hz_rollout in one launch: the chance
+ * streams are seeded and consumed in LDS and written to HBM once. */
+int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state,
+            uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done,
+            int32_t *steps_done);
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
 /* export: state[6][n] and, optionally, the MT streams in CPython getstate()

@@ -138,6 +138,23 @@ def test_full_size_4096_vs_oracle(Env):
     assert (score[:, 0] == finals[:, 76]).all() and (score[:, 1] == finals[:, 77]).all()
 
 
+def test_fused_play_and_staged_continue(Env):
+    """hz_play (reset fused into the rollout, streams seeded in LDS) and a
+    rollout continued from mid-game (streams staged HBM -> LDS -> HBM)."""
+    n, base = 4096, 4321
+    env = Env(n, seed_base=base, device=DEV)
+    games, steps, _ = env.rollout(21, reset=True)
+    assert (games.cpu().numpy() == 0).all() and (steps.cpu().numpy() == 21).all()
+    games2, steps2, _ = env.rollout(200)
+    total, finals, plies, nxt = oracle.play_rule_games(n, base, nthreads=8)
+    assert (states_of(env) == finals).all()
+    assert ((steps.cpu().numpy() + steps2.cpu().numpy()) == plies).all()
+    _, mt, idx = env.export_state(with_mt=True)
+    mt, idx = mt.cpu().numpy().view(np.uint32), idx.cpu().numpy()
+    for b in range(0, n, 97):
+        assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b]
+
+
 def test_auto_reset_steady_state(Env):
     """auto_reset: board b's k-th game is seeded seed_base + b + (k << 32)."""
     n, base, plies = 256, 31, 150

@@ -1,0 +1,33 @@
+"""Phase attribution for k_reset / k_rollout from the HZ_DIAG build
+(tools/libhz_diag.so): per-lane s_memtime stamps, reported in cycles."""
+import ctypes, json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["HZ_LIB"] = os.path.join(ROOT, "tools", "libhz_diag.so")
+sys.path.insert(0, os.path.join(ROOT, "harmonies-alphazero_amd"))
+import torch
+import hzamd._native as nat
+from hzamd.env import BatchedEnv
+
+n = 4096
+L = nat.lib()
+L.hz_diag_set_stamps.argtypes = [ctypes.c_void_p]
+stamps = torch.zeros(n, 16, dtype=torch.int64, device="cuda")
+L.hz_diag_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
+env = BatchedEnv(n, device="cuda")
+out = {}
+for rep in range(3):
+    stamps.zero_()
+    a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    a.record(); env.reset(); b.record(); env.rollout(96); c.record()
+    f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    f0.record(); env.rollout(96, reset=True); f1.record()
+    torch.cuda.synchronize()
+    s = stamps.cpu().double()
+    out = {"reset_us": a.elapsed_time(b) * 1e3, "rollout_us": b.elapsed_time(c) * 1e3, "play_us": f0.elapsed_time(f1) * 1e3,
+           "reset_seed_cyc": (s[:, 1] - s[:, 0]).mean().item(), "reset_draw_cyc": (s[:, 2] - s[:, 1]).mean().item(),
+           "reset_store_cyc": (s[:, 3] - s[:, 2]).mean().item(), "reset_writeout_cyc": (s[:, 4] - s[:, 3]).mean().item(),
+           "reset_total_cyc_max": (s[:, 4] - s[:, 0]).max().item(),
+           "roll_top_cyc": s[:, 8].mean().item(), "roll_legal_cyc": s[:, 9].mean().item(),
+           "roll_pick_cyc": s[:, 10].mean().item(), "roll_step_cyc": s[:, 11].mean().item(),
+           "roll_turnend_cyc": s[:, 12].mean().item()}
+print(json.dumps(out))

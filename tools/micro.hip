@@ -1,0 +1,92 @@
+// Microbenchmarks of the device rules in isolation (tools/micro.py).
+#include <hip/hip_runtime.h>
+#include "../harmonies-alphazero_amd/csrc/hz_device.hpp"
+using namespace hz;
+
+__global__ void __launch_bounds__(64) k_draws(uint32_t *mt, int32_t *cur, int n, int reps, uint32_t *sink) {
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, cur[b])};
+  uint64_t misc = 0;
+  for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  uint32_t acc = 0;
+  for (int r = 0; r < reps; r++) {
+    uint32_t p9 = d(misc);
+    apply_pile(misc, p9);
+    acc += p9;
+    if (bag_total(misc) < 6) misc = set_bits(misc, 11, 30, 0x3fffffffULL & 0x2108421ULL * 17);
+  }
+  sink[b] = acc;
+  cur[b] = d.m.cursor();
+}
+
+__global__ void __launch_bounds__(64) k_next(uint32_t *mt, int32_t *cur, int n, int reps, uint32_t *sink) {
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  MT m(mt + (size_t)b * kMT, cur[b]);
+  uint32_t acc = 0;
+  for (int r = 0; r < reps; r++) acc ^= m.next();
+  sink[b] = acc;
+  cur[b] = m.cursor();
+}
+
+__global__ void __launch_bounds__(64) k_score(const uint64_t *pl, int n, int reps, uint32_t *sink) {
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  State s;
+  for (int k = 0; k < 4; k++) s.pl[k] = pl[(size_t)k * n + b];
+  s.piles = 0; s.misc = 0;
+  uint32_t acc = 0;
+  for (int r = 0; r < reps; r++) {
+    acc += score_player(s, r & 1);
+    s.pl[0] ^= (uint64_t)(acc & 1);
+  }
+  sink[b] = acc;
+}
+
+__global__ void __launch_bounds__(64) k_seed(uint32_t *mt, int n, uint32_t *sink) {
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  mt_seed(mt + (size_t)b * kMT, 1, 1234 + b);
+  sink[b] = mt[(size_t)b * kMT + 5];
+}
+
+__global__ void __launch_bounds__(64) k_seed_lds(uint32_t *mt, int n, uint32_t *sink) {
+  extern __shared__ uint32_t lds[];
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  mt_seed(lds + threadIdx.x, 65, 1234 + b);
+  sink[b] = lds[5 * 65 + threadIdx.x];
+}
+
+__global__ void __launch_bounds__(64) k_pick(const uint64_t *seedv, int n, int reps, uint32_t *sink) {
+  int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  uint64_t mk[3] = {0x5555555555555555ull ^ b, 0x3333333333333333ull, 0x0f0f0f0f0f0full};
+  uint32_t acc = 0;
+  for (int r = 0; r < reps; r++) {
+    int L = __popcll(mk[0]) + __popcll(mk[1]) + __popcll(mk[2]);
+    acc += kth_action(mk, rule_pick(seedv[b], r, L));
+    mk[0] ^= acc;
+  }
+  sink[b] = acc;
+}
+
+extern "C" {
+int micro_run(int which, void *a, void *b, int n, int reps, void *sink, void *stream) {
+  dim3 g((n + 63) / 64), blk(64);
+  hipStream_t s = (hipStream_t)stream;
+  switch (which) {
+    case 0: hipLaunchKernelGGL(k_draws, g, blk, 0, s, (uint32_t *)a, (int32_t *)b, n, reps, (uint32_t *)sink); break;
+    case 1: hipLaunchKernelGGL(k_next, g, blk, 0, s, (uint32_t *)a, (int32_t *)b, n, reps, (uint32_t *)sink); break;
+    case 2: hipLaunchKernelGGL(k_score, g, blk, 0, s, (const uint64_t *)a, n, reps, (uint32_t *)sink); break;
+    case 3: hipLaunchKernelGGL(k_seed, g, blk, 0, s, (uint32_t *)a, n, (uint32_t *)sink); break;
+    case 4:
+      hipFuncSetAttribute((const void *)k_seed_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 624 * 65 * 4);
+      hipLaunchKernelGGL(k_seed_lds, g, blk, 624 * 65 * 4, s, (uint32_t *)a, n, (uint32_t *)sink);
+      break;
+    case 5: hipLaunchKernelGGL(k_pick, g, blk, 0, s, (const uint64_t *)a, n, reps, (uint32_t *)sink); break;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+}

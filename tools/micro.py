@@ -1,0 +1,35 @@
+"""Time device-rule microbenchmarks (tools/micro.hip) at 4096 lanes."""
+import ctypes, json, os, sys
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+L = ctypes.CDLL(os.path.join(ROOT, "tools", "libmicro.so"))
+vp = ctypes.c_void_p
+L.micro_run.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp]
+n = 4096
+dev = "cuda"
+mt = torch.zeros(n, 624, dtype=torch.int32, device=dev)
+cur = torch.full((n,), 624 | (624 << 16), dtype=torch.int32, device=dev)
+sink = torch.zeros(n, dtype=torch.int32, device=dev)
+pl = torch.randint(0, 2**62, (4, n), dtype=torch.int64, device=dev)
+seeds = torch.arange(n, dtype=torch.int64, device=dev)
+stream = vp(torch.cuda.current_stream().cuda_stream)
+P = lambda t: vp(t.data_ptr())
+
+def timeit(which, a, b, reps):
+    L.micro_run(which, a, b, n, reps, P(sink), stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(); L.micro_run(which, a, b, n, reps, P(sink), stream); e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3
+
+res = {}
+L.micro_run(3, P(mt), None, n, 0, P(sink), stream)  # seed streams
+res["seed_global_us"] = timeit(3, P(mt), None, 0)
+res["seed_lds_us"] = timeit(4, P(mt), None, 0)
+for reps in (16, 64):
+    res[f"next_x{reps}_us"] = timeit(1, P(mt), P(cur), reps)
+    res[f"draws_x{reps}_us"] = timeit(0, P(mt), P(cur), reps)
+    res[f"score_x{reps}_us"] = timeit(2, P(pl), None, reps)
+    res[f"pick_x{reps}_us"] = timeit(5, P(seeds), None, reps)
+print(json.dumps(res))
