@@ -292,142 +292,101 @@ __device__ __forceinline__ uint32_t twist_word(uint32_t cur, uint32_t next, uint
   return far ^ (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
 }
 
+// twist words [start, start + k), k = min(8, 624 - start), start == tw, of a
+// stream whose word i is at w[i * S]: sources below tw are new, from tw on
+// old, so all loads issue together.  Returns k.
+template <class Ptr>
+__device__ __forceinline__ int twist_block(Ptr w, int S, int start) {
+  int k = kMT - start < 8 ? kMT - start : 8;
+  uint32_t cur[9], far[8];
+#pragma unroll
+  for (int j = 0; j < 9; j++) {
+    int i = start + j;
+    cur[j] = (j <= k) ? w[(i < kMT ? i : 0) * S] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    int i = start + j;
+    int fi = i < 227 ? i + 397 : (i < 623 ? i - 227 : 396);
+    far[j] = (j < k) ? w[fi * S] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (j < k) w[(start + j) * S] = twist_word(cur[j], cur[j + 1], far[j]);
+  }
+  return k;
+}
+
+// A board's stream in global memory (board-major, contiguous): used by the
+// one-draw-per-call kernels (hz_step, hz_end_turn, ...) and the MCTS chance
+// replay.  Cursor = pos | tw << 16: pos = CPython's index, tw = words of the
+// current generation already twisted in place (8 at a time, on demand);
+// hz_mt_normalize finishes the twist to recover CPython's (mt, index).
 template <int S>
 struct MTS {
   uint32_t* w;  // word i at w[i * S]
-  int pos, tw;  // CPython index; words of this generation twisted in place
-  // Register window of TEMPERED outputs in three 8-word blocks A, B, C:
-  // slot t holds word base + t, slots [0, nw) are filled (blocks fill in
-  // order; only the generation's last block is short) and off = pos - base
-  // of them are consumed.  prefetch() tops the window up to 24 words at the
-  // start of every draw, where all lanes of the wave are together, so the
-  // wave pays one memory round trip for everybody's refill; a draw needs more
-  // than 24 words with probability ~1e-5 per lane.  Only static register
-  // indices are used (a dynamic index would move the stream to scratch), and
-  // a stored word is never re-read (vmcnt counts stores on CDNA).
-  uint32_t a0, a1, a2, a3, a4, a5, a6, a7;
-  uint32_t b0, b1, b2, b3, b4, b5, b6, b7;
-  uint32_t c0, c1, c2, c3, c4, c5, c6, c7;
-  int nw, off;
+  int pos, tw;
 
-  __device__ __forceinline__ MTS(uint32_t* words, int cursor)
-      : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16), a0(0), a1(0), a2(0), a3(0), a4(0), a5(0), a6(0),
-        a7(0), b0(0), b1(0), b2(0), b3(0), b4(0), b5(0), b6(0), b7(0), c0(0), c1(0), c2(0), c3(0), c4(0), c5(0),
-        c6(0), c7(0), nw(0), off(0) {}
+  __device__ __forceinline__ MTS(uint32_t* words, int cursor) : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
   __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
+  __device__ __forceinline__ void prefetch() {}
 
-  // Raw words [start, start + k), k = min(8, 624 - start), start <= tw: words
-  // below tw are loaded, the rest twisted (their sources are new below tw,
-  // old from tw on) and stored.  All 17 loads issue together.  Returns the
-  // tempered outputs in o[].
-  __device__ __forceinline__ int fill(int start, uint32_t o[8]) {
-    int k = kMT - start < 8 ? kMT - start : 8;
-    uint32_t cur[9], far[8];
-#pragma unroll
-    for (int j = 0; j < 9; j++) {
-      int i = start + j;
-      cur[j] = (j <= k) ? w[(i < kMT ? i : 0) * S] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      int i = start + j;
-      int fi = i < 227 ? i + 397 : (i < 623 ? i - 227 : 396);
-      far[j] = (j < k && i >= tw) ? w[fi * S] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      int i = start + j;
-      o[j] = (i < tw) ? cur[j] : twist_word(cur[j], cur[j + 1], far[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      int i = start + j;
-      if (j < k && i >= tw) w[i * S] = o[j];
-    }
-    if (start + k > tw) tw = start + k;
-#pragma unroll
-    for (int j = 0; j < 8; j++) o[j] = temper(o[j]);
-    return k;
-  }
-
-  // drop fully consumed leading blocks
-  __device__ __forceinline__ void compact() {
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-      if (off >= 8 && nw >= 8) {
-        a0 = b0; a1 = b1; a2 = b2; a3 = b3; a4 = b4; a5 = b5; a6 = b6; a7 = b7;
-        b0 = c0; b1 = c1; b2 = c2; b3 = c3; b4 = c4; b5 = c5; b6 = c6; b7 = c7;
-        off -= 8;
-        nw -= 8;
-      }
-    }
-    if (off >= nw) { off = 0; nw = 0; }
-  }
-
-  __device__ __forceinline__ void prefetch() {
-    compact();
-    if (pos >= kMT) { pos = 0; tw = 0; nw = off = 0; }  // the window is empty here
-    uint32_t o[8];
-    int base = pos - off;
-    if (nw == 0) {
-      nw = fill(base, o);
-      a0 = o[0]; a1 = o[1]; a2 = o[2]; a3 = o[3]; a4 = o[4]; a5 = o[5]; a6 = o[6]; a7 = o[7];
-    }
-    if (nw == 8 && base + 8 < kMT) {
-      nw += fill(base + 8, o);
-      b0 = o[0]; b1 = o[1]; b2 = o[2]; b3 = o[3]; b4 = o[4]; b5 = o[5]; b6 = o[6]; b7 = o[7];
-    }
-    if (nw == 16 && base + 16 < kMT) {
-      nw += fill(base + 16, o);
-      c0 = o[0]; c1 = o[1]; c2 = o[2]; c3 = o[3]; c4 = o[4]; c5 = o[5]; c6 = o[6]; c7 = o[7];
-    }
-  }
-
-  __device__ __forceinline__ uint32_t win(int t) const {  // t is a compile-time constant after unrolling
-    switch (t) {
-      case 0: return a0; case 1: return a1; case 2: return a2; case 3: return a3;
-      case 4: return a4; case 5: return a5; case 6: return a6; case 7: return a7;
-      case 8: return b0; case 9: return b1; case 10: return b2; case 11: return b3;
-      case 12: return b4; case 13: return b5; case 14: return b6; case 15: return b7;
-      case 16: return c0; case 17: return c1; case 18: return c2; case 19: return c3;
-      case 20: return c4; case 21: return c5; case 22: return c6; default: return c7;
-    }
-  }
-
-  __device__ __forceinline__ bool live(int t) const { return t >= off && t < nw; }
-
-  __device__ __forceinline__ void consume(int c) {
-    pos += c;
-    off += c;
-  }
-
-  // genrand_uint32 one word at a time (slow path; drops the window)
+  // genrand_uint32
   __device__ __forceinline__ uint32_t next() {
-    nw = off = 0;
     if (pos >= kMT) { pos = 0; tw = 0; }
-    if (pos >= tw) {
-      uint32_t o[8];
-      fill(pos, o);
-      pos++;
-      return o[0];
-    }
+    if (pos >= tw) tw += twist_block(w, S, tw);
     return temper(w[(pos++) * S]);
   }
 
   // finish the current generation's twist (CPython form afterwards)
   __device__ __forceinline__ void normalize() {
     if (pos >= kMT) return;
-    uint32_t o[8];
-    while (tw < kMT) fill(tw, o);
-    nw = off = 0;
+    while (tw < kMT) tw += twist_block(w, S, tw);
   }
 };
 using MT = MTS<1>;
 
+// Dynamic LDS of the lane-per-board kernels: the wave's 64 streams as
+// [624][65] words (word i of lane l at i*65 + l).  Addressing through this
+// __shared__ symbol keeps every access a 32-bit LDS address.
+constexpr int kLdsStride = 65;
+extern __shared__ uint32_t hz_lds[];
+
+// A board's stream resident in LDS (k_reset / k_rollout).  Draws scan the
+// next <= 24 twisted words in place, branch-free; prefetch() twists ahead
+// at a point the whole wave reaches together (the start of a draw).
+struct LdsMT {
+  int lane, pos, tw;
+  __device__ __forceinline__ LdsMT(int l, int cursor) : lane(l), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
+  __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
+  __device__ __forceinline__ uint32_t* w() const { return hz_lds + lane; }
+
+  __device__ __forceinline__ void prefetch() {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    while (tw < kMT && tw < pos + 24) tw += twist_block(w(), kLdsStride, tw);
+  }
+
+  __device__ __forceinline__ uint32_t word(int i) const {  // tempered output i (i < tw)
+    return temper(hz_lds[(i < kMT ? i : kMT - 1) * kLdsStride + lane]);
+  }
+
+  __device__ __forceinline__ uint32_t next() {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    if (pos >= tw) tw += twist_block(w(), kLdsStride, tw);
+    return word(pos++);
+  }
+
+  __device__ __forceinline__ void normalize() {
+    if (pos >= kMT) return;
+    while (tw < kMT) tw += twist_block(w(), kLdsStride, tw);
+  }
+};
+
 // random.seed(int) for 0 <= seed < 2^64 (_randommodule.c random_seed +
 // init_by_array) into w[i * stride]; init_genrand(19650218) is regenerated on
 // the fly.  The stream's cursor afterwards is kMTSeeded.
-__device__ __forceinline__ void mt_seed(uint32_t* w, int stride, uint64_t seed) {
+template <class Ptr>
+__device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed) {
   uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   int klen = key1 ? 2 : 1;
   uint32_t init = 19650218U;  // init_genrand word i, generated in order
@@ -487,22 +446,29 @@ __device__ __forceinline__ void sample3_serial(M& m, uint32_t n, int k, uint32_t
   }
 }
 
-// The raw picks of random.sample(range(n), k): the set method (n > 21) keeps
-// every value < n not already taken; the pool method (n <= 21) takes the
-// i-th value < n - i.  A word whose value is out of range is rejected
-// (_randbelow, random.py:239-249).  Branch-free scan of the register window
-// (the wave leaves early once every lane has its picks).
+// The raw picks of random.sample(range(n), k) (k <= 3): the set method
+// (n > 21) keeps every value < n not already taken; the pool method (n <= 21)
+// takes the i-th value < n - i.  A word whose value is out of range is
+// rejected (_randbelow, random.py:239-249).
 template <class M>
 __device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[3]) {
+  sample3_serial(m, n, k, j, 0);
+}
+
+// LDS stream: branch-free scan of the next 24 twisted words (the wave leaves
+// early once every lane has its picks; a lane needs more than 24 words with
+// probability ~1e-5 and then finishes serially).
+__device__ __forceinline__ void sample3_raw(LdsMT& m, uint32_t n, int k, uint32_t j[3]) {
   uint32_t j0 = 0, j1 = 0, j2 = 0;
   int got = 0, used = 0;
+  int avail = m.tw - m.pos;
   if (__all(n > 21)) {
     int sh = __clz(n);
 #pragma unroll
     for (int t = 0; t < 24; t++) {
       if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
-      bool lv = m.live(t) && got < k;
-      uint32_t v = m.win(t) >> sh;  // getrandbits(bit_length(n))
+      bool lv = t < avail && got < k;
+      uint32_t v = m.word(m.pos + t) >> sh;  // getrandbits(bit_length(n))
       bool ok = lv && v < n && (got < 1 || v != j0) && (got < 2 || v != j1);
       j0 = (ok && got == 0) ? v : j0;
       j1 = (ok && got == 1) ? v : j1;
@@ -516,10 +482,10 @@ __device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[
 #pragma unroll
     for (int t = 0; t < 24; t++) {
       if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
-      bool lv = m.live(t) && got < k;
+      bool lv = t < avail && got < k;
       int sh = pool ? (got == 0 ? sh0 : got == 1 ? sh1 : sh2) : sh0;
       uint32_t lim = pool ? n - (uint32_t)got : n;
-      uint32_t v = m.win(t) >> sh;
+      uint32_t v = m.word(m.pos + t) >> sh;
       bool ok = lv && v < lim && (pool || ((got < 1 || v != j0) && (got < 2 || v != j1)));
       j0 = (ok && got == 0) ? v : j0;
       j1 = (ok && got == 1) ? v : j1;
@@ -528,7 +494,7 @@ __device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[
       got += ok ? 1 : 0;
     }
   }
-  m.consume(used);
+  m.pos += used;
   j[0] = j0; j[1] = j1; j[2] = j2;
   if (got < k) sample3_serial(m, n, k, j, got);  // window exhausted (rare)
 }

@@ -65,7 +65,6 @@ inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 // reads are both bank-conflict free).  Seeding (two serial 623-step passes)
 // and the 15 opening draws run at LDS latency; one coalesced pass then writes
 // the block's contiguous 64 x 2,496 B of HBM.
-constexpr int kLdsStride = 65;
 constexpr size_t kResetLds = (size_t)kMT * kLdsStride * sizeof(uint32_t);  // 162,240 B
 
 __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
@@ -73,7 +72,7 @@ __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uin
                                                   int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
                                                   int n, uint64_t seed_base, const uint8_t *__restrict__ sel,
                                                   const uint64_t *__restrict__ seeds) {
-  extern __shared__ uint32_t lds[];
+  uint32_t *lds = hz_lds;
   int lane = threadIdx.x;
   int b0 = blockIdx.x * kBlock;
   int b = b0 + lane;
@@ -88,9 +87,9 @@ __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uin
       episode[b] = e + 1;
     }
     HZ_STAMP(0);
-    mt_seed(lds + lane, kLdsStride, sd);
+    mt_seed(hz_lds + lane, kLdsStride, sd);
     HZ_STAMP(1);
-    StreamDraw<MTS<kLdsStride>> d{MTS<kLdsStride>(lds + lane, kMTSeeded)};
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
     State s;
     reset_state(s, d);
     HZ_STAMP(2);
@@ -257,7 +256,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
                                                     uint64_t *__restrict__ traj_mask,
                                                     int16_t *__restrict__ traj_action, int32_t *__restrict__ games_done,
                                                     int32_t *__restrict__ steps_done) {
-  extern __shared__ uint32_t lds[];
+  uint32_t *lds = hz_lds;
   int lane = threadIdx.x;
   int b0 = blockIdx.x * kBlock;
   int b = b0 + lane;
@@ -268,7 +267,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
   if (!reset_first) stage_mt(lds, g, nb, lane, actmask, true);
   __syncthreads();
   if (act) {
-    StreamDraw<MTS<kLdsStride>> draw{MTS<kLdsStride>(lds + lane, reset_first ? kMTSeeded : pos[b])};
+    StreamDraw<LdsMT> draw{LdsMT(lane, reset_first ? kMTSeeded : pos[b])};
     State s;
     int g_ply, games = 0, steps = 0;
     uint64_t sd;
@@ -276,7 +275,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
       int e = episode[b];
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       episode[b] = e + 1;
-      mt_seed(lds + lane, kLdsStride, sd);
+      mt_seed(hz_lds + lane, kLdsStride, sd);
       reset_state(s, draw);
       g_ply = 0;
     } else {
@@ -299,8 +298,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
         int e = episode[b];
         sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
         episode[b] = e + 1;
-        mt_seed(lds + lane, kLdsStride, sd);
-        draw.m = MTS<kLdsStride>(lds + lane, kMTSeeded);
+        mt_seed(hz_lds + lane, kLdsStride, sd);
+        draw.m = LdsMT(lane, kMTSeeded);
         reset_state(s, draw);
         g_ply = 0;
       }

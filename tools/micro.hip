@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(64) k_seed(uint32_t *mt, int n, uint32_t *sink
 }
 
 __global__ void __launch_bounds__(64) k_seed_lds(uint32_t *mt, int n, uint32_t *sink) {
-  extern __shared__ uint32_t lds[];
+  uint32_t *lds = hz_lds;
   int b = blockIdx.x * 64 + threadIdx.x;
   if (b >= n) return;
   mt_seed(lds + threadIdx.x, 65, 1234 + b);
@@ -89,4 +89,34 @@ int micro_run(int which, void *a, void *b, int n, int reps, void *sink, void *st
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+}
+
+// draws with the stream in LDS (as in k_rollout)
+__global__ void __launch_bounds__(64) k_draws_lds(uint32_t *mt, int n, int reps, uint32_t *sink, uint64_t *cyc) {
+  uint32_t *lds = hz_lds;
+  int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
+  mt_seed(lds + lane, 65, 99 + b);
+  StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
+  uint64_t misc = 0;
+  for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  uint32_t acc = 0;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < reps; r++) {
+    uint32_t p9 = d(misc);
+    apply_pile(misc, p9);
+    acc += p9;
+    if (bag_total(misc) < 40) {
+      for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+    }
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  sink[b] = acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+extern "C" int micro_draws_lds(void *mt, int n, int reps, void *sink, void *cyc, void *stream) {
+  hipFuncSetAttribute((const void *)k_draws_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 624 * 65 * 4);
+  hipLaunchKernelGGL(k_draws_lds, dim3((n + 63) / 64), dim3(64), 624 * 65 * 4, (hipStream_t)stream, (uint32_t *)mt, n,
+                     reps, (uint32_t *)sink, (uint64_t *)cyc);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -33,3 +33,11 @@ for reps in (16, 64):
     res[f"score_x{reps}_us"] = timeit(2, P(pl), None, reps)
     res[f"pick_x{reps}_us"] = timeit(5, P(seeds), None, reps)
 print(json.dumps(res))
+
+L.micro_draws_lds.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+cyc = torch.zeros(n // 64, dtype=torch.int64, device=dev)
+for reps in (1, 17, 65):
+    L.micro_draws_lds(P(mt), n, reps, P(sink), P(cyc), stream)
+    torch.cuda.synchronize()
+    res[f"draws_lds_x{reps}_cyc"] = float(cyc.double().mean())
+print(json.dumps(res))
