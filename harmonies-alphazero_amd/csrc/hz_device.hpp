@@ -382,39 +382,87 @@ struct LdsMT {
   }
 };
 
+// init_genrand(19650218) (_randommodule.c), the starting array of
+// init_by_array: the same for every seed, so it is a constant table read
+// through the scalar cache instead of a per-step multiply chain.
+struct InitGen { uint32_t v[kMT]; };
+constexpr InitGen make_init_gen() {
+  InitGen g{};
+  uint32_t x = 19650218u;
+  g.v[0] = x;
+  for (int i = 1; i < kMT; i++) {
+    x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+    g.v[i] = x;
+  }
+  return g;
+}
+__constant__ InitGen kInitGen = make_init_gen();
+
 // random.seed(int) for 0 <= seed < 2^64 (_randommodule.c random_seed +
-// init_by_array) into w[i * stride]; init_genrand(19650218) is regenerated on
-// the fly.  The stream's cursor afterwards is kMTSeeded.
+// init_by_array with key = the seed's 32-bit words) into w[i * stride].
+// Both passes are serial recurrences; the code keeps each step to its five
+// dependent ALU ops (key selection unrolled by two, pass-1 words read eight
+// ahead in pass 2).  The stream's cursor afterwards is kMTSeeded.
 template <class Ptr>
 __device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed) {
   uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
-  int klen = key1 ? 2 : 1;
-  uint32_t init = 19650218U;  // init_genrand word i, generated in order
-  uint32_t prev = init;       // mt[i-1]
-  int j = 0;
-  // first pass: i = 1..623, then mt[0] = mt[623] and one more step at i = 1
-  for (int i = 1; i < kMT; i++) {
-    init = 1812433253U * (init ^ (init >> 30)) + (uint32_t)i;
-    uint32_t v = (init ^ ((prev ^ (prev >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
-    w[i * stride] = v;
-    prev = v;
-    if (++j >= klen) j = 0;
+  // key[j] + j for j = (i - 1) % keylen: odd i -> kA, even i -> kB
+  uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
+  uint32_t prev = 19650218u;  // mt[i-1]
+  // first pass: i = 1..623 (mt[0] = mt[623] afterwards, then one more step
+  // at i = 1); table words fetched a group of eight ahead
+  uint32_t iv[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[1 + u];
+  for (int g = 1; g < kMT - 7; g += 8) {  // g = 1, 9, ..., 609 (groups end at 616)
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      w[(g + u) * stride] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = nx[u];
   }
-  uint32_t mt0 = prev;
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // i = 617..623
+    uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(617 + u) * stride] = v;
+    prev = v;
+  }
+  // iteration 624 at i = 1 with j = 623 % keylen (-> kB)
   uint32_t m1 = w[1 * stride];
-  prev = (m1 ^ ((mt0 ^ (mt0 >> 30)) * 1664525U)) + (j ? key1 : key0) + (uint32_t)j;
+  prev = (m1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
   w[1 * stride] = prev;
-  // second pass: 623 steps starting at i = 2, reading 4 words ahead
-  uint32_t r0 = w[2 * stride], r1 = w[3 * stride], r2 = w[4 * stride], r3 = w[5 * stride];
-  for (int i = 2; i < kMT; i++) {
-    uint32_t after = i + 4 < kMT ? w[(i + 4) * stride] : 0u;
-    uint32_t v = (r0 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
-    w[i * stride] = v;
-    prev = v;
-    r0 = r1; r1 = r2; r2 = r3; r3 = after;
+  uint32_t first1 = prev;
+  // second pass: i = 2..623, pass-1 words fetched eight ahead
+  uint32_t cur[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) cur[u] = w[(2 + u) * stride];
+  for (int g = 2; g < kMT - 6; g += 8) {  // g = 2, 10, ..., 610 (groups end at 617)
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = w[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
+      w[(g + u) * stride] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
   }
-  mt0 = prev;  // mt[0] = mt[623]
-  w[1 * stride] = (w[1 * stride] ^ ((mt0 ^ (mt0 >> 30)) * 1566083941U)) - 1U;
+#pragma unroll
+  for (int u = 0; u < 6; u++) {  // i = 618..623
+    uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(618 + u);
+    w[(618 + u) * stride] = v;
+    prev = v;
+  }
+  // mt[0] = mt[623]; last step at i = 1; then mt[0] = 0x80000000
+  w[1 * stride] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
   w[0] = 0x80000000U;
 }
 

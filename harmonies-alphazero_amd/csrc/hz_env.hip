@@ -25,6 +25,17 @@ struct hz_env {
   int32_t *ply;      // [n]
   int32_t *episode;  // [n]
   uint64_t *seed;    // [n]
+  // seed-ahead (hz_play): a concurrent kernel on an auxiliary stream seeds
+  // the streams of each board's next episode into a double-buffered slot
+  // while k_rollout plays the current one (see launch_rollout)
+  int seed_ahead;            // enabled (default 1)
+  hipStream_t aux;
+  uint32_t *ahead_mt[2];     // [n][624] seeded streams
+  int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
+  int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
+  hipEvent_t ev_ro[2], ev_sa[2], ev_prime;
+  int calls;                 // hz_play calls since the last prime
+  int primed, sa_valid[2];
 };
 
 #ifdef HZ_DIAG
@@ -59,25 +70,74 @@ constexpr int kBlock = 64;  // one wave per workgroup: 4096 boards -> 64 waves
 
 inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 
+// The 64-board LDS kernels (k_reset, k_rollout, k_seed_ahead) run 256
+// threads per block: wave 0 plays (lane = board), waves 1-3 only help move
+// the block's streams between HBM and LDS (one 162 KB block per CU, so the
+// extra waves cost no occupancy) and wait at the barriers meanwhile.
+constexpr int kStageThreads = 256;
+constexpr size_t kResetLds = (size_t)kMT * kLdsStride * sizeof(uint32_t);  // 162,240 B
+
+// Copy the streams of boards set in `mask` between HBM (one contiguous span
+// of nb x 624 words, board-major) and LDS ([624][65]); 16 B per thread-load,
+// eight loads in flight per thread.
+__device__ __forceinline__ void stage_mt(uint32_t *__restrict__ g, int nb, int tid, uint64_t mask, bool to_lds) {
+  uint32_t *lds = hz_lds;
+  constexpr int U = 8;
+  int total4 = nb * (kMT / 4);
+  for (int q0 = 0; q0 < total4; q0 += kStageThreads * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
+      if (q < total4 && ((mask >> bl) & 1)) {
+        if (to_lds) {
+          v[u] = reinterpret_cast<const uint4 *>(g)[q];
+        } else {
+          v[u].x = lds[i * kLdsStride + bl];
+          v[u].y = lds[(i + 1) * kLdsStride + bl];
+          v[u].z = lds[(i + 2) * kLdsStride + bl];
+          v[u].w = lds[(i + 3) * kLdsStride + bl];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
+      if (q < total4 && ((mask >> bl) & 1)) {
+        if (to_lds) {
+          lds[i * kLdsStride + bl] = v[u].x;
+          lds[(i + 1) * kLdsStride + bl] = v[u].y;
+          lds[(i + 2) * kLdsStride + bl] = v[u].z;
+          lds[(i + 3) * kLdsStride + bl] = v[u].w;
+        } else {
+          reinterpret_cast<uint4 *>(g)[q] = v[u];
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ reset
 // Lane-per-board with the 64 boards' MT arrays staged in LDS as [624][65]
 // words (stride 65: the per-lane seeding writes and the board-major write-out
 // reads are both bank-conflict free).  Seeding (two serial 623-step passes)
 // and the 15 opening draws run at LDS latency; one coalesced pass then writes
 // the block's contiguous 64 x 2,496 B of HBM.
-constexpr size_t kResetLds = (size_t)kMT * kLdsStride * sizeof(uint32_t);  // 162,240 B
-
-__global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
+__global__ void __launch_bounds__(kStageThreads) k_reset(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                   int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                   int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
                                                   int n, uint64_t seed_base, const uint8_t *__restrict__ sel,
                                                   const uint64_t *__restrict__ seeds) {
-  uint32_t *lds = hz_lds;
-  int lane = threadIdx.x;
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  bool w0 = tid < 64;
   int b0 = blockIdx.x * kBlock;
   int b = b0 + lane;
   bool act = b < n && (!sel || sel[b]);
-  if (act) {
+  uint64_t actmask = __ballot(act);  // the same in every wave
+  if (w0 && act) {
     uint64_t sd;
     if (seeds) {
       sd = seeds[b];
@@ -98,29 +158,11 @@ __global__ void __launch_bounds__(kBlock) k_reset(uint64_t *__restrict__ st, uin
     ply[b] = 0;
     seed[b] = sd;
   }
-  uint64_t actmask = __ballot(act);
   __syncthreads();
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
-  uint32_t *g = mt + (size_t)b0 * kMT;
-  HZ_STAMP(3);
-  // board by board: lanes copy words lane, lane + 64, ... (LDS banks distinct,
-  // 256 B coalesced stores, ten LDS reads in flight per board)
-  for (int bl = 0; bl < nb; bl++) {
-    if (!((actmask >> bl) & 1)) continue;
-    uint32_t v[10];
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-      int i = lane + kBlock * k;
-      v[k] = i < kMT ? lds[i * kLdsStride + bl] : 0u;
-    }
-    uint32_t *gb = g + (size_t)bl * kMT;
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-      int i = lane + kBlock * k;
-      if (i < kMT) gb[i] = v[k];
-    }
-  }
-  HZ_STAMP(4);
+  if (w0 && act) HZ_STAMP(3);
+  stage_mt(mt + (size_t)b0 * kMT, nb, tid, actmask, false);
+  if (w0 && act) HZ_STAMP(4);
 }
 
 // ------------------------------------------------------------- legal mask
@@ -209,64 +251,34 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 // LDS latency instead of paying a scattered HBM round trip per draw.  The
 // streams are staged in (or seeded in place when reset_first) and written
 // back once.
-__device__ __forceinline__ void stage_mt(uint32_t *__restrict__ lds, uint32_t *__restrict__ g, int nb, int lane,
-                                         uint64_t actmask, bool to_lds) {
-  // the block's streams are one contiguous span of nb * 624 words in HBM
-  int total4 = nb * (kMT / 4);
-  for (int q0 = 0; q0 < total4; q0 += kBlock * 4) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      int q = q0 + u * kBlock + lane;
-      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
-      if (q < total4 && ((actmask >> bl) & 1)) {
-        if (to_lds) {
-          v[u] = reinterpret_cast<const uint4 *>(g)[q];
-        } else {
-          v[u].x = lds[i * kLdsStride + bl];
-          v[u].y = lds[(i + 1) * kLdsStride + bl];
-          v[u].z = lds[(i + 2) * kLdsStride + bl];
-          v[u].w = lds[(i + 3) * kLdsStride + bl];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      int q = q0 + u * kBlock + lane;
-      int o = q * 4, bl = o / kMT, i = o - bl * kMT;
-      if (q < total4 && ((actmask >> bl) & 1)) {
-        if (to_lds) {
-          lds[i * kLdsStride + bl] = v[u].x;
-          lds[(i + 1) * kLdsStride + bl] = v[u].y;
-          lds[(i + 2) * kLdsStride + bl] = v[u].z;
-          lds[(i + 3) * kLdsStride + bl] = v[u].w;
-        } else {
-          reinterpret_cast<uint4 *>(g)[q] = v[u];
-        }
-      }
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
+__global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                     int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                     int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
                                                     int n, uint64_t seed_base, int max_plies, int auto_reset,
                                                     int reset_first, uint64_t *__restrict__ traj_state,
                                                     uint64_t *__restrict__ traj_mask,
                                                     int16_t *__restrict__ traj_action, int32_t *__restrict__ games_done,
-                                                    int32_t *__restrict__ steps_done) {
-  uint32_t *lds = hz_lds;
-  int lane = threadIdx.x;
+                                                    int32_t *__restrict__ steps_done,
+                                                    const uint32_t *__restrict__ ahead_mt,
+                                                    const int32_t *__restrict__ ahead_tag,
+                                                    int32_t *__restrict__ ep_final) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  bool w0 = tid < 64;
   int b0 = blockIdx.x * kBlock;
   int b = b0 + lane;
   bool act = b < n;
-  uint64_t actmask = __ballot(act);
+  uint64_t actmask = __ballot(act);  // the same in every wave
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
   uint32_t *g = mt + (size_t)b0 * kMT;
-  if (!reset_first) stage_mt(lds, g, nb, lane, actmask, true);
+  // reset_first: boards whose next-episode stream was seeded ahead stage it
+  // in; the others seed in place below
+  bool seeded = reset_first && act && ahead_tag && ahead_tag[b] == episode[b];
+  uint64_t seededmask = __ballot(seeded);
+  if (!reset_first) stage_mt(g, nb, tid, actmask, true);
+  else if (seededmask) stage_mt(const_cast<uint32_t *>(ahead_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
   __syncthreads();
-  if (act) {
+  if (w0 && act) {
     StreamDraw<LdsMT> draw{LdsMT(lane, reset_first ? kMTSeeded : pos[b])};
     State s;
     int g_ply, games = 0, steps = 0;
@@ -275,7 +287,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
       int e = episode[b];
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       episode[b] = e + 1;
-      mt_seed(hz_lds + lane, kLdsStride, sd);
+      if (!seeded) mt_seed(hz_lds + lane, kLdsStride, sd);
       reset_state(s, draw);
       g_ply = 0;
     } else {
@@ -343,9 +355,33 @@ __global__ void __launch_bounds__(kBlock) k_rollout(uint64_t *__restrict__ st, u
 #endif
     if (games_done) games_done[b] = games;
     if (steps_done) steps_done[b] = steps;
+    if (ep_final) ep_final[b] = episode[b];
   }
   __syncthreads();
-  stage_mt(lds, g, nb, lane, actmask, false);
+  stage_mt(g, nb, tid, actmask, false);
+}
+
+// Seed-ahead: the streams of each board's predicted next episode (the
+// episode counter the last k_rollout left, plus one) seeded in LDS and
+// written out board-major with their tags; runs on the CUs k_rollout leaves
+// idle (one 64-board block per CU each).
+__global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
+                                                              const int32_t *__restrict__ ep_final, int n,
+                                                              uint64_t seed_base) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  int b0 = blockIdx.x * kBlock;
+  int b = b0 + lane;
+  bool act = b < n;
+  uint64_t actmask = __ballot(act);
+  int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  if (tid < 64 && act) {
+    int e = ep_final[b] + 1;
+    mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
+    tag[b] = e;
+  }
+  __syncthreads();
+  stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
 }
 
 // ---------------------------------------------------------- state transfer
@@ -388,6 +424,8 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   if (hipFuncSetAttribute((const void *)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
           hipSuccess ||
       hipFuncSetAttribute((const void *)k_rollout, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void *)k_seed_ahead, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
           hipSuccess) {
     free(e);
     return nullptr;
@@ -405,6 +443,18 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMemset(e->episode, 0, n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->seed, 0, n * sizeof(uint64_t)) == hipSuccess;
   }
+  for (int k = 0; ok && k < 2; k++) {
+    ok = hipMalloc(&e->ahead_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
+         hipEventCreateWithFlags(&e->ev_ro[k], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&e->ev_sa[k], hipEventDisableTiming) == hipSuccess;
+  }
+  ok = ok && hipEventCreateWithFlags(&e->ev_prime, hipEventDisableTiming) == hipSuccess &&
+       hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) == hipSuccess &&
+       hipDeviceSynchronize() == hipSuccess;
+  e->seed_ahead = 1;
   if (!ok) {
     hz_env_destroy(e);
     return nullptr;
@@ -414,6 +464,18 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
 
 void hz_env_destroy(hz_env *e) {
   if (!e) return;
+  if (e->aux) {
+    (void)hipStreamSynchronize(e->aux);
+    (void)hipStreamDestroy(e->aux);
+  }
+  for (int k = 0; k < 2; k++) {
+    if (e->ahead_mt[k]) (void)hipFree(e->ahead_mt[k]);
+    if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
+    if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
+    if (e->ev_ro[k]) (void)hipEventDestroy(e->ev_ro[k]);
+    if (e->ev_sa[k]) (void)hipEventDestroy(e->ev_sa[k]);
+  }
+  if (e->ev_prime) (void)hipEventDestroy(e->ev_prime);
   if (e->state) (void)hipFree(e->state);
   if (e->mt) (void)hipFree(e->mt);
   if (e->pos) (void)hipFree(e->pos);
@@ -437,9 +499,17 @@ int32_t *hz_env_mt_pos_ptr(hz_env *e) { return e ? e->pos : nullptr; }
 int32_t *hz_env_ply_ptr(hz_env *e) { return e ? e->ply : nullptr; }
 uint64_t *hz_env_seed_ptr(hz_env *e) { return e ? e->seed : nullptr; }
 
+int hz_env_set_seed_ahead(hz_env *e, int32_t enable) {
+  if (!e) return -1;
+  e->seed_ahead = enable ? 1 : 0;
+  e->primed = 0;
+  return 0;
+}
+
 int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   if (!e) return -1;
-  hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), kResetLds, e->stream, e->state, e->mt, e->pos,
+  e->primed = 0;  // episode counters move outside hz_play's plan
+  hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
   return launch_err();
 }
@@ -478,13 +548,62 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
   return launch_err();
 }
 
+// hz_play's seed-ahead pipeline.  Call i plays from slot r = i & 1 and,
+// concurrently on the auxiliary stream, seeds slot w = r ^ 1 for call i + 1:
+//   aux : wait ev_ro[w] (call i-1's k_rollout: done reading slot w, wrote
+//         ep_final[w]) -> k_seed_ahead(w) -> record ev_sa[w]
+//   main: wait ev_sa[r] (call i-1's k_seed_ahead) -> k_rollout(r) -> record ev_ro[r]
+// The prediction (the episode call i+1 resets to = the counter call i-1 left,
+// plus one) only decides which boards skip seeding: a board stages a
+// seeded-ahead stream only when the slot's tag equals its episode counter,
+// so the results never depend on it.  Anything else that moves episode
+// counters (hz_reset, hz_rollout) re-primes with a copy of the counters.
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
-  hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kBlock), kResetLds, e->stream, e->state, e->mt, e->pos,
+  const uint32_t *ahead_mt = nullptr;
+  const int32_t *ahead_tag = nullptr;
+  int32_t *ep_final = nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(e->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
+  bool pipe = reset_first && e->seed_ahead && cap == hipStreamCaptureStatusNone;
+  int r = e->calls & 1, w = r ^ 1;
+  if (pipe) {
+    size_t n = (size_t)e->n;
+    bool wait_r = e->sa_valid[r];  // call i-1's k_seed_ahead wrote slot r and read ep_final[r]
+    bool use_r = wait_r && e->primed;
+    if (!e->primed) {
+      if (hipMemcpyAsync(e->ep_final[w], e->episode, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream) ||
+          hipEventRecord(e->ev_prime, e->stream) || hipStreamWaitEvent(e->aux, e->ev_prime, 0))
+        return 1;
+      e->primed = 1;
+    } else if (hipStreamWaitEvent(e->aux, e->ev_ro[w], 0)) {
+      return 1;
+    }
+    hipLaunchKernelGGL(k_seed_ahead, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->aux, e->ahead_mt[w],
+                       e->ahead_tag[w], e->ep_final[w], e->n, e->seed_base);
+    int err = launch_err();
+    if (err || hipEventRecord(e->ev_sa[w], e->aux)) return err ? err : 1;
+    if (wait_r && hipStreamWaitEvent(e->stream, e->ev_sa[r], 0)) return 1;
+    if (use_r) {
+      ahead_mt = e->ahead_mt[r];
+      ahead_tag = e->ahead_tag[r];
+    }
+    ep_final = e->ep_final[r];
+  } else {
+    e->primed = 0;
+  }
+  hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
-                     traj_mask, traj_action, games_done, steps_done);
-  return launch_err();
+                     traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ep_final);
+  int err = launch_err();
+  if (err) return err;
+  if (pipe) {
+    if (hipEventRecord(e->ev_ro[r], e->stream)) return 1;
+    e->sa_valid[w] = 1;
+    e->calls++;
+  }
+  return 0;
 }
 
 int hz_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state, uint64_t *traj_mask,

@@ -51,6 +51,10 @@ class BatchedEnv:
     def handle(self):
         return self._h
 
+    def set_seed_ahead(self, enable):
+        """hz_play's concurrent next-episode seeding on/off (results identical)."""
+        nat.check(nat.lib().hz_env_set_seed_ahead(self._h, 1 if enable else 0), "hz_env_set_seed_ahead")
+
     # -- env surface ---------------------------------------------------------
     def reset(self, sel=None, seeds=None):
         """HarmoniesGameState() on every board (or on boards where sel != 0)."""

@@ -63,6 +63,9 @@ def lib():
         L.or_play_rule_games.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.or_play_rule_games.restype = ctypes.c_int64
+        L.or_play_rule_games_ep.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.or_play_rule_games_ep.restype = ctypes.c_int64
         L.or_mcts_search.argtypes = [ctypes.c_void_p, P(MT), P(MctsCfg), ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.or_mcts_search.restype = ctypes.c_int
@@ -150,12 +153,14 @@ def rule(seed, ply):
     return lib().or_rule(ctypes.c_uint64(seed), ctypes.c_uint64(ply))
 
 
-def play_rule_games(n, seed_base, nthreads=0):
+def play_rule_games(n, seed_base, nthreads=0, episode=0):
+    """Every board b plays its episode-`episode` game (seed = seed_base + b +
+    (episode << 32)) with the build-defined rule policy to the end."""
     finals = np.zeros((n, REFSTATE), np.int16)
     plies = np.zeros(n, np.int32)
     nxt = np.zeros(n, np.uint32)
-    total = lib().or_play_rule_games(n, ctypes.c_uint64(seed_base), _p(finals), _p(plies), _p(nxt),
-                                     nthreads)
+    total = lib().or_play_rule_games_ep(n, ctypes.c_uint64(seed_base), int(episode), _p(finals), _p(plies),
+                                        _p(nxt), nthreads)
     return total, finals, plies, nxt
 
 

@@ -583,6 +583,13 @@ static int kth_legal(const uint8_t *mask, int k) {
 
 int64_t or_play_rule_games(int n, uint64_t seed_base, int16_t *finals, int32_t *plies,
                            uint32_t *next_word, int nthreads) {
+  return or_play_rule_games_ep(n, seed_base, 0, finals, plies, next_word, nthreads);
+}
+
+/* the same for every board's episode e: seed = seed_base + b + (e << 32)
+ * (the env's hz_reset / hz_play seeding of a board's (e+1)-th game) */
+int64_t or_play_rule_games_ep(int n, uint64_t seed_base, int episode, int16_t *finals, int32_t *plies,
+                              uint32_t *next_word, int nthreads) {
   geom_init();
   int64_t total = 0;
 #ifdef _OPENMP
@@ -591,7 +598,7 @@ int64_t or_play_rule_games(int n, uint64_t seed_base, int16_t *finals, int32_t *
 #endif
   for (int b = 0; b < n; b++) {
     or_mt m;
-    uint64_t seed = seed_base + (uint64_t)b;
+    uint64_t seed = seed_base + (uint64_t)b + ((uint64_t)(uint32_t)episode << 32);
     or_mt_seed(&m, seed);
     int16_t st[78];
     or_reset(&m, st);

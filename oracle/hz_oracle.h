@@ -49,6 +49,8 @@ uint64_t or_rule(uint64_t seed, uint64_t ply);
  * steps.  finals: n*78, plies: n, next_word: n (CPython next getrandbits(32)). */
 int64_t or_play_rule_games(int n, uint64_t seed_base, int16_t *finals, int32_t *plies,
                            uint32_t *next_word, int nthreads);
+int64_t or_play_rule_games_ep(int n, uint64_t seed_base, int episode, int16_t *finals, int32_t *plies,
+                              uint32_t *next_word, int nthreads);
 
 /* MCTS (reference MCTS.py get_best_action_and_pi) with the deterministic stub
  * evaluator of tests/golden/make_golden.py, canonical (ascending action index)

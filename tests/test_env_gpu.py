@@ -155,6 +155,56 @@ def test_fused_play_and_staged_continue(Env):
         assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b]
 
 
+def _check_episode(env, base, ep, steps, nthreads=8):
+    total, finals, plies, nxt = oracle.play_rule_games(env.n, base, nthreads=nthreads, episode=ep)
+    assert (states_of(env) == finals).all(), ep
+    assert (steps.cpu().numpy() == plies).all(), ep
+    _, mt, idx = env.export_state(with_mt=True)
+    mt, idx = mt.cpu().numpy().view(np.uint32), idx.cpu().numpy()
+    for b in range(0, env.n, 131):
+        assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b], (ep, b)
+
+
+@pytest.mark.parametrize("ahead", [True, False])
+def test_play_seed_ahead_pipeline(Env, ahead):
+    """Consecutive hz_play calls (episodes 0, 1, 2 from seeded-ahead slots),
+    an hz_reset + hz_rollout in between (episode 3, re-primes the pipeline),
+    then episodes 4 and 5: every game bit-exact vs the oracle's episode."""
+    n, base = 4096, 2024
+    env = Env(n, seed_base=base, device=DEV)
+    env.set_seed_ahead(ahead)
+    for ep in range(3):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+    env.reset()
+    _, steps, _ = env.rollout(200)
+    _check_episode(env, base, 3, steps)
+    for ep in (4, 5):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+
+
+def test_play_after_auto_reset_mispredicts_safely(Env):
+    """hz_play with auto_reset moves episode counters by a board-dependent
+    amount, so the concurrent seed-ahead guesses wrong for some boards: the
+    next hz_play must still play every board's true next episode."""
+    n, base = 1024, 55
+    env = Env(n, seed_base=base, device=DEV)
+    env.rollout(200, reset=True)                                  # episode 0 everywhere
+    games, _, _ = env.rollout(64, auto_reset=True, reset=True)    # episode 1, then maybe 2
+    resets = games.cpu().numpy() - env.done().cpu().numpy().astype(np.int64)
+    nxt_ep = 2 + resets
+    assert len(set(nxt_ep.tolist())) > 1
+    _, steps, _ = env.rollout(200, reset=True)
+    st = states_of(env)
+    steps = steps.cpu().numpy()
+    for ep in sorted(set(nxt_ep.tolist())):
+        _, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=int(ep))
+        sel = nxt_ep == ep
+        assert (st[sel] == finals[sel]).all(), ep
+        assert (steps[sel] == plies[sel]).all(), ep
+
+
 def test_auto_reset_steady_state(Env):
     """auto_reset: board b's k-th game is seeded seed_base + b + (k << 32)."""
     n, base, plies = 256, 31, 150
