@@ -154,15 +154,35 @@ __host__ __device__ constexpr uint64_t valid35() {
 }
 constexpr uint64_t kValid35 = valid35();
 
-__device__ __forceinline__ uint64_t to35(uint32_t m) {
-  uint64_t g = 0;
-#pragma unroll
-  for (int c = 0; c < 23; c++) g |= (uint64_t)((m >> c) & 1u) << grid_bit(c);
-  return g;
+// Scoring layout: column-major with a guard row, bit = (q+3)*6 + (r+2).
+// Axial direction (dq,dr) is a shift by 6*dq + dr (+-1, +-5, +-6); every
+// wrap-around lands on a guard row (r = 3) or outside the 7 columns, masked
+// by kValid42.  A column's cells are consecutive cell indices with
+// consecutive r, so the conversion from the 23-bit cell set is 7 runs.
+__host__ __device__ constexpr int col_bit(int c) {
+  constexpr int Q[23] = {-3, -2, -2, -2, -1, -1, -1, -1, -1, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 3};
+  constexpr int R[23] = {2, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, 1, 2, -2, -1, 0, -2};
+  return (Q[c] + 3) * 6 + (R[c] + 2);
+}
+__host__ __device__ constexpr uint64_t valid42() {
+  uint64_t v = 0;
+  for (int c = 0; c < 23; c++) v |= 1ull << col_bit(c);
+  return v;
+}
+constexpr uint64_t kValid42 = valid42();
+static_assert(col_bit(0) == 4 && col_bit(1) == 8 && col_bit(4) == 12 && col_bit(9) == 18 && col_bit(14) == 24 &&
+                  col_bit(19) == 30 && col_bit(22) == 36,
+              "column runs");
+
+__device__ __forceinline__ uint64_t to42(uint32_t m) {
+  uint32_t lo = ((m & 1u) << 4) | (((m >> 1) & 7u) << 8) | (((m >> 4) & 31u) << 12) | (((m >> 9) & 31u) << 18) |
+                (((m >> 14) & 31u) << 24) | (((m >> 19) & 3u) << 30);
+  uint32_t hi = ((m >> 21) & 1u) | (((m >> 22) & 1u) << 4);  // bits 32 and 36
+  return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t nbr35(uint64_t s) {
-  return ((s << 1) | (s >> 1) | (s << 7) | (s >> 7) | (s << 6) | (s >> 6)) & kValid35;
+__device__ __forceinline__ uint64_t nbr42(uint64_t s) {
+  return ((s << 1) | (s >> 1) | (s << 5) | (s >> 5) | (s << 6) | (s >> 6)) & kValid42;
 }
 
 // ------------------------------------------------------------------ scoring
@@ -173,14 +193,86 @@ __device__ __forceinline__ int water_points(int len) {  // :18-27
   return 15 + (len - 6) * 4;
 }
 
+// The connected-component part of scoring for one 23-bit cell set S:
+// low byte  = number of components of size >= 2 (fields, :424-452: +5 each),
+// high byte = sum over those components of get_water_score(d + 1) with d the
+// component's graph diameter (water, :480-523).  Flood fill + BFS from every
+// cell; evaluated for all 2^23 sets once per process into kCompTable.
+__device__ __forceinline__ uint32_t comp_stats(uint32_t set23) {
+  uint64_t all = to42(set23);
+  uint64_t two = all & nbr42(all);  // cells of components of size >= 2
+  int ncomp = 0, wpts = 0;
+  while (two) {
+    uint64_t comp = two & (~two + 1);
+    for (;;) {
+      uint64_t nx = (comp | nbr42(comp)) & two;
+      if (nx == comp) break;
+      comp = nx;
+    }
+    two &= ~comp;
+    ncomp++;
+    int diam = 0;
+    uint64_t todo = comp;
+    while (todo) {
+      uint64_t reach = todo & (~todo + 1);
+      todo &= ~reach;
+      int d = 0;
+      for (;;) {
+        uint64_t nx = (reach | nbr42(reach)) & comp;
+        if (nx == reach) break;
+        reach = nx;
+        d++;
+      }
+      diam = d > diam ? d : diam;
+    }
+    wpts += water_points(diam + 1);
+  }
+  return (uint32_t)ncomp | ((uint32_t)wpts << 8);
+}
+
+constexpr uint32_t kCompTableSize = 1u << 23;  // u16 entries (16 MiB)
+
+namespace {
+// this translation unit's copy of the table pointer (install_comp_table)
+__device__ const uint16_t *g_comp_table;
+
+__global__ void __launch_bounds__(256) k_comp_table(uint16_t *__restrict__ t) {
+  uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s < kCompTableSize) t[s] = (uint16_t)comp_stats(s);
+}
+
+// Build the component table once per device (for this translation unit) and
+// point g_comp_table at it.  Host side; returns 0 on success.
+inline int install_comp_table() {
+  static const uint16_t *tables[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!tables[dev]) {
+    uint16_t *t = nullptr;
+    if (hipMalloc(&t, kCompTableSize * sizeof(uint16_t)) != hipSuccess) return 1;
+    hipLaunchKernelGGL(k_comp_table, dim3(kCompTableSize / 256), dim3(256), 0, 0, t);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(t);
+      return 1;
+    }
+    tables[dev] = t;
+  }
+  const uint16_t *p = tables[dev];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_comp_table), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+}  // namespace
+
 struct ScoreParts { int grass, mount, field, bldg, water; };
 
 __device__ __forceinline__ ScoreParts score_parts(const uint32_t b23[4]) {
+  // fields and water: one table load each (issued first)
+  uint32_t f23 = is_code<6>(b23), w23 = is_code<1>(b23);
+  uint32_t tf = g_comp_table[f23], tw = g_comp_table[w23];
   uint64_t b[4];
 #pragma unroll
-  for (int k = 0; k < 4; k++) b[k] = to35(b23[k]);
+  for (int k = 0; k < 4; k++) b[k] = to42(b23[k]);
   auto is = [&](int c) -> uint64_t {
-    uint64_t m = kValid35;
+    uint64_t m = kValid42;
     m &= (c & 1) ? b[0] : ~b[0];
     m &= (c & 2) ? b[1] : ~b[1];
     m &= (c & 4) ? b[2] : ~b[2];
@@ -189,75 +281,31 @@ __device__ __forceinline__ ScoreParts score_parts(const uint32_t b23[4]) {
   };
   ScoreParts r;
   // grass :369-390 (h1 plant 1; wood+plant 3; the h3 case is unreachable)
-  r.grass = __popcll(is(2)) + 3 * __popcll(is(7));
-  // mountains :392-422
+  r.grass = __popc(is_code<2>(b23)) + 3 * __popc(is_code<7>(b23));
+  // mountains :392-422: stone tops with a stone-top neighbour, by height
   uint64_t st1 = is(4), st2 = is(8), st3 = is(9);
   uint64_t stone = st1 | st2 | st3;
-  uint64_t adj = stone & nbr35(stone);
+  uint64_t adj = stone & nbr42(stone);
   r.mount = __popcll(adj & st1) + 3 * __popcll(adj & st2) + 7 * __popcll(adj & st3);
-  // fields :424-452 — +5 per connected component of size >= 2
-  uint64_t f = is(6);
-  uint64_t f2 = f & nbr35(f);
-  r.field = 0;
-  while (f2) {
-    uint64_t comp = f2 & (~f2 + 1);
-    for (;;) {
-      uint64_t nx = (comp | nbr35(comp)) & f2;
-      if (nx == comp) break;
-      comp = nx;
-    }
-    f2 &= ~comp;
-    r.field += 5;
-  }
-  // buildings :454-478 — building on top at height 2 with >= 3 distinct
-  // neighbouring top types
-  uint64_t tops[6];
-  tops[WATER] = is(1);
-  tops[PLANT] = is(2) | is(7);
-  tops[WOOD] = is(3);
-  tops[STONE] = stone;
-  tops[BUILDING] = is(5) | is(10) | is(11) | is(12);
-  tops[FIELD] = f;
+  // buildings :454-478 — a building on top at height 2 with >= 3 distinct
+  // neighbouring top types: per cell, count the types among its neighbours
+  // with a bit-sliced adder over the six "next to a t-top" sets
   uint64_t bh2 = is(10) | is(11) | is(12);
   r.bldg = 0;
-  while (bh2) {
-    uint64_t cbit = bh2 & (~bh2 + 1);
-    bh2 &= ~cbit;
-    uint64_t nb = nbr35(cbit);
-    int types = 0;
-#pragma unroll
-    for (int t = 0; t < 6; t++) types += (tops[t] & nb) ? 1 : 0;
-    if (types >= 3) r.bldg += 5;
+  if (bh2) {
+    uint64_t x0 = nbr42(is(1));                                 // water
+    uint64_t x1 = nbr42(is(2) | is(7));                         // plant
+    uint64_t x2 = nbr42(is(3));                                 // wood
+    uint64_t x3 = nbr42(stone);                                 // stone
+    uint64_t x4 = nbr42(is(5) | is(10) | is(11) | is(12));      // building
+    uint64_t x5 = nbr42(is(6));                                 // field
+    uint64_t s1 = x0 ^ x1 ^ x2, c1 = (x0 & x1) | (x2 & (x0 ^ x1));
+    uint64_t s2 = x3 ^ x4 ^ x5, c2 = (x3 & x4) | (x5 & (x3 ^ x4));
+    uint64_t ge3 = (c1 & c2) | ((c1 | c2) & (s1 | s2));
+    r.bldg = 5 * __popcll(ge3 & bh2);
   }
-  // water :480-523 — per component of size >= 2, graph diameter d
-  // (max BFS eccentricity inside the component), get_water_score(d + 1)
-  uint64_t w = tops[WATER];
-  uint64_t w2 = w & nbr35(w);
-  r.water = 0;
-  while (w2) {
-    uint64_t comp = w2 & (~w2 + 1);
-    for (;;) {
-      uint64_t nx = (comp | nbr35(comp)) & w2;
-      if (nx == comp) break;
-      comp = nx;
-    }
-    w2 &= ~comp;
-    int diam = 0;
-    uint64_t todo = comp;
-    while (todo) {
-      uint64_t reach = todo & (~todo + 1);
-      todo &= ~reach;
-      int d = 0;
-      for (;;) {
-        uint64_t nx = (reach | nbr35(reach)) & comp;
-        if (nx == reach) break;
-        reach = nx;
-        d++;
-      }
-      diam = d > diam ? d : diam;
-    }
-    r.water += water_points(diam + 1);
-  }
+  r.field = 5 * (int)(tf & 0xFF);
+  r.water = (int)(tw >> 8);
   return r;
 }
 
@@ -742,7 +790,16 @@ __device__ __forceinline__ void finish_game(State& s) {  // :344-354
   s.misc = m;
 }
 
-template <class Draw>
+// A finished game whose scoring is deferred (Defer = true, k_rollout): phase
+// game_over with winner None, a combination no reference state has.  The
+// caller scores it with finish_game at a point where the whole wave can do
+// it together.
+__device__ __forceinline__ void mark_over(State& s) { s.misc = set_bits(s.misc, 42, 3, PH_OVER); }
+__device__ __forceinline__ bool score_pending(uint64_t m) {
+  return phase_of(m) == PH_OVER && winner_code(m) == 0;
+}
+
+template <bool Defer = false, class Draw>
 __device__ __forceinline__ void end_turn(State& s, Draw& draw) {  // :301-329
   int p = player_of(s.misc);
   uint32_t b[4];
@@ -753,24 +810,29 @@ __device__ __forceinline__ void end_turn(State& s, Draw& draw) {  // :301-329
   replenish(s, draw);
   bool bag_trigger = bag_empty_before && npiles_of(s.piles) == 0;
   bool end = player_trigger || bag_trigger;
+  bool finish = false;
   if (end && !over_flag(s.misc)) {
     s.misc = set_bits(s.misc, 45, 1, 1);
     if (p == 0) {
       s.misc = set_bits(s.misc, 41, 1, 1);
       s.misc = set_bits(s.misc, 42, 3, PH_CHOOSE);
     } else {
-      finish_game(s);
+      finish = true;
     }
   } else if (over_flag(s.misc)) {
-    finish_game(s);
+    finish = true;
   } else {
     s.misc = set_bits(s.misc, 41, 1, (uint64_t)(1 - p));
     s.misc = set_bits(s.misc, 42, 3, PH_CHOOSE);
   }
+  if (finish) {
+    if constexpr (Defer) mark_over(s);
+    else finish_game(s);
+  }
 }
 
 // apply_move (:210-298) in place; returns a status (state untouched unless OK).
-template <class Draw>
+template <bool Defer = false, class Draw>
 __device__ __forceinline__ int step_state(State& s, int a, Draw& draw) {
   if (a < 0 || a >= kActions) return ST_BAD_ACTION;
   int ph = phase_of(s.misc);
@@ -808,7 +870,7 @@ __device__ __forceinline__ int step_state(State& s, int a, Draw& draw) {
     s.misc = set_bits(m, 9, 2, (uint64_t)(nh - 1));
     set_code(s, p, c, nc);
     if (ph < PH_P3) s.misc = set_bits(s.misc, 42, 3, (uint64_t)(ph + 1));
-    else end_turn(s, draw);
+    else end_turn<Defer>(s, draw);
     return ST_OK;
   }
   return ST_BAD_PHASE;

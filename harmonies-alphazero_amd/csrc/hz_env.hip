@@ -297,16 +297,17 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     }
 #ifdef HZ_DIAG
     uint64_t t0 = __builtin_amdgcn_s_memtime();
-    uint64_t acc8 = 0, acc9 = 0, acc10 = 0, acc11 = 0, acc12 = 0;
+    uint64_t acc8 = 0, acc9 = 0, acc10 = 0, acc11 = 0, acc12 = 0, acc13 = 0;
 #endif
     for (int i = 0; i < max_plies; i++) {
-      if (game_done(s.misc)) {
+      if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
         if (!auto_reset) {
           if (traj_action) {
             for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
           }
           break;
         }
+        if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
         int e = episode[b];
         sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
         episode[b] = e + 1;
@@ -336,13 +337,16 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
       HZ_ACC(10, t0);
       bool te = phase_of(s.misc) == PH_P3;
-      step_state(s, a, draw);
+      step_state<true>(s, a, draw);
       if (te) HZ_ACC(12, t0);
       else HZ_ACC(11, t0);
       g_ply++;
       steps++;
-      if (game_done(s.misc)) games++;
+      if (phase_of(s.misc) == PH_OVER) games++;
     }
+    // final scoring of the games that ended in this call, the whole wave at once
+    if (score_pending(s.misc)) finish_game(s);
+    HZ_ACC(13, t0);
     store_state(st, n, b, s);
     pos[b] = draw.m.cursor();
     ply[b] = g_ply;
@@ -350,7 +354,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #ifdef HZ_DIAG
     if (g_stamps) {
       uint64_t *o = g_stamps + (size_t)b * 16;
-      o[8] = acc8; o[9] = acc9; o[10] = acc10; o[11] = acc11; o[12] = acc12;
+      o[8] = acc8; o[9] = acc9; o[10] = acc10; o[11] = acc11; o[12] = acc12; o[13] = acc13;
     }
 #endif
     if (games_done) games_done[b] = games;
@@ -414,6 +418,7 @@ extern "C" {
 
 hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   if (n_boards <= 0) return nullptr;
+  if (install_comp_table()) return nullptr;  // scoring's component table (hz_device.hpp)
   hz_env *e = (hz_env *)calloc(1, sizeof(hz_env));
   if (!e) return nullptr;
   e->n = n_boards;

@@ -411,6 +411,7 @@ extern "C" {
 
 hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream) {
   if (n_boards <= 0 || max_nodes < 2 || max_depth < 1) return nullptr;
+  if (install_comp_table()) return nullptr;  // terminal expansions score boards
   hz_mcts *m = (hz_mcts *)calloc(1, sizeof(hz_mcts));
   if (!m) return nullptr;
   m->n = n_boards;

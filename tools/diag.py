@@ -29,5 +29,5 @@ for rep in range(3):
            "reset_total_cyc_max": (s[:, 4] - s[:, 0]).max().item(),
            "roll_top_cyc": s[:, 8].mean().item(), "roll_legal_cyc": s[:, 9].mean().item(),
            "roll_pick_cyc": s[:, 10].mean().item(), "roll_step_cyc": s[:, 11].mean().item(),
-           "roll_turnend_cyc": s[:, 12].mean().item()}
+           "roll_turnend_cyc": s[:, 12].mean().item(), "roll_final_cyc": s[:, 13].mean().item()}
 print(json.dumps(out))

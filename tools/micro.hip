@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(64) k_pick(const uint64_t *seedv, int n, int r
 
 extern "C" {
 int micro_run(int which, void *a, void *b, int n, int reps, void *sink, void *stream) {
+  if (install_comp_table()) return -1;
   dim3 g((n + 63) / 64), blk(64);
   hipStream_t s = (hipStream_t)stream;
   switch (which) {
