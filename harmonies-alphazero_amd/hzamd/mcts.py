@@ -125,18 +125,30 @@ class BatchedPredictor:
     """ModelManager.predict (model.py:81-110) for a whole batch: eval mode,
     no grad, softmax over all 143 logits (illegal moves are not masked)."""
 
-    def __init__(self, model, dtype=None):
+    def __init__(self, model, dtype=None, fold=True):
         self.model = model
         self.dtype = dtype
+        # eval-mode BatchNorm folded into the convs (hzamd.infer): same fp32
+        # arithmetic up to rounding, ~3x faster on MI355X at batch 4096
+        self.fast = None
+        if fold and hasattr(model, "residual_blocks"):
+            from .infer import FoldedNet
+            self.fast = FoldedNet(model)
+
+    def refresh(self):
+        """Re-fold after the model's weights changed."""
+        if self.fast is not None:
+            self.fast.refresh()
 
     @torch.no_grad()
     def __call__(self, board, glob):
         self.model.eval()
+        net = self.fast if self.fast is not None else self.model
         if self.dtype is not None and self.dtype != torch.float32:
             with torch.autocast(device_type="cuda", dtype=self.dtype):
-                logits, value = self.model(board, glob)
+                logits, value = net(board, glob)
         else:
-            logits, value = self.model(board, glob)
+            logits, value = net(board, glob)
         return torch.softmax(logits.float(), dim=1), value.float().reshape(-1)
 
 

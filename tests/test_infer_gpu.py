@@ -1,0 +1,31 @@
+"""FoldedNet on the GPU (MIOpen NHWC convs) against the unfolded eval-mode
+network run on the CPU in fp32: max |diff| <= 2e-3 on logits and values at
+batch 512 with non-trivial BatchNorm statistics (different conv algorithms
+and summation orders on the two devices)."""
+import pytest
+import torch
+
+from hzamd.infer import FoldedNet
+from hzamd.mcts import BatchedPredictor
+from hzamd.net import HarmoniesNet
+from test_infer_cpu import _randomise_bn
+
+pytestmark = pytest.mark.gpu
+
+
+def test_folded_gpu_matches_cpu_reference():
+    g = torch.Generator().manual_seed(5)
+    torch.manual_seed(0)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    board = (torch.rand(512, 38, 5, 7, generator=g) > 0.8).float()
+    glob = torch.rand(512, 42, generator=g)
+    with torch.no_grad():
+        l0, v0 = net(board, glob)
+    gnet = net.to("cuda")
+    l1, v1 = FoldedNet(gnet)(board.cuda(), glob.cuda())
+    assert (l1.cpu() - l0).abs().max().item() <= 2e-3
+    assert (v1.cpu() - v0).abs().max().item() <= 2e-3
+    p, v = BatchedPredictor(gnet)(board.cuda(), glob.cuda())
+    assert (p.cpu() - torch.softmax(l0, 1)).abs().max().item() <= 2e-3
+    assert (v.cpu() - v0.reshape(-1)).abs().max().item() <= 2e-3

@@ -35,4 +35,16 @@ for name, dtype, cl in [("fp32", None, False), ("fp32_cl", None, True), ("bf16",
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / R
     res[name] = {"ms": dt * 1e3, "tflops": flops_per_eval() * B / dt / 1e12}
+from hzamd.infer import FoldedNet
+fn = FoldedNet(net.to(memory_format=torch.contiguous_format))
+with torch.no_grad():
+    for _ in range(3):
+        fn(board, glob)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(10):
+        fn(board, glob)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / 10
+res["fp32_folded"] = {"ms": dt * 1e3, "tflops": flops_per_eval() * B / dt / 1e12}
 print(json.dumps(res))
