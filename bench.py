@@ -172,12 +172,12 @@ def main():
     steps = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def one_step(ev=None):
+    def one_step(ev=None, g=games, s=steps):
         # hz_play: HarmoniesGameState() on every board fused with rule-driven
         # play to the end of the game, one launch
         if ev:
             ev[0].record(stream)
-        env.rollout(MAX_PLIES, games_done=games, steps_done=steps, reset=True)
+        env.rollout(MAX_PLIES, games_done=g, steps_done=s, reset=True)
         if ev:
             ev[1].record(stream)
 
@@ -189,39 +189,41 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         one_step()
     torch.cuda.synchronize(dev)
-    env_steps_per_step = int(steps.sum().item())
-    games_per_step = int(games.sum().item())
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
+    # per-step counters of the timed launches (each step plays a new episode)
+    games_t = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
+    steps_t = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_step(evs[i])
+        one_step(evs[i], games_t[i], steps_t[i])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
+    timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-        c = torch.tensor([env_steps_per_step, games_per_step], dtype=torch.int64, device=dev)
+        c = torch.tensor([timed_steps, timed_games], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         env_steps_all, games_all = int(c[0]), int(c[1])
     else:
-        env_steps_all, games_all = env_steps_per_step, games_per_step
+        env_steps_all, games_all = timed_steps, timed_games
 
-    value = env_steps_all * args.steps / elapsed
-    games_per_s = games_all * args.steps / elapsed
+    value = env_steps_all / elapsed
+    games_per_s = games_all / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # roofline of the dominant kernel (hz_play = k_rollout with reset), per launch
-    alg_bytes = env_steps_per_step * BYTES_PER_ENV_STEP + games_per_step * BYTES_PER_RESET
+    alg_bytes = (timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET) / args.steps
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -255,8 +257,8 @@ def main():
             "data": "synthetic: CPython-seeded games, seeds = global board id, build-defined splitmix rule policy",
             "config": {"workload": "config2: 4096 concurrent boards/GPU, reset + rule-driven play to game end "
                                    "(legal mask, step, chance draws, final scoring), one hz_play launch",
-                       "boards_per_gpu": n, "env_steps_per_step": env_steps_per_step,
-                       "games_per_step": games_per_step, "parallelism": f"shard{world}"},
+                       "boards_per_gpu": n, "env_steps_per_step": timed_steps / args.steps,
+                       "games_per_step": timed_games / args.steps, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rollout", "kernel_ms": kern_ms,

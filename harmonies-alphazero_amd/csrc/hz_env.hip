@@ -388,6 +388,63 @@ __global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restri
   stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
 }
 
+// ---------------------------------------------------------- greedy agent
+// evaluation.py:137-196 choose_move_greedy, one wave per board: lane l scores
+// legal moves l, l+64 (canonical ascending order) by applying the placement
+// to a register copy and scoring the mover's board; a shuffle reduction keeps
+// the first strictly best.  The reference applies every candidate with
+// apply_move, whose place_tile_3 turn end refills the piles from the global
+// `random`: lane 0 replays those L refills (identical bag and piles for every
+// candidate) on the board's stream before the real move is stepped.
+struct NoDraw {
+  __device__ __forceinline__ uint32_t operator()(uint64_t) { return 0x1FFu; }
+};
+
+__global__ void __launch_bounds__(64) k_greedy(const uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
+                                               int32_t *__restrict__ pos, int n, const uint8_t *__restrict__ sel,
+                                               int16_t *__restrict__ action) {
+  int b = blockIdx.x, lane = threadIdx.x;
+  if (b >= n) return;
+  bool on = !sel || sel[b];
+  State s = load_state(st, n, b);
+  uint64_t mk[3];
+  int L = legal_mask(s, mk);
+  if (!on || game_done(s.misc) || L == 0) {
+    if (lane == 0) action[b] = -1;
+    return;
+  }
+  int ph = phase_of(s.misc), p = player_of(s.misc);
+  int best_sc = -1, best_k = 0x7fffffff;
+  for (int k = lane; k < L; k += 64) {
+    int sc;
+    if (ph == PH_CHOOSE) {
+      sc = score_player(s, p);  // choosing a pile leaves the board as it is
+    } else {
+      State t = s;
+      NoDraw nd;
+      step_state<true>(t, kth_action(mk, k), nd);
+      sc = score_player(t, p);
+    }
+    if (sc > best_sc) { best_sc = sc; best_k = k; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    int osc = __shfl_xor(best_sc, off), ok = __shfl_xor(best_k, off);
+    if (osc > best_sc || (osc == best_sc && ok < best_k)) { best_sc = osc; best_k = ok; }
+  }
+  if (lane == 0) {
+    if (ph == PH_P3) {
+      StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
+      for (int k = 0; k < L; k++) {
+        State t = s;
+        replenish(t, d);
+      }
+      pos[b] = d.m.cursor();
+    }
+    action[b] = (int16_t)kth_action(mk, best_k);
+  }
+}
+
 // ---------------------------------------------------------- state transfer
 __global__ void __launch_bounds__(kBlock) k_mt_normalize(uint32_t *__restrict__ mt, int32_t *__restrict__ pos,
                                                          int n, int32_t *__restrict__ index) {
@@ -563,6 +620,12 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
 // seeded-ahead stream only when the slot's tag equals its episode counter,
 // so the results never depend on it.  Anything else that moves episode
 // counters (hz_reset, hz_rollout) re-primes with a copy of the counters.
+int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
+  if (!e || !action) return -1;
+  hipLaunchKernelGGL(k_greedy, dim3(e->n), dim3(64), 0, e->stream, e->state, e->mt, e->pos, e->n, sel, action);
+  return launch_err();
+}
+
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;

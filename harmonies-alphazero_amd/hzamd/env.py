@@ -133,6 +133,18 @@ class BatchedEnv:
                   "hz_rule_actions")
         return out
 
+    def greedy_actions(self, sel=None, out=None):
+        """choose_move_greedy (evaluation.py:137-196) for every board (or where
+        sel != 0): int16 [n], -1 where finished / unselected.  Consumes the
+        chance streams like the reference's simulated apply_move calls; apply
+        the result with step()."""
+        self._sync_stream()
+        if sel is not None:
+            sel = sel.to(device=self.device, dtype=torch.uint8).contiguous()
+        out = torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None else out
+        nat.check(nat.lib().hz_greedy_actions(self._h, nat.ptr(sel), nat.ptr(out)), "hz_greedy_actions")
+        return out
+
     def rollout(self, max_plies, auto_reset=False, record=False, games_done=None, steps_done=None, reset=False):
         """Fused rule-driven play of up to max_plies plies per board
         (reset=True: start every board's next game first, in the same launch)."""

@@ -103,6 +103,16 @@ int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_s
  * ascending action order.  Writes action[b] (-1 if no legal move). */
 int hz_rule_actions(hz_env *env, const uint64_t *mask, const int32_t *count, int16_t *action);
 
+/* evaluation.py:137-196 choose_move_greedy for every selected board (sel may
+ * be NULL = all): the legal move whose resulting board scores highest for the
+ * player to move, first strictly best in ascending action order.  Like the
+ * reference, whose simulated apply_move calls refill the piles from the
+ * global `random` at the end of a turn, it consumes each board's chance
+ * stream once per candidate when the phase is place_tile_3; apply the
+ * returned move with hz_step.  action[b] = -1 when unselected, finished or
+ * without a legal move. */
+int hz_greedy_actions(hz_env *env, const uint8_t *sel, int16_t *action);
+
 /* Fused env loop: every board plays up to max_plies rule-driven plies
  * (legal mask -> rule pick -> step), stopping at game end (auto_reset = 0) or
  * starting its next game (auto_reset != 0).  Optional per-ply records

@@ -122,6 +122,12 @@ def step(st, action, m):
     return r, st
 
 
+def greedy_move(st, m):
+    """choose_move_greedy's action index (consumes m like the reference)."""
+    st = np.ascontiguousarray(st, np.int16)
+    return lib().or_greedy_move(_p(st), ctypes.byref(m))
+
+
 def score_board(cells23):
     cells = np.ascontiguousarray(cells23, np.uint8)
     out = np.zeros(5, np.int32)

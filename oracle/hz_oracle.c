@@ -835,3 +835,34 @@ int or_mcts_search(const int16_t *root_ref, or_mt *m, const or_mcts_cfg *cfg, co
   free(t.nodes); free(t.edges); free(t.hslot);
   return best;
 }
+
+/* ---------------------------------------------------------- greedy agent
+ * evaluation.py:137-196 choose_move_greedy: apply every legal move (in the
+ * canonical ascending action order) to a copy of the state — each apply
+ * consumes the chance stream exactly like the reference's apply_move, whose
+ * turn end refills the piles from the global `random` — score the copy for
+ * the player to move, keep the first strictly best.  Returns the action, or
+ * -1 when there is no legal move. */
+int or_greedy_move(const int16_t *st, or_mt *m) {
+  uint8_t mask[143];
+  int L = or_legal(st, mask);
+  if (!L) return -1;
+  int p = st[72];
+  int best = -1, best_score = -1;
+  for (int a = 0; a < 143; a++) {
+    if (!mask[a]) continue;
+    int16_t t[OR_REFSTATE];
+    memcpy(t, st, sizeof(t));
+    if (or_step(t, a, m)) continue; /* the reference skips moves that raise */
+    uint8_t cells[23];
+    for (int c = 0; c < 23; c++) cells[c] = (uint8_t)t[p * 23 + c];
+    int32_t parts[5];
+    or_score_board(cells, parts);
+    int sc = parts[0] + parts[1] + parts[2] + parts[3] + parts[4];
+    if (sc > best_score) {
+      best_score = sc;
+      best = a;
+    }
+  }
+  return best;
+}

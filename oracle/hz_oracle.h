@@ -42,6 +42,9 @@ int  or_is_game_over(const int16_t *st);
 void or_encode(const int16_t *st, float *board1330, float *glob42);
 void or_canonical(const int16_t *st, uint8_t *key128, int pyhash);
 
+/* evaluation.py choose_move_greedy; consumes m like the reference. */
+int or_greedy_move(const int16_t *st, or_mt *m);
+
 /* Build-defined action rule used by the env benchmark / fixtures. */
 uint64_t or_rule(uint64_t seed, uint64_t ply);
 

@@ -17,13 +17,18 @@ Fixtures (all int arrays unless noted; REFSTATE = 78 x int16, see `ref_state`):
   encoder.npz        create_state_tensors() outputs (f32) at sampled states.
   scoring.npz        per-habitat scores of the known-answer board
                      and of random reachable-stack boards.
+  greedy.npz         greedy-vs-greedy games of evaluation.choose_move_greedy
+                     (canonical move order): per-ply REFSTATE + chosen action,
+                     final state and next MT word (the greedy agent's
+                     simulated apply_move calls consume `random` too).
   mcts.npz           get_best_action_and_pi() root visit counts, chosen move,
                      tree size and next MT word under a canonical (ascending
                      action index) move order and a deterministic stub
                      evaluator; testing=True and testing=False (noise/choice
                      injected through patched numpy calls).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [part ...]
+        (parts: mt env encoder scoring mcts greedy; default all)
 """
 import logging
 import os
@@ -361,16 +366,51 @@ def capture_mcts(he, pgs, mcts_mod, states, sorted_coords, idx_of):
     np.savez_compressed(os.path.join(OUT, "mcts.npz"), **out)
 
 
+def capture_greedy(he, pgs, idx_of, seeds=range(5000, 5032)):
+    """Greedy (P0) vs greedy (P1) through evaluation.play_game's loop
+    (evaluation.py:68-133) with evaluation.choose_move_greedy (:137-196)."""
+    import evaluation as ev
+    orig = he.HarmoniesGameState.get_legal_moves
+    he.HarmoniesGameState.get_legal_moves = lambda self: sorted(orig(self), key=pgs.get_action_index)
+    st, ac, off, fin, nxt = [], [], [0], [], []
+    try:
+        for seed in seeds:
+            random.seed(seed)
+            g = he.HarmoniesGameState()
+            while not g.is_game_over():
+                mv, _ = ev.choose_move_greedy(g.clone())
+                st.append(ref_state(g, idx_of))
+                ac.append(pgs.get_action_index(mv))
+                g = g.apply_move(mv)
+            off.append(len(st))
+            fin.append(ref_state(g, idx_of))
+            nxt.append(random.getrandbits(32))
+    finally:
+        he.HarmoniesGameState.get_legal_moves = orig
+    np.savez_compressed(os.path.join(OUT, "greedy.npz"), seeds=np.array(list(seeds), np.uint64),
+                        states=np.array(st, np.int16), actions=np.array(ac, np.int16),
+                        offsets=np.array(off, np.int32), finals=np.array(fin, np.int16),
+                        next_word=np.array(nxt, np.uint32))
+
+
 def main():
+    parts = set(sys.argv[1:]) or {"mt", "env", "encoder", "scoring", "mcts", "greedy"}
     he, pgs, mcts_mod = import_reference()
     import constants as C
     sorted_coords = list(C.sorted_coords)
     idx_of = {c: i for i, c in enumerate(sorted_coords)}
-    capture_mt()
-    states = capture_env(he, pgs, idx_of)
-    capture_encoder(he, pgs, states, sorted_coords, idx_of)
-    capture_scoring(he, sorted_coords, idx_of)
-    capture_mcts(he, pgs, mcts_mod, states, sorted_coords, idx_of)
+    if "mt" in parts:
+        capture_mt()
+    if parts & {"env", "encoder", "mcts"}:
+        states = capture_env(he, pgs, idx_of)
+        if "encoder" in parts:
+            capture_encoder(he, pgs, states, sorted_coords, idx_of)
+        if "mcts" in parts:
+            capture_mcts(he, pgs, mcts_mod, states, sorted_coords, idx_of)
+    if "scoring" in parts:
+        capture_scoring(he, sorted_coords, idx_of)
+    if "greedy" in parts:
+        capture_greedy(he, pgs, idx_of)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

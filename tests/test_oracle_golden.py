@@ -109,3 +109,22 @@ def test_mcts_matches_reference(k):
     assert a == f["action"][k]
     assert (nn, ne) == (f["n_nodes"][k], f["n_edges"][k])
     assert oracle.mt_next32(m) == f["next_word"][k]
+
+
+def test_greedy_games_match_reference():
+    """evaluation.choose_move_greedy games (greedy.npz): every state, every
+    chosen action, the final state and the next CPython word — the greedy
+    agent's simulated apply_move calls consume `random` like real moves."""
+    f = np.load(os.path.join(GOLDEN, "greedy.npz"))
+    off = f["offsets"]
+    for g in range(len(f["seeds"])):
+        m = oracle.mt_seed(int(f["seeds"][g]))
+        s = oracle.reset(m)
+        for p in range(off[g], off[g + 1]):
+            assert (s == f["states"][p]).all(), (g, p - off[g])
+            a = oracle.greedy_move(s, m)
+            assert a == f["actions"][p], (g, p - off[g])
+            r, s = oracle.step(s, a, m)
+            assert r == 0
+        assert (s == f["finals"][g]).all() and oracle.is_game_over(s)
+        assert oracle.mt_next32(m) == f["next_word"][g]
