@@ -21,6 +21,10 @@ Fixtures (all int arrays unless noted; REFSTATE = 78 x int16, see `ref_state`):
                      (canonical move order): per-ply REFSTATE + chosen action,
                      final state and next MT word (the greedy agent's
                      simulated apply_move calls consume `random` too).
+  train.npz          ModelManager.train_step (model.py:112-157) on the test
+                     model config: initial / final state_dict, batch, losses;
+  ref_ckpt_tiny.pth.tar  the same manager's save_checkpoint (model.py:159-182)
+                     output after those steps (iteration 7), for the loader.
   mcts.npz           get_best_action_and_pi() root visit counts, chosen move,
                      tree size and next MT word under a canonical (ascending
                      action index) move order and a deterministic stub
@@ -28,7 +32,7 @@ Fixtures (all int arrays unless noted; REFSTATE = 78 x int16, see `ref_state`):
                      injected through patched numpy calls).
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [part ...]
-        (parts: mt env encoder scoring mcts greedy; default all)
+        (parts: mt env encoder scoring mcts greedy train; default all)
 """
 import logging
 import os
@@ -393,8 +397,43 @@ def capture_greedy(he, pgs, idx_of, seeds=range(5000, 5032)):
                         next_word=np.array(nxt, np.uint32))
 
 
+def capture_train():
+    """Three ModelManager.train_step calls on one fixed batch with the
+    reference's test model/training configs (CPU, fp32), plus the checkpoint
+    save_checkpoint writes afterwards."""
+    import shutil
+    import tempfile
+    import torch
+    import config as cfg
+    from model import ModelManager
+    tcfg = dict(cfg.test_training_config, device="cpu")
+    torch.manual_seed(0)
+    mm = ModelManager(cfg.test_model_config, tcfg)
+    init = {k: v.detach().clone().numpy() for k, v in mm.model.state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    B = 8
+    board = (torch.rand(B, 38, 5, 7, generator=g) > 0.8).float()
+    glob = torch.rand(B, 42, generator=g)
+    vis = torch.randint(0, 20, (B, 143), generator=g).float()
+    pi = vis / vis.sum(1, keepdim=True)
+    z = torch.randint(-1, 2, (B, 1), generator=g).float()
+    losses = [mm.train_step(board, glob, pi, z) for _ in range(3)]
+    final = {k: v.detach().clone().numpy() for k, v in mm.model.state_dict().items()}
+    out = {"board": board.numpy(), "glob": glob.numpy(), "pi": pi.numpy(), "z": z.numpy(),
+           "losses": np.array(losses, np.float64)}
+    out.update({"init/" + k: v for k, v in init.items()})
+    out.update({"final/" + k: v for k, v in final.items()})
+    np.savez_compressed(os.path.join(OUT, "train.npz"), **out)
+    d = tempfile.mkdtemp()
+    try:
+        mm.save_checkpoint(folder=d, filename="ck.pth.tar", iteration=7)
+        shutil.copy(os.path.join(d, "ck.pth.tar"), os.path.join(OUT, "ref_ckpt_tiny.pth.tar"))
+    finally:
+        shutil.rmtree(d)
+
+
 def main():
-    parts = set(sys.argv[1:]) or {"mt", "env", "encoder", "scoring", "mcts", "greedy"}
+    parts = set(sys.argv[1:]) or {"mt", "env", "encoder", "scoring", "mcts", "greedy", "train"}
     he, pgs, mcts_mod = import_reference()
     import constants as C
     sorted_coords = list(C.sorted_coords)
@@ -411,6 +450,8 @@ def main():
         capture_scoring(he, sorted_coords, idx_of)
     if "greedy" in parts:
         capture_greedy(he, pgs, idx_of)
+    if "train" in parts:
+        capture_train()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

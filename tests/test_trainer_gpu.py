@@ -1,0 +1,67 @@
+"""The batched training loop (hzamd.trainer.Trainer, trainer.py's phases) end
+to end on one GPU with the reference's test configs (config.py test_*):
+self-play -> device replay buffer -> training -> checkpoint -> buffer file
+-> evaluation arena, two iterations; then a resume from the candidate
+checkpoint and the reference-pickle export of the buffer."""
+import collections
+import os
+import pickle
+
+import pytest
+import torch
+
+from hzamd import buffer_io
+from hzamd.manager import ModelManager
+from hzamd.trainer import Trainer
+from test_manager_cpu import MODEL_CFG
+
+pytestmark = pytest.mark.gpu
+
+TRAIN = {"device": "cuda", "optimizer_type": "Adam", "learning_rate": 0.001, "weight_decay": 0.0,
+         "value_loss_weight": 1.0, "policy_loss_weight": 1.0, "batch_size": 4, "momentum": 0.9,
+         "use_scheduler": True, "scheduler_type": "StepLR", "scheduler_step_size": 30, "scheduler_gamma": 0.5,
+         "force_lr_reset_on_load": False, "new_forced_lr": 0.000125}
+MCTS = {"num_simulations": 4, "cpuct": 1.0, "dirichlet_alpha": 0.3, "dirichlet_epsilon": 0.0, "fpu_value": 0.25,
+        "turns_until_tau0": 0, "action_size": 143, "testing": True}
+EVAL = {"num_simulations": 4, "cpuct": 1.0, "dirichlet_alpha": 0.1, "dirichlet_epsilon": 0.0,
+        "turns_until_tau0": 0, "testing": True}
+
+
+def sp_cfg(tmp):
+    return {"num_iterations": 2, "num_games_per_iter": 8, "epochs_per_iter": 1, "replay_buffer_size": 1000,
+            "checkpoint_folder": str(tmp / "ck"), "replay_buffer_folder": str(tmp / "buf"),
+            "replay_buffer_filename": "test_replay_buffer.pkl", "eval_frequency": 2, "eval_episodes": 4,
+            "eval_win_rate_threshold": 0.55, "best_model_filename": "test_best_model.pth.tar",
+            "export_reference_pickle": True}
+
+
+def test_training_loop_end_to_end(tmp_path):
+    torch.manual_seed(0)
+    cfg = sp_cfg(tmp_path)
+    mm = ModelManager(MODEL_CFG, TRAIN)
+    tr = Trainer(mm, MCTS, cfg, TRAIN, eval_mcts_config=EVAL, seed_base=11, log=lambda *_: None)
+    hist = tr.run_training_loop()
+    assert [h["iteration"] for h in hist] == [1, 2]
+    ex = sum(h["self_play"]["examples"] for h in hist)
+    assert len(tr.replay_buffer) == min(ex, 1000)
+    assert all(h["training"] is not None and h["training"]["loss"] == h["training"]["loss"] for h in hist)
+    assert hist[1]["evaluation"] is not None and hist[0]["evaluation"] is None
+    e = hist[1]["evaluation"]
+    assert e["wins"] + e["losses"] + e["draws"] == 4
+    assert os.path.exists(tmp_path / "ck" / "latest_candidate.pth.tar")
+    assert os.path.exists(tmp_path / "ck" / "test_best_model.pth.tar")
+    rec, maxlen = buffer_io.load_compact(tmp_path / "buf" / "test_replay_buffer.hz.npz", "cuda")
+    assert maxlen == 1000 and torch.equal(rec, tr.replay_buffer.records())
+    with open(tmp_path / "buf" / "test_replay_buffer.pkl", "rb") as f:   # our own file
+        buf = pickle.load(f)
+    assert isinstance(buf, collections.deque) and buf.maxlen == 1000 and len(buf) == len(tr.replay_buffer)
+    b, g, pi, z = buf[0]
+    assert b.shape == (38, 5, 7) and g.shape == (42,) and pi.shape == (143,) and z.shape == (1,)
+    assert abs(float(pi.sum()) - 1.0) < 1e-5 and float(z) in (-1.0, 0.0, 1.0)
+    # resume: the loop continues after the saved candidate iteration
+    mm2 = ModelManager(MODEL_CFG, TRAIN)
+    tr2 = Trainer(mm2, MCTS, dict(cfg, num_iterations=3), TRAIN, eval_mcts_config=EVAL, seed_base=11,
+                  log=lambda *_: None)
+    assert len(tr2.replay_buffer) == len(tr.replay_buffer)
+    hist2 = tr2.run_training_loop()
+    assert [h["iteration"] for h in hist2] == [3]
