@@ -428,7 +428,18 @@ struct LdsMT {
     if (pos >= kMT) return;
     while (tw < kMT) tw += twist_block(w(), kLdsStride, tw);
   }
+
+  // start the next generation now and twist its first `target` words
+  // (k_seed_ahead: a typical game then never twists)
+  __device__ __forceinline__ void twist_ahead(int target) {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    while (tw < target) tw += twist_block(w(), kLdsStride, tw);
+  }
 };
+
+// cursor of a seeded-ahead stream: fresh generation, kAheadTwist words twisted
+constexpr int kAheadTwist = 224;
+constexpr int kMTAhead = 0 | (kAheadTwist << 16);
 
 // init_genrand(19650218) (_randommodule.c), the starting array of
 // init_by_array: the same for every seed, so it is a constant table read
@@ -745,38 +756,51 @@ __device__ __forceinline__ int legal_mask(const State& s, uint64_t mask[3]) {
   int count = 0;
 #pragma unroll
   for (int t = 0; t < 6; t++) {
-    if (!(has & (1u << t))) continue;
     uint32_t m = empty;
     if (t == PLANT) m |= wood1;
     if (t == STONE) m |= stone1 | stone2;
     if (t == BUILDING) m |= wood1 | stone1 | bld1;
+    m = (has >> t) & 1u ? m : 0u;  // branch-free: same instructions on every lane
     or_range(mask, 5 + 23 * t, m);
     count += __popc(m);
   }
   return count;
 }
 
-__device__ __forceinline__ int select64(uint64_t w, int k) {
+// position of the k-th (0-based) set bit of a 32-bit word, branch-free
+__device__ __forceinline__ int select32(uint32_t w, int k) {
   int pos = 0;
 #pragma unroll
-  for (int s = 32; s > 0; s >>= 1) {
-    uint64_t lo = w & ((1ull << s) - 1);
-    int c = __popcll(lo);
-    if (k >= c) { k -= c; w >>= s; pos += s; }
-    else w = lo;
+  for (int s = 16; s > 0; s >>= 1) {
+    uint32_t lo = w & ((1u << s) - 1);
+    int c = __popc(lo);
+    bool up = k >= c;
+    k = up ? k - c : k;
+    w = up ? w >> s : lo;
+    pos += up ? s : 0;
   }
   return pos;
 }
 
-// k-th (0-based) legal action in ascending action order.
+// k-th (0-based) legal action in ascending action order: the 32-bit word
+// holding it is found by prefix popcounts, then one branch-free select
+// (every lane runs the same instructions whatever word its action is in).
 __device__ __forceinline__ int kth_action(const uint64_t mask[3], int k) {
-  int c0 = __popcll(mask[0]);
-  if (k < c0) return select64(mask[0], k);
-  k -= c0;
-  int c1 = __popcll(mask[1]);
-  if (k < c1) return 64 + select64(mask[1], k);
-  k -= c1;
-  return 128 + select64(mask[2], k);
+  uint32_t w[5] = {(uint32_t)mask[0], (uint32_t)(mask[0] >> 32), (uint32_t)mask[1], (uint32_t)(mask[1] >> 32),
+                   (uint32_t)mask[2]};
+  uint32_t word = w[4];
+  int base = 128, pre = 0;
+  bool found = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    int c = __popc(w[i]);
+    bool here = !found && k - pre < c;
+    word = here ? w[i] : word;
+    base = here ? 32 * i : base;
+    found = found || here;
+    pre += found ? 0 : c;
+  }
+  return base + select32(word, k - pre);
 }
 
 // ------------------------------------------------------------------- step
@@ -979,17 +1003,25 @@ __device__ __forceinline__ bool key_eq(const CKey& a, const CKey& b) {
 }
 
 // ------------------------------------------------------------ action rule
-__device__ __forceinline__ uint64_t rule_hash(uint64_t seed, uint64_t ply) {
-  uint64_t x = seed * 0x9E3779B97F4A7C15ULL + ply;
-  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+__device__ __forceinline__ uint64_t rule_key(uint64_t seed) {  // the per-game part of rule_hash
+  return seed * 0x9E3779B97F4A7C15ULL + 0x9E3779B97F4A7C15ULL;
+}
+__device__ __forceinline__ uint64_t rule_hash_k(uint64_t key, uint64_t ply) {
+  uint64_t z = key + ply;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
   return z ^ (z >> 31);
 }
+__device__ __forceinline__ uint64_t rule_hash(uint64_t seed, uint64_t ply) {
+  return rule_hash_k(rule_key(seed), ply);
+}
 
+__device__ __forceinline__ int rule_pick_k(uint64_t key, int ply, int n_legal) {
+  uint32_t hi = (uint32_t)(rule_hash_k(key, (uint64_t)ply) >> 32);
+  return (int)(((uint64_t)hi * (uint32_t)n_legal) >> 32);
+}
 __device__ __forceinline__ int rule_pick(uint64_t seed, int ply, int n_legal) {
-  uint64_t z = rule_hash(seed, (uint64_t)ply);
-  return (int)(((z >> 32) * (uint64_t)n_legal) >> 32);
+  return rule_pick_k(rule_key(seed), ply, n_legal);
 }
 
 // ------------------------------------------------------------ SoA access

@@ -279,13 +279,14 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   else if (seededmask) stage_mt(const_cast<uint32_t *>(ahead_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
   __syncthreads();
   if (w0 && act) {
-    StreamDraw<LdsMT> draw{LdsMT(lane, reset_first ? kMTSeeded : pos[b])};
+    StreamDraw<LdsMT> draw{LdsMT(lane, reset_first ? (seeded ? kMTAhead : kMTSeeded) : pos[b])};
     State s;
     int g_ply, games = 0, steps = 0;
-    uint64_t sd;
+    uint64_t sd, rkey;
     if (reset_first) {
       int e = episode[b];
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+      rkey = rule_key(sd);
       episode[b] = e + 1;
       if (!seeded) mt_seed(hz_lds + lane, kLdsStride, sd);
       reset_state(s, draw);
@@ -294,6 +295,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       s = load_state(st, n, b);
       g_ply = ply[b];
       sd = seed[b];
+      rkey = rule_key(sd);
     }
 #ifdef HZ_DIAG
     uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -310,6 +312,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
         int e = episode[b];
         sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+        rkey = rule_key(sd);
         episode[b] = e + 1;
         mt_seed(hz_lds + lane, kLdsStride, sd);
         draw.m = LdsMT(lane, kMTSeeded);
@@ -333,7 +336,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         if (traj_action) traj_action[(size_t)i * n + b] = -1;
         break;
       }
-      int a = kth_action(mk, rule_pick(sd, g_ply, L));
+      int a = kth_action(mk, rule_pick_k(rkey, g_ply, L));
       if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
       HZ_ACC(10, t0);
       bool te = phase_of(s.misc) == PH_P3;
@@ -382,6 +385,8 @@ __global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restri
   if (tid < 64 && act) {
     int e = ep_final[b] + 1;
     mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
+    LdsMT m(lane, kMTSeeded);
+    m.twist_ahead(kAheadTwist);  // cursor kMTAhead
     tag[b] = e;
   }
   __syncthreads();
