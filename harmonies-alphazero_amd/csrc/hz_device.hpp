@@ -564,42 +564,75 @@ __device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[
 
 // LDS stream: branch-free scan of the next 24 twisted words (the wave leaves
 // early once every lane has its picks; a lane needs more than 24 words with
-// probability ~1e-5 and then finishes serially).
-__device__ __forceinline__ void sample3_raw(LdsMT& m, uint32_t n, int k, uint32_t j[3]) {
-  uint32_t j0 = 0, j1 = 0, j2 = 0;
-  int got = 0, used = 0;
+// probability ~1e-5 and then finishes serially).  The words are read twelve
+// ahead, four more per step of four, at immediate offsets from the lane's
+// cursor row (Clamp: near the end of a generation, rows clamped to 623; the
+// rows past tw are never live).  Unset picks hold a sentinel no value < n
+// equals, so the distinctness test needs no pick count.
+template <bool Clamp>
+__device__ __forceinline__ uint32_t scan_word(const LdsMT& m, int t) {
+  if (Clamp) {
+    int i = m.pos + t < kMT ? m.pos + t : kMT - 1;
+    return hz_lds[i * kLdsStride + m.lane];
+  }
+  return hz_lds[(m.pos + t) * kLdsStride + m.lane];
+}
+
+// the top 14 bits of temper(y): its last step (y ^= y >> 18) leaves them
+// unchanged; every draw keeps at most 7 (the bag never exceeds 120 tiles)
+__device__ __forceinline__ uint32_t temper_top14(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  return y;
+}
+
+template <bool Clamp, bool Set>
+__device__ __forceinline__ void scan24(const LdsMT& m, uint32_t n, int k, uint32_t& j0, uint32_t& j1,
+                                       uint32_t& j2, int& got, int& used) {
   int avail = m.tw - m.pos;
+  bool pool = !Set && n <= 21;
+  int sh0 = __clz(n), sh1 = __clz(n > 1 ? n - 1 : 1), sh2 = __clz(n > 2 ? n - 2 : 1);
+  // three segments of eight words; each segment's words are read together
+  // (one LDS wait), the wave stops after a segment once every lane is done
+#pragma unroll
+  for (int seg = 0; seg < 3; seg++) {
+    if (seg > 0 && __all(got >= k)) break;
+    uint32_t w[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) w[u] = scan_word<Clamp>(m, 8 * seg + u);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      int t = 8 * seg + u;
+      bool lv = (t < avail) & (got < k);
+      uint32_t v, lim;
+      if (Set) {
+        v = temper_top14(w[u]) >> sh0;  // getrandbits(bit_length(n)), n <= 120
+        lim = n;
+      } else {
+        int sh = pool ? (got == 0 ? sh0 : got == 1 ? sh1 : sh2) : sh0;
+        v = temper_top14(w[u]) >> sh;
+        lim = pool ? n - (uint32_t)got : n;
+      }
+      bool ok = lv & (v < lim) & (pool | ((v != j0) & (v != j1)));  // set method: distinct values
+      j0 = (ok & (got == 0)) ? v : j0;
+      j1 = (ok & (got == 1)) ? v : j1;
+      j2 = (ok & (got == 2)) ? v : j2;
+      used += lv ? 1 : 0;
+      got += ok ? 1 : 0;
+    }
+  }
+}
+
+__device__ __forceinline__ void sample3_raw(LdsMT& m, uint32_t n, int k, uint32_t j[3]) {
+  uint32_t j0 = 0xffffffffu, j1 = 0xffffffffu, j2 = 0;
+  int got = 0, used = 0;
+  bool far = __any(m.pos > kMT - 24);
   if (__all(n > 21)) {
-    int sh = __clz(n);
-#pragma unroll
-    for (int t = 0; t < 24; t++) {
-      if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
-      bool lv = t < avail && got < k;
-      uint32_t v = m.word(m.pos + t) >> sh;  // getrandbits(bit_length(n))
-      bool ok = lv && v < n && (got < 1 || v != j0) && (got < 2 || v != j1);
-      j0 = (ok && got == 0) ? v : j0;
-      j1 = (ok && got == 1) ? v : j1;
-      j2 = (ok && got == 2) ? v : j2;
-      used += lv ? 1 : 0;
-      got += ok ? 1 : 0;
-    }
+    if (far) scan24<true, true>(m, n, k, j0, j1, j2, got, used);
+    else scan24<false, true>(m, n, k, j0, j1, j2, got, used);
   } else {
-    bool pool = n <= 21;
-    int sh0 = __clz(n), sh1 = __clz(n > 1 ? n - 1 : 1), sh2 = __clz(n > 2 ? n - 2 : 1);
-#pragma unroll
-    for (int t = 0; t < 24; t++) {
-      if ((t == 8 || t == 12 || t == 16 || t == 20) && __all(got >= k)) break;
-      bool lv = t < avail && got < k;
-      int sh = pool ? (got == 0 ? sh0 : got == 1 ? sh1 : sh2) : sh0;
-      uint32_t lim = pool ? n - (uint32_t)got : n;
-      uint32_t v = m.word(m.pos + t) >> sh;
-      bool ok = lv && v < lim && (pool || ((got < 1 || v != j0) && (got < 2 || v != j1)));
-      j0 = (ok && got == 0) ? v : j0;
-      j1 = (ok && got == 1) ? v : j1;
-      j2 = (ok && got == 2) ? v : j2;
-      used += lv ? 1 : 0;
-      got += ok ? 1 : 0;
-    }
+    scan24<true, false>(m, n, k, j0, j1, j2, got, used);
   }
   m.pos += used;
   j[0] = j0; j[1] = j1; j[2] = j2;
@@ -715,8 +748,8 @@ __device__ __forceinline__ uint64_t replenish(State& s, Draw& draw) {
 }
 
 // HarmoniesGameState.__init__ (:66-79)
-template <class M>
-__device__ __forceinline__ void reset_state(State& s, StreamDraw<M>& d) {
+template <class Draw>
+__device__ __forceinline__ void reset_state(State& s, Draw& d) {
   s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
   s.piles = (1ull << 45) - 1;  // every tile slot = 7 (none), 0 piles
   uint64_t misc = 0x1FF;        // empty hand

@@ -28,10 +28,12 @@ struct hz_env {
   // seed-ahead (hz_play): a concurrent kernel on an auxiliary stream seeds
   // the streams of each board's next episode into a double-buffered slot
   // while k_rollout plays the current one (see launch_rollout)
-  int seed_ahead;            // enabled (default 1)
+  int seed_ahead;            // scripted draws prepared per board (0: off; default kAheadDraws)
   hipStream_t aux;
   uint32_t *ahead_mt[2];     // [n][624] seeded streams
   int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
+  uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
+  int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
   hipEvent_t ev_ro[2], ev_sa[2], ev_prime;
   int calls;                 // hz_play calls since the last prime
@@ -251,6 +253,72 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 // LDS latency instead of paying a scattered HBM round trip per draw.  The
 // streams are staged in (or seeded in place when reset_first) and written
 // back once.
+// ------------------------------------------------------------ chance-ahead
+// The piles a game draws do not depend on its moves: only a turn end draws
+// (one pile: a turn takes exactly one of the five), the bag changes only by
+// draws, and the stream only by draws.  So a board's whole chance sequence
+// for an episode is fixed by its seed.  k_seed_ahead (on the CUs k_rollout
+// leaves idle, one call ahead) seeds the stream and runs its first
+// kAheadDraws pile draws on the initial bag: it stores the piles (9 bits
+// each, 7 per u64), the stream cursor after each draw, and the stream.
+// k_rollout then plays such a board from the pile script; a game that needs
+// more draws continues on the stored stream (slot, global memory) from the
+// cursor after the last scripted draw.
+constexpr int kAheadDraws = 24;             // 5 opening + 19 turn ends (rule games: at most 23)
+constexpr int kAheadWords = (kAheadDraws + 6) / 7;  // 4 u64 of packed piles
+
+struct PlayDraw {
+  LdsMT m;                 // stream in LDS (boards not prepared ahead, auto-reset games)
+  bool scripted;           // replaying the prepared pile script
+  bool fell;               // script exhausted: drawing from the slot stream
+  int d;                   // script entries consumed
+  int nd;                  // script length (<= kAheadDraws)
+  uint64_t q0, q1, q2, q3; // the script
+  MT gm;                   // slot stream (valid once fell)
+  const int32_t *cur_tail; // cursor after the last scripted draw (global)
+
+  __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
+    if (scripted) {
+      if (d < nd) {
+        int w = d / 7;
+        uint64_t q = w == 0 ? q0 : w == 1 ? q1 : w == 2 ? q2 : q3;
+        int sh = 9 * (d - 7 * w);
+        d++;
+        return (uint32_t)(q >> sh) & 0x1FFu;
+      }
+      if (!fell) {
+        gm = MT(gm.w, *cur_tail);
+        fell = true;
+      }
+      uint32_t p9;
+      return draw_pile(misc, gm, p9) ? p9 : 0x1FFu;
+    }
+    m.prefetch();  // the one point where the wave's refills line up
+    uint32_t p9;
+    return draw_pile(misc, m, p9) ? p9 : 0x1FFu;
+  }
+};
+
+// copy the streams of boards in `mask` from `src` to `dst` (both board-major
+// spans of nb x 624 words), threads [t0, t0 + nt) of the block
+__device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int nb,
+                                             int t, int nt, uint64_t mask) {
+  int total4 = nb * (kMT / 4);
+  for (int q0 = 0; q0 < total4; q0 += nt * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int q = q0 + u * nt + t;
+      if (q < total4 && ((mask >> ((q * 4) / kMT)) & 1)) v[u] = reinterpret_cast<const uint4 *>(src)[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int q = q0 + u * nt + t;
+      if (q < total4 && ((mask >> ((q * 4) / kMT)) & 1)) reinterpret_cast<uint4 *>(dst)[q] = v[u];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                     int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                     int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
@@ -259,27 +327,40 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     uint64_t *__restrict__ traj_mask,
                                                     int16_t *__restrict__ traj_action, int32_t *__restrict__ games_done,
                                                     int32_t *__restrict__ steps_done,
-                                                    const uint32_t *__restrict__ ahead_mt,
+                                                    uint32_t *__restrict__ ahead_mt,
                                                     const int32_t *__restrict__ ahead_tag,
+                                                    const uint64_t *__restrict__ ahead_pile,
+                                                    const int32_t *__restrict__ ahead_cur, int ahead_draws,
                                                     int32_t *__restrict__ ep_final) {
+  __shared__ uint64_t s_lds_mask, s_recopy_mask;
   int tid = threadIdx.x;
   int lane = tid & 63;
-  bool w0 = tid < 64;
+  bool w0 = __builtin_amdgcn_readfirstlane(tid) < 64;  // wave-uniform: wave 0 plays
   int b0 = blockIdx.x * kBlock;
   int b = b0 + lane;
   bool act = b < n;
   uint64_t actmask = __ballot(act);  // the same in every wave
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
   uint32_t *g = mt + (size_t)b0 * kMT;
-  // reset_first: boards whose next-episode stream was seeded ahead stage it
-  // in; the others seed in place below
+  // reset_first: a board whose episode was prepared ahead plays its pile
+  // script; the others seed their stream in LDS below
   bool seeded = reset_first && act && ahead_tag && ahead_tag[b] == episode[b];
   uint64_t seededmask = __ballot(seeded);
   if (!reset_first) stage_mt(g, nb, tid, actmask, true);
-  else if (seededmask) stage_mt(const_cast<uint32_t *>(ahead_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
   __syncthreads();
-  if (w0 && act) {
-    StreamDraw<LdsMT> draw{LdsMT(lane, reset_first ? (seeded ? kMTAhead : kMTSeeded) : pos[b])};
+  if (!w0) {
+    // waves 1-3: the prepared streams become the boards' streams while wave 0 plays
+    if (seededmask) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid - 64, kStageThreads - 64, seededmask);
+  } else if (act) {
+    PlayDraw draw{LdsMT(lane, reset_first ? kMTSeeded : pos[b]), seeded, false, 0, ahead_draws, 0, 0, 0, 0,
+                  MT(ahead_mt ? ahead_mt + (size_t)b * kMT : nullptr, 0),
+                  ahead_cur ? ahead_cur + (size_t)ahead_draws * n + b : nullptr};
+    if (seeded) {
+      draw.q0 = ahead_pile[b];
+      draw.q1 = ahead_pile[(size_t)n + b];
+      draw.q2 = ahead_pile[(size_t)2 * n + b];
+      draw.q3 = ahead_pile[(size_t)3 * n + b];
+    }
     State s;
     int g_ply, games = 0, steps = 0;
     uint64_t sd, rkey;
@@ -301,6 +382,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     uint64_t t0 = __builtin_amdgcn_s_memtime();
     uint64_t acc8 = 0, acc9 = 0, acc10 = 0, acc11 = 0, acc12 = 0, acc13 = 0;
 #endif
+    bool lds_used = !seeded;  // the LDS copy of the stream is live
     for (int i = 0; i < max_plies; i++) {
       if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
         if (!auto_reset) {
@@ -316,6 +398,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         episode[b] = e + 1;
         mt_seed(hz_lds + lane, kLdsStride, sd);
         draw.m = LdsMT(lane, kMTSeeded);
+        draw.scripted = false;
+        lds_used = true;
         reset_state(s, draw);
         g_ply = 0;
       }
@@ -351,7 +435,9 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     if (score_pending(s.misc)) finish_game(s);
     HZ_ACC(13, t0);
     store_state(st, n, b, s);
-    pos[b] = draw.m.cursor();
+    if (lds_used) pos[b] = draw.m.cursor();
+    else if (draw.fell) pos[b] = draw.gm.cursor();
+    else pos[b] = ahead_cur[(size_t)draw.d * n + b];
     ply[b] = g_ply;
     seed[b] = sd;
 #ifdef HZ_DIAG
@@ -363,18 +449,31 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     if (games_done) games_done[b] = games;
     if (steps_done) steps_done[b] = steps;
     if (ep_final) ep_final[b] = episode[b];
+    uint64_t lm = __ballot(lds_used), rm = __ballot(!lds_used && draw.fell);
+    if (lane == 0) {
+      s_lds_mask = lm;
+      s_recopy_mask = rm;
+    }
+  }
+  if (w0 && !act && lane == 0 && actmask == 0) {
+    s_lds_mask = 0;
+    s_recopy_mask = 0;
   }
   __syncthreads();
-  stage_mt(g, nb, tid, actmask, false);
+  uint64_t lds_mask = s_lds_mask & actmask, recopy = s_recopy_mask & actmask;
+  if (lds_mask) stage_mt(g, nb, tid, lds_mask, false);
+  if (recopy) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid, kStageThreads, recopy);
 }
 
-// Seed-ahead: the streams of each board's predicted next episode (the
-// episode counter the last k_rollout left, plus one) seeded in LDS and
-// written out board-major with their tags; runs on the CUs k_rollout leaves
-// idle (one 64-board block per CU each).
+// Chance-ahead: each board's predicted next episode (the episode counter
+// the last k_rollout left, plus one) prepared on the CUs k_rollout leaves
+// idle: the stream seeded in LDS and pre-twisted, the first kAheadDraws
+// pile draws run on the initial bag (piles packed 7 per u64, cursor after
+// each draw), then the stream written out board-major with the tag.
 __global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
+                                                              uint64_t *__restrict__ pile, int32_t *__restrict__ cur,
                                                               const int32_t *__restrict__ ep_final, int n,
-                                                              uint64_t seed_base) {
+                                                              uint64_t seed_base, int draws) {
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b0 = blockIdx.x * kBlock;
@@ -385,8 +484,24 @@ __global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restri
   if (tid < 64 && act) {
     int e = ep_final[b] + 1;
     mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-    LdsMT m(lane, kMTSeeded);
-    m.twist_ahead(kAheadTwist);  // cursor kMTAhead
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
+    d.m.twist_ahead(kAheadTwist);
+    uint64_t bag = 0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+    uint64_t q[kAheadWords] = {};
+    cur[b] = d.m.cursor();
+#pragma unroll
+    for (int i = 0; i < kAheadDraws; i++) {
+      if (i < draws) {
+        uint32_t p9 = d(bag);
+        if (p9 != 0x1FFu) apply_pile(bag, p9);
+        q[i / 7] |= (uint64_t)p9 << (9 * (i % 7));
+        cur[(size_t)(i + 1) * n + b] = d.m.cursor();
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
     tag[b] = e;
   }
   __syncthreads();
@@ -513,6 +628,8 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   for (int k = 0; ok && k < 2; k++) {
     ok = hipMalloc(&e->ahead_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
+         hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
          hipEventCreateWithFlags(&e->ev_ro[k], hipEventDisableTiming) == hipSuccess &&
@@ -521,7 +638,7 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   ok = ok && hipEventCreateWithFlags(&e->ev_prime, hipEventDisableTiming) == hipSuccess &&
        hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) == hipSuccess &&
        hipDeviceSynchronize() == hipSuccess;
-  e->seed_ahead = 1;
+  e->seed_ahead = kAheadDraws;
   if (!ok) {
     hz_env_destroy(e);
     return nullptr;
@@ -538,6 +655,8 @@ void hz_env_destroy(hz_env *e) {
   for (int k = 0; k < 2; k++) {
     if (e->ahead_mt[k]) (void)hipFree(e->ahead_mt[k]);
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
+    if (e->ahead_pile[k]) (void)hipFree(e->ahead_pile[k]);
+    if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
     if (e->ev_ro[k]) (void)hipEventDestroy(e->ev_ro[k]);
     if (e->ev_sa[k]) (void)hipEventDestroy(e->ev_sa[k]);
@@ -566,9 +685,9 @@ int32_t *hz_env_mt_pos_ptr(hz_env *e) { return e ? e->pos : nullptr; }
 int32_t *hz_env_ply_ptr(hz_env *e) { return e ? e->ply : nullptr; }
 uint64_t *hz_env_seed_ptr(hz_env *e) { return e ? e->seed : nullptr; }
 
-int hz_env_set_seed_ahead(hz_env *e, int32_t enable) {
-  if (!e) return -1;
-  e->seed_ahead = enable ? 1 : 0;
+int hz_env_set_seed_ahead(hz_env *e, int32_t draws) {
+  if (!e || draws < 0) return -1;
+  e->seed_ahead = draws > kAheadDraws ? kAheadDraws : draws;
   e->primed = 0;
   return 0;
 }
@@ -634,8 +753,10 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
-  const uint32_t *ahead_mt = nullptr;
+  uint32_t *ahead_mt = nullptr;
   const int32_t *ahead_tag = nullptr;
+  const uint64_t *ahead_pile = nullptr;
+  const int32_t *ahead_cur = nullptr;
   int32_t *ep_final = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(e->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
@@ -654,13 +775,16 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
       return 1;
     }
     hipLaunchKernelGGL(k_seed_ahead, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->aux, e->ahead_mt[w],
-                       e->ahead_tag[w], e->ep_final[w], e->n, e->seed_base);
+                       e->ahead_tag[w], e->ahead_pile[w], e->ahead_cur[w], e->ep_final[w], e->n, e->seed_base,
+                       e->seed_ahead);
     int err = launch_err();
     if (err || hipEventRecord(e->ev_sa[w], e->aux)) return err ? err : 1;
     if (wait_r && hipStreamWaitEvent(e->stream, e->ev_sa[r], 0)) return 1;
     if (use_r) {
       ahead_mt = e->ahead_mt[r];
       ahead_tag = e->ahead_tag[r];
+      ahead_pile = e->ahead_pile[r];
+      ahead_cur = e->ahead_cur[r];
     }
     ep_final = e->ep_final[r];
   } else {
@@ -668,7 +792,8 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   }
   hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
-                     traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ep_final);
+                     traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
+                     e->seed_ahead, ep_final);
   int err = launch_err();
   if (err) return err;
   if (pipe) {

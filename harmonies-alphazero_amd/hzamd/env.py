@@ -51,9 +51,10 @@ class BatchedEnv:
     def handle(self):
         return self._h
 
-    def set_seed_ahead(self, enable):
-        """hz_play's concurrent next-episode seeding on/off (results identical)."""
-        nat.check(nat.lib().hz_env_set_seed_ahead(self._h, 1 if enable else 0), "hz_env_set_seed_ahead")
+    def set_seed_ahead(self, enable, draws=24):
+        """hz_play's concurrent next-episode preparation (seeding + the first
+        `draws` pile draws) on/off; results are identical either way."""
+        nat.check(nat.lib().hz_env_set_seed_ahead(self._h, int(draws) if enable else 0), "hz_env_set_seed_ahead")
 
     # -- env surface ---------------------------------------------------------
     def reset(self, sel=None, seeds=None):

@@ -124,16 +124,19 @@ int hz_rollout(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *tra
                int32_t *steps_done);
 /* hz_reset (all boards) fused with hz_rollout in one launch: the chance
  * streams are seeded and consumed in LDS and written to HBM once.  With
- * seed-ahead on (the default), each call also seeds, on an internal stream
- * and concurrently with its own play, the streams of every board's next
- * episode; the next call stages those instead of seeding (identical
- * results; a board whose episode counter was moved by anything else seeds
- * in place).  Not used while the env stream is being graph-captured. */
+ * chance-ahead on (the default), each call also prepares, on an internal
+ * stream and concurrently with its own play, every board's next episode:
+ * its stream seeded and its first piles drawn (a game's draws do not depend
+ * on its moves); the next call replays those piles instead of seeding and
+ * drawing (identical results; a board whose episode counter was moved by
+ * anything else seeds in place, a game needing more piles continues on the
+ * prepared stream).  Not used while the env stream is being graph-captured. */
 int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state,
             uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done,
             int32_t *steps_done);
-/* seed-ahead for hz_play on (1, default) or off (0). */
-int hz_env_set_seed_ahead(hz_env *env, int32_t enable);
+/* chance-ahead for hz_play: draws = piles prepared per board (0 = off,
+ * capped at 24 = the default). */
+int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
 /* export: state[6][n] and, optionally, the MT streams in CPython getstate()

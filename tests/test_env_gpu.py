@@ -165,14 +165,16 @@ def _check_episode(env, base, ep, steps, nthreads=8):
         assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b], (ep, b)
 
 
-@pytest.mark.parametrize("ahead", [True, False])
-def test_play_seed_ahead_pipeline(Env, ahead):
-    """Consecutive hz_play calls (episodes 0, 1, 2 from seeded-ahead slots),
+@pytest.mark.parametrize("ahead,draws", [(True, 24), (True, 3), (True, 19), (False, 0)])
+def test_play_seed_ahead_pipeline(Env, ahead, draws):
+    """Consecutive hz_play calls (episodes 0, 1, 2 from prepared slots),
     an hz_reset + hz_rollout in between (episode 3, re-primes the pipeline),
-    then episodes 4 and 5: every game bit-exact vs the oracle's episode."""
+    then episodes 4 and 5: every game bit-exact vs the oracle's episode.
+    draws < 19 makes every game (19-23 draws) run past its pile script onto
+    the prepared stream; 19 covers the boundary."""
     n, base = 4096, 2024
     env = Env(n, seed_base=base, device=DEV)
-    env.set_seed_ahead(ahead)
+    env.set_seed_ahead(ahead, draws)
     for ep in range(3):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)

@@ -92,32 +92,59 @@ int micro_run(int which, void *a, void *b, int n, int reps, void *sink, void *st
 }
 }
 
-// draws with the stream in LDS (as in k_rollout)
-__global__ void __launch_bounds__(64) k_draws_lds(uint32_t *mt, int n, int reps, uint32_t *sink, uint64_t *cyc) {
+// draws with the stream in LDS (as in k_rollout).  mode 0: fresh seeding
+// (twists on demand), bag 120 -> 40; modes 1-4: stream pre-twisted like a
+// seeded-ahead one and the bag kept in a game's range (105 -> 57):
+// 1 full draw (prefetch + draw_pile + apply_pile), 2 sample3_raw only,
+// 3 draw_pile only (no prefetch), 4 prefetch only.
+__global__ void __launch_bounds__(64) k_draws_lds(uint32_t *mt, int n, int reps, uint32_t *sink, uint64_t *cyc,
+                                                  int mode) {
   uint32_t *lds = hz_lds;
   int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
   mt_seed(lds + lane, 65, 99 + b);
   StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
-  uint64_t misc = 0;
-  for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  if (mode > 0) d.m.twist_ahead(kAheadTwist);
+  int lo = mode ? 57 : 40;
+  uint64_t misc0 = 0;
+  for (int t = 0; t < 6; t++) misc0 = set_bits(misc0, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  if (mode) {  // 15 tiles out, as after the opening piles
+    misc0 = set_bits(misc0, 11, 5, 20);
+    misc0 = set_bits(misc0, 16, 5, 16);
+    misc0 = set_bits(misc0, 21, 5, 18);
+    misc0 = set_bits(misc0, 26, 5, 20);
+    misc0 = set_bits(misc0, 31, 5, 13);
+    misc0 = set_bits(misc0, 36, 5, 18);
+  }
+  uint64_t misc = misc0;
   uint32_t acc = 0;
   uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < reps; r++) {
-    uint32_t p9 = d(misc);
-    apply_pile(misc, p9);
-    acc += p9;
-    if (bag_total(misc) < 40) {
-      for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+    uint32_t p9 = 0;
+    if (mode <= 1) {
+      p9 = d(misc);
+    } else if (mode == 2) {
+      uint32_t j[3];
+      sample3_raw(d.m, (uint32_t)bag_total(misc), 3, j);
+      p9 = j[0] ^ (j[1] << 3) ^ (j[2] << 6);
+    } else if (mode == 3) {
+      draw_pile(misc, d.m, p9);
+    } else {
+      d.m.prefetch();
+      d.m.pos += 5;
+      p9 = d.m.tw;
     }
+    if (mode <= 3) apply_pile(misc, p9 & 0x1FF);
+    acc += p9;
+    if (bag_total(misc) < lo) misc = misc0;
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime();
   sink[b] = acc;
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-extern "C" int micro_draws_lds(void *mt, int n, int reps, void *sink, void *cyc, void *stream) {
+extern "C" int micro_draws_lds(void *mt, int n, int reps, void *sink, void *cyc, void *stream, int mode) {
   hipFuncSetAttribute((const void *)k_draws_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 624 * 65 * 4);
   hipLaunchKernelGGL(k_draws_lds, dim3((n + 63) / 64), dim3(64), 624 * 65 * 4, (hipStream_t)stream, (uint32_t *)mt, n,
-                     reps, (uint32_t *)sink, (uint64_t *)cyc);
+                     reps, (uint32_t *)sink, (uint64_t *)cyc, mode);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -34,10 +34,13 @@ for reps in (16, 64):
     res[f"pick_x{reps}_us"] = timeit(5, P(seeds), None, reps)
 print(json.dumps(res))
 
-L.micro_draws_lds.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+L.micro_draws_lds.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int]
 cyc = torch.zeros(n // 64, dtype=torch.int64, device=dev)
-for reps in (1, 17, 65):
-    L.micro_draws_lds(P(mt), n, reps, P(sink), P(cyc), stream)
-    torch.cuda.synchronize()
-    res[f"draws_lds_x{reps}_cyc"] = float(cyc.double().mean())
+names = {0: "draw_fresh", 1: "draw_pretwisted", 2: "scan_only", 3: "draw_pile_only", 4: "prefetch_only"}
+for mode, name in names.items():
+    for reps in (1, 33):  # 33 draws stay inside the 224 pre-twisted words
+        L.micro_draws_lds(P(mt), n, reps, P(sink), P(cyc), stream, mode)
+        torch.cuda.synchronize()
+        res[f"lds_{name}_x{reps}_cyc"] = float(cyc.double().mean())
+    res[f"lds_{name}_per_draw_cyc"] = (res[f"lds_{name}_x33_cyc"] - res[f"lds_{name}_x1_cyc"]) / 32
 print(json.dumps(res))
