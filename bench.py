@@ -232,6 +232,32 @@ def main():
         except Exception:
             traffic = None
 
+    # the same workload with chance-ahead off (every launch seeds and draws
+    # in-kernel), for comparison; not the headline number
+    env.set_seed_ahead(False)
+    for _ in range(2):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    steps_o = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(None, games, steps_o[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    off_elapsed = time.perf_counter() - t1
+    off_steps = int(steps_o.sum(dtype=torch.int64))
+    if world > 1:
+        t = torch.tensor([off_elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        off_elapsed = t.item()
+        c = torch.tensor([off_steps], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        off_steps = int(c[0])
+    env.set_seed_ahead(True)
+
     api = None
     if args.api_mode and rank == 0:
         api = api_mode(env, dev, stream)
@@ -263,6 +289,11 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rollout", "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes},
+            "chance_ahead": {"on": True, "note": "each hz_play also prepares every board's next episode "
+                                                 "(seeding + its pile draws, which do not depend on moves) on "
+                                                 "idle CUs; steady state: one preparation per game in the timed "
+                                                 "region", "value_off": off_steps / off_elapsed,
+                             "ms_per_step_off": off_elapsed * 1000.0 / args.steps},
             "cpu_baseline": cpu,
             "parity": f"first batch: {first_steps} env steps == C oracle ({ref_total})",
         }
