@@ -25,19 +25,17 @@ struct hz_env {
   int32_t *ply;      // [n]
   int32_t *episode;  // [n]
   uint64_t *seed;    // [n]
-  // seed-ahead (hz_play): a concurrent kernel on an auxiliary stream seeds
-  // the streams of each board's next episode into a double-buffered slot
-  // while k_rollout plays the current one (see launch_rollout)
+  // chance-ahead (hz_play): extra blocks of the same launch prepare each
+  // board's next episode into a double-buffered slot while the playing
+  // blocks play the current one (see launch_rollout)
   int seed_ahead;            // scripted draws prepared per board (0: off; default kAheadDraws)
-  hipStream_t aux;
   uint32_t *ahead_mt[2];     // [n][624] seeded streams
   int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
-  hipEvent_t ev_ro[2], ev_sa[2], ev_prime;
   int calls;                 // hz_play calls since the last prime
-  int primed, sa_valid[2];
+  int primed, slot_valid[2];
 };
 
 #ifdef HZ_DIAG
@@ -72,7 +70,7 @@ constexpr int kBlock = 64;  // one wave per workgroup: 4096 boards -> 64 waves
 
 inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 
-// The 64-board LDS kernels (k_reset, k_rollout, k_seed_ahead) run 256
+// The 64-board LDS kernels (k_reset, k_rollout) run 256
 // threads per block: wave 0 plays (lane = board), waves 1-3 only help move
 // the block's streams between HBM and LDS (one 162 KB block per CU, so the
 // extra waves cost no occupancy) and wait at the barriers meanwhile.
@@ -257,13 +255,14 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 // The piles a game draws do not depend on its moves: only a turn end draws
 // (one pile: a turn takes exactly one of the five), the bag changes only by
 // draws, and the stream only by draws.  So a board's whole chance sequence
-// for an episode is fixed by its seed.  k_seed_ahead (on the CUs k_rollout
-// leaves idle, one call ahead) seeds the stream and runs its first
-// kAheadDraws pile draws on the initial bag: it stores the piles (9 bits
-// each, 7 per u64), the stream cursor after each draw, and the stream.
-// k_rollout then plays such a board from the pile script; a game that needs
-// more draws continues on the stored stream (slot, global memory) from the
-// cursor after the last scripted draw.
+// for an episode is fixed by its seed.  The preparing blocks of one hz_play
+// launch (on CUs the playing blocks leave idle) seed the stream of each
+// board's next episode and run its first kAheadDraws pile draws on the
+// initial bag: they store the piles (9 bits each, 7 per u64), the stream
+// cursor after each draw, and the stream.  The next launch plays such a
+// board from the pile script; a game that needs more draws continues on the
+// stored stream (slot, global memory) from the cursor after the last
+// scripted draw.
 constexpr int kAheadDraws = 24;             // 5 opening + 19 turn ends (rule games: at most 23)
 constexpr int kAheadWords = (kAheadDraws + 6) / 7;  // 4 u64 of packed piles
 
@@ -319,6 +318,50 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
   }
 }
 
+// Chance-ahead preparation (blocks nblk.. of a k_rollout launch, on CUs the
+// playing blocks leave idle): each board's predicted next episode (the
+// episode counter the previous launch left, plus one): the stream seeded in
+// LDS and pre-twisted, the first `draws` pile draws run on the initial bag
+// (piles packed 7 per u64, cursor after each draw), then the stream written
+// out board-major with the tag.
+__device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
+                                              uint64_t *__restrict__ pile, int32_t *__restrict__ cur,
+                                              const int32_t *__restrict__ ep_final, int n, uint64_t seed_base,
+                                              int draws) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  int b0 = blk * kBlock;
+  int b = b0 + lane;
+  bool act = b < n;
+  uint64_t actmask = __ballot(act);
+  int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  if (tid < 64 && act) {
+    int e = ep_final[b] + 1;
+    mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
+    d.m.twist_ahead(kAheadTwist);
+    uint64_t bag = 0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+    uint64_t q[kAheadWords] = {};
+    cur[b] = d.m.cursor();
+#pragma unroll
+    for (int i = 0; i < kAheadDraws; i++) {
+      if (i < draws) {
+        uint32_t p9 = d(bag);
+        if (p9 != 0x1FFu) apply_pile(bag, p9);
+        q[i / 7] |= (uint64_t)p9 << (9 * (i % 7));
+        cur[(size_t)(i + 1) * n + b] = d.m.cursor();
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
+    tag[b] = e;
+  }
+  __syncthreads();
+  stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
+}
+
 __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                     int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                     int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
@@ -331,7 +374,15 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     const int32_t *__restrict__ ahead_tag,
                                                     const uint64_t *__restrict__ ahead_pile,
                                                     const int32_t *__restrict__ ahead_cur, int ahead_draws,
-                                                    int32_t *__restrict__ ep_final) {
+                                                    int32_t *__restrict__ ep_final, int nblk,
+                                                    uint32_t *__restrict__ prep_mt, int32_t *__restrict__ prep_tag,
+                                                    uint64_t *__restrict__ prep_pile, int32_t *__restrict__ prep_cur,
+                                                    const int32_t *__restrict__ prep_ep) {
+  if ((int)blockIdx.x >= nblk) {  // chance-ahead role (uniform per block)
+    prepare_block((int)blockIdx.x - nblk, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base,
+                  ahead_draws);
+    return;
+  }
   __shared__ uint64_t s_lds_mask, s_recopy_mask;
   int tid = threadIdx.x;
   int lane = tid & 63;
@@ -465,49 +516,6 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   if (recopy) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid, kStageThreads, recopy);
 }
 
-// Chance-ahead: each board's predicted next episode (the episode counter
-// the last k_rollout left, plus one) prepared on the CUs k_rollout leaves
-// idle: the stream seeded in LDS and pre-twisted, the first kAheadDraws
-// pile draws run on the initial bag (piles packed 7 per u64, cursor after
-// each draw), then the stream written out board-major with the tag.
-__global__ void __launch_bounds__(kStageThreads) k_seed_ahead(uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
-                                                              uint64_t *__restrict__ pile, int32_t *__restrict__ cur,
-                                                              const int32_t *__restrict__ ep_final, int n,
-                                                              uint64_t seed_base, int draws) {
-  int tid = threadIdx.x;
-  int lane = tid & 63;
-  int b0 = blockIdx.x * kBlock;
-  int b = b0 + lane;
-  bool act = b < n;
-  uint64_t actmask = __ballot(act);
-  int nb = n - b0 < kBlock ? n - b0 : kBlock;
-  if (tid < 64 && act) {
-    int e = ep_final[b] + 1;
-    mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
-    d.m.twist_ahead(kAheadTwist);
-    uint64_t bag = 0;
-#pragma unroll
-    for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
-    uint64_t q[kAheadWords] = {};
-    cur[b] = d.m.cursor();
-#pragma unroll
-    for (int i = 0; i < kAheadDraws; i++) {
-      if (i < draws) {
-        uint32_t p9 = d(bag);
-        if (p9 != 0x1FFu) apply_pile(bag, p9);
-        q[i / 7] |= (uint64_t)p9 << (9 * (i % 7));
-        cur[(size_t)(i + 1) * n + b] = d.m.cursor();
-      }
-    }
-#pragma unroll
-    for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
-    tag[b] = e;
-  }
-  __syncthreads();
-  stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
-}
-
 // ---------------------------------------------------------- greedy agent
 // evaluation.py:137-196 choose_move_greedy, one wave per board: lane l scores
 // legal moves l, l+64 (canonical ascending order) by applying the placement
@@ -607,8 +615,7 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
           hipSuccess ||
       hipFuncSetAttribute((const void *)k_rollout, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
           hipSuccess ||
-      hipFuncSetAttribute((const void *)k_seed_ahead, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
-          hipSuccess) {
+      false) {
     free(e);
     return nullptr;
   }
@@ -631,13 +638,9 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
          hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
-         hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
-         hipEventCreateWithFlags(&e->ev_ro[k], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&e->ev_sa[k], hipEventDisableTiming) == hipSuccess;
+         hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
-  ok = ok && hipEventCreateWithFlags(&e->ev_prime, hipEventDisableTiming) == hipSuccess &&
-       hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) == hipSuccess &&
-       hipDeviceSynchronize() == hipSuccess;
+  ok = ok && hipDeviceSynchronize() == hipSuccess;
   e->seed_ahead = kAheadDraws;
   if (!ok) {
     hz_env_destroy(e);
@@ -648,20 +651,13 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
 
 void hz_env_destroy(hz_env *e) {
   if (!e) return;
-  if (e->aux) {
-    (void)hipStreamSynchronize(e->aux);
-    (void)hipStreamDestroy(e->aux);
-  }
   for (int k = 0; k < 2; k++) {
     if (e->ahead_mt[k]) (void)hipFree(e->ahead_mt[k]);
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
     if (e->ahead_pile[k]) (void)hipFree(e->ahead_pile[k]);
     if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
-    if (e->ev_ro[k]) (void)hipEventDestroy(e->ev_ro[k]);
-    if (e->ev_sa[k]) (void)hipEventDestroy(e->ev_sa[k]);
   }
-  if (e->ev_prime) (void)hipEventDestroy(e->ev_prime);
   if (e->state) (void)hipFree(e->state);
   if (e->mt) (void)hipFree(e->mt);
   if (e->pos) (void)hipFree(e->pos);
@@ -734,22 +730,23 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
   return launch_err();
 }
 
-// hz_play's seed-ahead pipeline.  Call i plays from slot r = i & 1 and,
-// concurrently on the auxiliary stream, seeds slot w = r ^ 1 for call i + 1:
-//   aux : wait ev_ro[w] (call i-1's k_rollout: done reading slot w, wrote
-//         ep_final[w]) -> k_seed_ahead(w) -> record ev_sa[w]
-//   main: wait ev_sa[r] (call i-1's k_seed_ahead) -> k_rollout(r) -> record ev_ro[r]
-// The prediction (the episode call i+1 resets to = the counter call i-1 left,
-// plus one) only decides which boards skip seeding: a board stages a
-// seeded-ahead stream only when the slot's tag equals its episode counter,
-// so the results never depend on it.  Anything else that moves episode
-// counters (hz_reset, hz_rollout) re-primes with a copy of the counters.
 int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
   if (!e || !action) return -1;
   hipLaunchKernelGGL(k_greedy, dim3(e->n), dim3(64), 0, e->stream, e->state, e->mt, e->pos, e->n, sel, action);
   return launch_err();
 }
 
+// hz_play's chance-ahead pipeline: one launch per call, blocks [0, nblk)
+// play from slot r = calls & 1, blocks [nblk, 2 nblk) prepare slot w = r ^ 1
+// for the next call.  Launch order on the stream is the only synchronisation:
+// a slot is written by call i's preparing blocks and read by call i+1's
+// playing blocks; the preparing blocks read ep_final[w], written by call
+// i-1's playing blocks (the episode counter each board ended with).  The
+// prediction (call i+1 resets to that counter plus one) only decides which
+// boards skip seeding and drawing: a board replays a slot only when the
+// slot's tag equals its episode counter, so results never depend on it.
+// Anything else that moves episode counters (hz_reset, hz_rollout) makes
+// the next call re-prime ep_final from the counters.
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
@@ -758,47 +755,37 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   const uint64_t *ahead_pile = nullptr;
   const int32_t *ahead_cur = nullptr;
   int32_t *ep_final = nullptr;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(e->stream, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
-  bool pipe = reset_first && e->seed_ahead && cap == hipStreamCaptureStatusNone;
+  int nblk = grid_for(e->n), grid = nblk;
+  bool pipe = reset_first && e->seed_ahead > 0;
   int r = e->calls & 1, w = r ^ 1;
   if (pipe) {
     size_t n = (size_t)e->n;
-    bool wait_r = e->sa_valid[r];  // call i-1's k_seed_ahead wrote slot r and read ep_final[r]
-    bool use_r = wait_r && e->primed;
     if (!e->primed) {
-      if (hipMemcpyAsync(e->ep_final[w], e->episode, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream) ||
-          hipEventRecord(e->ev_prime, e->stream) || hipStreamWaitEvent(e->aux, e->ev_prime, 0))
+      if (hipMemcpyAsync(e->ep_final[w], e->episode, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream))
         return 1;
+      e->slot_valid[r] = 0;
       e->primed = 1;
-    } else if (hipStreamWaitEvent(e->aux, e->ev_ro[w], 0)) {
-      return 1;
     }
-    hipLaunchKernelGGL(k_seed_ahead, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->aux, e->ahead_mt[w],
-                       e->ahead_tag[w], e->ahead_pile[w], e->ahead_cur[w], e->ep_final[w], e->n, e->seed_base,
-                       e->seed_ahead);
-    int err = launch_err();
-    if (err || hipEventRecord(e->ev_sa[w], e->aux)) return err ? err : 1;
-    if (wait_r && hipStreamWaitEvent(e->stream, e->ev_sa[r], 0)) return 1;
-    if (use_r) {
+    if (e->slot_valid[r]) {
       ahead_mt = e->ahead_mt[r];
       ahead_tag = e->ahead_tag[r];
       ahead_pile = e->ahead_pile[r];
       ahead_cur = e->ahead_cur[r];
     }
     ep_final = e->ep_final[r];
+    grid = 2 * nblk;
   } else {
     e->primed = 0;
   }
-  hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
+  hipLaunchKernelGGL(k_rollout, dim3(grid), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
-                     e->seed_ahead, ep_final);
+                     e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
+                     e->ahead_cur[w], e->ep_final[w]);
   int err = launch_err();
   if (err) return err;
   if (pipe) {
-    if (hipEventRecord(e->ev_ro[r], e->stream)) return 1;
-    e->sa_valid[w] = 1;
+    e->slot_valid[w] = 1;
     e->calls++;
   }
   return 0;
