@@ -258,13 +258,13 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 // for an episode is fixed by its seed.  The preparing blocks of one hz_play
 // launch (on CUs the playing blocks leave idle) seed the stream of each
 // board's next episode and run its first kAheadDraws pile draws on the
-// initial bag: they store the piles (9 bits each, 7 per u64), the stream
+// initial bag: they store the piles (9 bits each, packed), the stream
 // cursor after each draw, and the stream.  The next launch plays such a
 // board from the pile script; a game that needs more draws continues on the
 // stored stream (slot, global memory) from the cursor after the last
 // scripted draw.
 constexpr int kAheadDraws = 24;             // 5 opening + 19 turn ends (rule games: at most 23)
-constexpr int kAheadWords = (kAheadDraws + 6) / 7;  // 4 u64 of packed piles
+constexpr int kAheadWords = (9 * kAheadDraws + 63) / 64;  // 4 u64: the piles, 9 bits each
 
 struct PlayDraw {
   LdsMT m;                 // stream in LDS (boards not prepared ahead, auto-reset games)
@@ -272,18 +272,22 @@ struct PlayDraw {
   bool fell;               // script exhausted: drawing from the slot stream
   int d;                   // script entries consumed
   int nd;                  // script length (<= kAheadDraws)
-  uint64_t q0, q1, q2, q3; // the script
+  uint64_t q0, q1, q2, q3; // the rest of the script, next entry in the low 9 bits
   MT gm;                   // slot stream (valid once fell)
   const int32_t *cur_tail; // cursor after the last scripted draw (global)
 
   __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
     if (scripted) {
       if (d < nd) {
-        int w = d / 7;
-        uint64_t q = w == 0 ? q0 : w == 1 ? q1 : w == 2 ? q2 : q3;
-        int sh = 9 * (d - 7 * w);
+        // pop the next 9-bit entry: a shift queue (a select over the four
+        // words would become a dynamic index into a scratch copy)
+        uint32_t p9 = (uint32_t)q0 & 0x1FFu;
+        q0 = (q0 >> 9) | (q1 << 55);
+        q1 = (q1 >> 9) | (q2 << 55);
+        q2 = (q2 >> 9) | (q3 << 55);
+        q3 >>= 9;
         d++;
-        return (uint32_t)(q >> sh) & 0x1FFu;
+        return p9;
       }
       if (!fell) {
         gm = MT(gm.w, *cur_tail);
@@ -306,9 +310,9 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
   for (int q0 = 0; q0 < total4; q0 += nt * 4) {
     uint4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < 4; u++) {  // unconditional (clamped) loads: the values stay in registers
       int q = q0 + u * nt + t;
-      if (q < total4 && ((mask >> ((q * 4) / kMT)) & 1)) v[u] = reinterpret_cast<const uint4 *>(src)[q];
+      v[u] = reinterpret_cast<const uint4 *>(src)[q < total4 ? q : total4 - 1];
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -322,7 +326,7 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 // playing blocks leave idle): each board's predicted next episode (the
 // episode counter the previous launch left, plus one): the stream seeded in
 // LDS and pre-twisted, the first `draws` pile draws run on the initial bag
-// (piles packed 7 per u64, cursor after each draw), then the stream written
+// (piles packed 9 bits each, cursor after each draw), then the stream written
 // out board-major with the tag.
 __device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
                                               uint64_t *__restrict__ pile, int32_t *__restrict__ cur,
@@ -350,7 +354,10 @@ __device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ ou
       if (i < draws) {
         uint32_t p9 = d(bag);
         if (p9 != 0x1FFu) apply_pile(bag, p9);
-        q[i / 7] |= (uint64_t)p9 << (9 * (i % 7));
+        // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
+        int bit = 9 * i, wd = bit / 64, off = bit % 64;
+        q[wd] |= (uint64_t)p9 << off;
+        if (off > 55) q[wd + 1] |= (uint64_t)p9 >> (64 - off);
         cur[(size_t)(i + 1) * n + b] = d.m.cursor();
       }
     }
