@@ -369,6 +369,10 @@ __device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ ou
   stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
 }
 
+// AutoReset / Record are template parameters so that the common variant
+// (play to the end, no trajectory) has a plain loop: no reset path, no
+// record stores, fewer live scalar values across the ply loop.
+template <bool AutoReset, bool Record>
 __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                     int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                     int32_t *__restrict__ episode, uint64_t *__restrict__ seed,
@@ -443,8 +447,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     bool lds_used = !seeded;  // the LDS copy of the stream is live
     for (int i = 0; i < max_plies; i++) {
       if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
-        if (!auto_reset) {
-          if (traj_action) {
+        if constexpr (!AutoReset) {
+          if (Record && traj_action) {
             for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
           }
           break;
@@ -465,21 +469,21 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       HZ_ACC(8, t0);
       int L = legal_mask(s, mk);
       HZ_ACC(9, t0);
-      if (traj_state) {
+      if (Record && traj_state) {
         uint64_t *o = traj_state + (size_t)i * 6 * n + b;
         o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
         o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
       }
-      if (traj_mask) {
+      if (Record && traj_mask) {
         uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
         o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
       }
       if (L == 0) {  // stuck board (unreachable from HarmoniesGameState())
-        if (traj_action) traj_action[(size_t)i * n + b] = -1;
+        if (Record && traj_action) traj_action[(size_t)i * n + b] = -1;
         break;
       }
       int a = kth_action(mk, rule_pick_k(rkey, g_ply, L));
-      if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
+      if (Record && traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
       HZ_ACC(10, t0);
       bool te = phase_of(s.misc) == PH_P3;
       step_state<true>(s, a, draw);
@@ -620,8 +624,14 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   // k_reset / k_rollout stage 64 boards' MT words in 158 KiB of LDS
   if (hipFuncSetAttribute((const void *)k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
           hipSuccess ||
-      hipFuncSetAttribute((const void *)k_rollout, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
-          hipSuccess ||
+      hipFuncSetAttribute((const void *)k_rollout<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)kResetLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)k_rollout<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)kResetLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)k_rollout<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)kResetLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)k_rollout<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)kResetLds) != hipSuccess ||
       false) {
     free(e);
     return nullptr;
@@ -784,8 +794,11 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   } else {
     e->primed = 0;
   }
-  hipLaunchKernelGGL(k_rollout, dim3(grid), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
-                     e->ply, e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
+  bool rec = traj_state || traj_mask || traj_action;
+  auto kern = auto_reset ? (rec ? k_rollout<true, true> : k_rollout<true, false>)
+                         : (rec ? k_rollout<false, true> : k_rollout<false, false>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos, e->ply,
+                     e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
                      e->ahead_cur[w], e->ep_final[w]);
