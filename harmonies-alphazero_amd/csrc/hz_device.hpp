@@ -933,6 +933,46 @@ __device__ __forceinline__ int step_state(State& s, int a, Draw& draw) {
   return ST_BAD_PHASE;
 }
 
+// apply_move for an action taken from the legal mask (the fused rollout):
+// the same transitions as step_state without its validation, written
+// branch-free so that every lane of a wave runs the same instructions.
+template <bool Defer, class Draw>
+__device__ __forceinline__ void step_trusted(State& s, int a, Draw& draw) {
+  int ph = phase_of(s.misc);
+  if (ph == PH_CHOOSE) {
+    int np = npiles_of(s.piles);
+    uint32_t pile9 = (uint32_t)(s.piles >> (9 * a)) & 0x1FF;
+    int len = ((pile9 & 7) != 7) + (((pile9 >> 3) & 7) != 7) + (((pile9 >> 6) & 7) != 7);
+    uint64_t lower = s.piles & ((1ull << (9 * a)) - 1);
+    uint64_t upper = (s.piles & ((1ull << 45) - 1)) >> (9 * (a + 1));
+    uint64_t np_piles = lower | (upper << (9 * a)) | (0x1FFull << 36);
+    s.piles = set_bits(np_piles, 45, 3, (uint64_t)(np - 1));
+    uint64_t m = set_bits(s.misc, 0, 9, pile9);
+    m = set_bits(m, 9, 2, (uint64_t)len);
+    s.misc = set_bits(m, 42, 3, PH_P1);
+    return;
+  }
+  int t = (a - 5) / 23, c = (a - 5) - 23 * t;
+  int nh = hand_n(s.misc);
+  uint32_t h9 = (uint32_t)(s.misc & 0x1FF);
+  // hand.remove(tile): the first entry equal to t
+  int j = (int)(h9 & 7) == t ? 0 : (int)((h9 >> 3) & 7) == t ? 1 : 2;
+  int p = player_of(s.misc);
+  int code = code_at(s, p, c);
+  // place_code for a legal placement: empty -> 1 + t; plant on wood 7;
+  // stone on stone 8 / on stone-stone 9; building on wood/stone/building 10/11/12
+  int nc = t == PLANT ? 7 : t == STONE ? (code == 4 ? 8 : 9) : code + 7;
+  nc = code == 0 ? 1 + t : nc;
+  uint32_t low = h9 & ((1u << (3 * j)) - 1);
+  uint32_t high = h9 >> (3 * (j + 1));
+  uint32_t nh9 = (low | (high << (3 * j)) | (7u << 6)) & 0x1FF;
+  uint64_t m = set_bits(s.misc, 0, 9, nh9);
+  s.misc = set_bits(m, 9, 2, (uint64_t)(nh - 1));
+  set_code(s, p, c, nc);
+  if (ph < PH_P3) s.misc = set_bits(s.misc, 42, 3, (uint64_t)(ph + 1));
+  else end_turn<Defer>(s, draw);
+}
+
 // ------------------------------------------------------- transposition key
 // MCTS.py keys its DAG by hash(state) (MCTS.py:14,177,185) of
 // get_canonical_tuple() (harmonies_engine.py:81-110).  Because CPython hashes

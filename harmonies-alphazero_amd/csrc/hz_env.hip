@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       if (Record && traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
       HZ_ACC(10, t0);
       bool te = phase_of(s.misc) == PH_P3;
-      step_state<true>(s, a, draw);
+      step_trusted<true>(s, a, draw);
       if (te) HZ_ACC(12, t0);
       else HZ_ACC(11, t0);
       g_ply++;
