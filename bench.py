@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--seed-base", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-off-compare", action="store_true",
+                    help="skip the chance-ahead-off comparison run (profiling)")
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
@@ -200,11 +202,17 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        one_step(evs[i], games_t[i], steps_t[i])
+        one_step(None, games_t[i], steps_t[i])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the dominant kernel's average launch duration, from HIP events around
+    # each launch on its stream, in a separate loop of the same launches (the
+    # event markers would otherwise sit between the timed launches)
+    for i in range(args.steps):
+        one_step(evs[i], games, steps)
+    torch.cuda.synchronize(dev)
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
@@ -234,29 +242,9 @@ def main():
 
     # the same workload with chance-ahead off (every launch seeds and draws
     # in-kernel), for comparison; not the headline number
-    env.set_seed_ahead(False)
-    for _ in range(2):
-        one_step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    steps_o = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
-    t1 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(None, games, steps_o[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    off_elapsed = time.perf_counter() - t1
-    off_steps = int(steps_o.sum(dtype=torch.int64))
-    if world > 1:
-        t = torch.tensor([off_elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        off_elapsed = t.item()
-        c = torch.tensor([off_steps], dtype=torch.int64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        off_steps = int(c[0])
-    env.set_seed_ahead(True)
+    off_steps, off_elapsed = 0, float("nan")
+    if not args.no_off_compare:
+        off_steps, off_elapsed = off_compare(env, one_step, games, args, dev, world)
 
     api = None
     if args.api_mode and rank == 0:
@@ -292,8 +280,8 @@ def main():
             "chance_ahead": {"on": True, "note": "each hz_play also prepares every board's next episode "
                                                  "(seeding + its pile draws, which do not depend on moves) on "
                                                  "idle CUs; steady state: one preparation per game in the timed "
-                                                 "region", "value_off": off_steps / off_elapsed,
-                             "ms_per_step_off": off_elapsed * 1000.0 / args.steps},
+                                                 "region", "value_off": (off_steps / off_elapsed) if off_steps else None,
+                             "ms_per_step_off": (off_elapsed * 1000.0 / args.steps) if off_steps else None},
             "cpu_baseline": cpu,
             "parity": f"first batch: {first_steps} env steps == C oracle ({ref_total})",
         }
@@ -303,6 +291,35 @@ def main():
     env.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def off_compare(env, one_step, games, args, dev, world):
+    """Time the same workload with chance-ahead off (every launch seeds and
+    draws in-kernel); returns (env steps of all ranks, max elapsed)."""
+    env.set_seed_ahead(False)
+    for _ in range(2):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    steps_o = torch.zeros(args.steps, env.n, dtype=torch.int32, device=dev)
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(None, games, steps_o[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t1
+    total = int(steps_o.sum(dtype=torch.int64))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        c = torch.tensor([total], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total = int(c[0])
+    env.set_seed_ahead(True)
+    return total, elapsed
 
 
 def api_mode(env, dev, stream, plies=MAX_PLIES, reps=5):
