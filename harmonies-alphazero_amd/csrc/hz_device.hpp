@@ -836,6 +836,54 @@ __device__ __forceinline__ int kth_action(const uint64_t mask[3], int k) {
   return base + select32(word, k - pre);
 }
 
+// The benchmark rule's action without materialising the 143-bit mask (the
+// fused rollout when no trajectory is recorded): with h the rule hash's top
+// 32 bits, the action is the k-th legal one, k = (h * L) >> 32, in ascending
+// action order; for placements that is tile-major over the hand's distinct
+// tiles, so the tile is found by prefix counts and the cell by one select.
+// Returns -1 when there is no legal move.
+__device__ __forceinline__ int rule_action(const State& s, uint32_t h) {
+  int ph = phase_of(s.misc);
+  if (ph == PH_CHOOSE) {
+    int np = npiles_of(s.piles);
+    return np ? (int)(((uint64_t)h * (uint32_t)np) >> 32) : -1;
+  }
+  uint32_t b[4];
+  planes_of(s, player_of(s.misc), b);
+  uint32_t empty = kAll23 & ~(b[0] | b[1] | b[2] | b[3]);
+  uint32_t wood1 = is_code<3>(b), stone1 = is_code<4>(b), stone2 = is_code<8>(b), bld1 = is_code<5>(b);
+  int nh = (ph >= PH_P1 && ph <= PH_P3) ? hand_n(s.misc) : 0;
+  uint32_t has = 0;
+#pragma unroll
+  for (int j = 0; j < 3; j++) has |= j < nh ? 1u << hand_tile(s.misc, j) : 0u;
+  uint32_t m[6];
+  int c[6], L = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    uint32_t mt = empty;
+    if (t == PLANT) mt |= wood1;
+    if (t == STONE) mt |= stone1 | stone2;
+    if (t == BUILDING) mt |= wood1 | stone1 | bld1;
+    m[t] = (has >> t) & 1u ? mt : 0u;
+    c[t] = __popc(m[t]);
+    L += c[t];
+  }
+  if (L == 0) return -1;
+  int k = (int)(((uint64_t)h * (uint32_t)L) >> 32);
+  uint32_t word = m[5];
+  int tt = 5, pre = 0;
+  bool found = false;
+#pragma unroll
+  for (int t = 0; t < 5; t++) {
+    bool here = !found && k - pre < c[t];
+    word = here ? m[t] : word;
+    tt = here ? t : tt;
+    found = found || here;
+    pre += found ? 0 : c[t];
+  }
+  return 5 + 23 * tt + select32(word, k - pre);
+}
+
 // ------------------------------------------------------------------- step
 __device__ __forceinline__ void finish_game(State& s) {  // :344-354
   int s0 = score_player(s, 0), s1 = score_player(s, 1);
@@ -1089,6 +1137,9 @@ __device__ __forceinline__ uint64_t rule_hash(uint64_t seed, uint64_t ply) {
   return rule_hash_k(rule_key(seed), ply);
 }
 
+__device__ __forceinline__ uint32_t rule_h32(uint64_t key, int ply) {
+  return (uint32_t)(rule_hash_k(key, (uint64_t)ply) >> 32);
+}
 __device__ __forceinline__ int rule_pick_k(uint64_t key, int ply, int n_legal) {
   uint32_t hi = (uint32_t)(rule_hash_k(key, (uint64_t)ply) >> 32);
   return (int)(((uint64_t)hi * (uint32_t)n_legal) >> 32);

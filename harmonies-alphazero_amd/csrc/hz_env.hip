@@ -34,8 +34,10 @@ struct hz_env {
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
+  uint32_t *seed_mt[2];      // [n][624] seed slots: streams seeded (and pre-twisted) two calls ahead
+  int32_t *seed_tag[2];      // [n] episode each seed slot holds
   int calls;                 // hz_play calls since the last prime
-  int primed, slot_valid[2];
+  int primed, slot_valid[2], seed_valid[2];
 };
 
 #ifdef HZ_DIAG
@@ -322,16 +324,20 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
   }
 }
 
-// Chance-ahead preparation (blocks nblk.. of a k_rollout launch, on CUs the
-// playing blocks leave idle): each board's predicted next episode (the
-// episode counter the previous launch left, plus one): the stream seeded in
-// LDS and pre-twisted, the first `draws` pile draws run on the initial bag
-// (piles packed 9 bits each, cursor after each draw), then the stream written
-// out board-major with the tag.
-__device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ tag,
-                                              uint64_t *__restrict__ pile, int32_t *__restrict__ cur,
-                                              const int32_t *__restrict__ ep_final, int n, uint64_t seed_base,
-                                              int draws) {
+// Chance-ahead preparation, a two-stage pipeline in the blocks of each
+// hz_play launch beyond the playing ones (on CUs those leave idle):
+//   seed blocks  [2 nblk, 3 nblk): the stream of each board's episode two
+//     calls ahead (the episode counter the previous launch left, plus two),
+//     seeded in LDS and pre-twisted, written to a seed slot with its tag;
+//   draw blocks  [nblk, 2 nblk): each board's next episode (counter plus
+//     one): its stream staged from the seed slot the previous launch wrote
+//     (seeded in place when the tag disagrees), the first `draws` pile draws
+//     run on the initial bag (piles packed 9 bits each, cursor after each
+//     draw), then stream, script and tag written to a play slot.
+// Seeding (two serial 623-step chains) and drawing thus run side by side,
+// each on its own CUs, and neither is on the playing blocks' path.
+__device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ out_tag,
+                                           const int32_t *__restrict__ ep_final, int n, uint64_t seed_base) {
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b0 = blk * kBlock;
@@ -340,10 +346,40 @@ __device__ __forceinline__ void prepare_block(int blk, uint32_t *__restrict__ ou
   uint64_t actmask = __ballot(act);
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
   if (tid < 64 && act) {
-    int e = ep_final[b] + 1;
+    int e = ep_final[b] + 2;
     mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
-    d.m.twist_ahead(kAheadTwist);
+    LdsMT m(lane, kMTSeeded);
+    m.twist_ahead(kAheadTwist);  // cursor kMTAhead
+    out_tag[b] = e;
+  }
+  __syncthreads();
+  stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
+}
+
+__device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__ in_mt,
+                                           const int32_t *__restrict__ in_tag, uint32_t *__restrict__ out_mt,
+                                           int32_t *__restrict__ tag, uint64_t *__restrict__ pile,
+                                           int32_t *__restrict__ cur, const int32_t *__restrict__ ep_final, int n,
+                                           uint64_t seed_base, int draws) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  int b0 = blk * kBlock;
+  int b = b0 + lane;
+  bool act = b < n;
+  uint64_t actmask = __ballot(act);
+  int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  int e = act ? ep_final[b] + 1 : 0;
+  bool seeded = act && in_tag && in_tag[b] == e;
+  uint64_t seededmask = __ballot(seeded);
+  if (seededmask) stage_mt(const_cast<uint32_t *>(in_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
+  __syncthreads();
+  if (tid < 64 && act) {
+    if (!seeded) {
+      mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
+      LdsMT m(lane, kMTSeeded);
+      m.twist_ahead(kAheadTwist);
+    }
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
     uint64_t bag = 0;
 #pragma unroll
     for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
@@ -388,10 +424,18 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     int32_t *__restrict__ ep_final, int nblk,
                                                     uint32_t *__restrict__ prep_mt, int32_t *__restrict__ prep_tag,
                                                     uint64_t *__restrict__ prep_pile, int32_t *__restrict__ prep_cur,
-                                                    const int32_t *__restrict__ prep_ep) {
-  if ((int)blockIdx.x >= nblk) {  // chance-ahead role (uniform per block)
-    prepare_block((int)blockIdx.x - nblk, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base,
-                  ahead_draws);
+                                                    const int32_t *__restrict__ prep_ep,
+                                                    const uint32_t *__restrict__ seed_in_mt,
+                                                    const int32_t *__restrict__ seed_in_tag,
+                                                    uint32_t *__restrict__ seed_out_mt,
+                                                    int32_t *__restrict__ seed_out_tag) {
+  if ((int)blockIdx.x >= nblk) {  // chance-ahead roles (uniform per block)
+    int blk = (int)blockIdx.x - nblk;
+    if (blk < nblk)
+      draw_block(blk, seed_in_mt, seed_in_tag, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base,
+                 ahead_draws);
+    else
+      seed_block(blk - nblk, seed_out_mt, seed_out_tag, prep_ep, n, seed_base);
     return;
   }
   __shared__ uint64_t s_lds_mask, s_recopy_mask;
@@ -465,25 +509,28 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         reset_state(s, draw);
         g_ply = 0;
       }
-      uint64_t mk[3];
+      int a;
       HZ_ACC(8, t0);
-      int L = legal_mask(s, mk);
-      HZ_ACC(9, t0);
-      if (Record && traj_state) {
-        uint64_t *o = traj_state + (size_t)i * 6 * n + b;
-        o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
-        o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+      if constexpr (Record) {
+        uint64_t mk[3];
+        int L = legal_mask(s, mk);
+        HZ_ACC(9, t0);
+        if (traj_state) {
+          uint64_t *o = traj_state + (size_t)i * 6 * n + b;
+          o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
+          o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+        }
+        if (traj_mask) {
+          uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
+          o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+        }
+        a = L ? kth_action(mk, rule_pick_k(rkey, g_ply, L)) : -1;
+        if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
+      } else {
+        a = rule_action(s, rule_h32(rkey, g_ply));  // legal mask + rule pick, fused
+        HZ_ACC(9, t0);
       }
-      if (Record && traj_mask) {
-        uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
-        o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
-      }
-      if (L == 0) {  // stuck board (unreachable from HarmoniesGameState())
-        if (Record && traj_action) traj_action[(size_t)i * n + b] = -1;
-        break;
-      }
-      int a = kth_action(mk, rule_pick_k(rkey, g_ply, L));
-      if (Record && traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
+      if (a < 0) break;  // stuck board (unreachable from HarmoniesGameState())
       HZ_ACC(10, t0);
       bool te = phase_of(s.misc) == PH_P3;
       step_trusted<true>(s, a, draw);
@@ -654,6 +701,9 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
          hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->seed_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc(&e->seed_tag[k], n * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(e->seed_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
@@ -673,6 +723,8 @@ void hz_env_destroy(hz_env *e) {
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
     if (e->ahead_pile[k]) (void)hipFree(e->ahead_pile[k]);
     if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
+    if (e->seed_mt[k]) (void)hipFree(e->seed_mt[k]);
+    if (e->seed_tag[k]) (void)hipFree(e->seed_tag[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
   }
   if (e->state) (void)hipFree(e->state);
@@ -754,11 +806,12 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
 }
 
 // hz_play's chance-ahead pipeline: one launch per call, blocks [0, nblk)
-// play from slot r = calls & 1, blocks [nblk, 2 nblk) prepare slot w = r ^ 1
-// for the next call.  Launch order on the stream is the only synchronisation:
-// a slot is written by call i's preparing blocks and read by call i+1's
-// playing blocks; the preparing blocks read ep_final[w], written by call
-// i-1's playing blocks (the episode counter each board ended with).  The
+// play from play slot r = calls & 1, blocks [nblk, 2 nblk) fill play slot
+// w = r ^ 1 for the next call from seed slot r, blocks [2 nblk, 3 nblk)
+// fill seed slot w for the call after.  Launch order on the stream is the
+// only synchronisation: a slot written by call i is read by call i+1; the
+// preparing blocks read ep_final[w], written by call i-1's playing blocks
+// (the episode counter each board ended with).  The
 // prediction (call i+1 resets to that counter plus one) only decides which
 // boards skip seeding and drawing: a board replays a slot only when the
 // slot's tag equals its episode counter, so results never depend on it.
@@ -781,6 +834,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
       if (hipMemcpyAsync(e->ep_final[w], e->episode, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream))
         return 1;
       e->slot_valid[r] = 0;
+      e->seed_valid[r] = 0;
       e->primed = 1;
     }
     if (e->slot_valid[r]) {
@@ -790,7 +844,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
       ahead_cur = e->ahead_cur[r];
     }
     ep_final = e->ep_final[r];
-    grid = 2 * nblk;
+    grid = 3 * nblk;
   } else {
     e->primed = 0;
   }
@@ -801,11 +855,13 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
-                     e->ahead_cur[w], e->ep_final[w]);
+                     e->ahead_cur[w], e->ep_final[w], e->seed_mt[r], e->seed_valid[r] ? e->seed_tag[r] : nullptr,
+                     e->seed_mt[w], e->seed_tag[w]);
   int err = launch_err();
   if (err) return err;
   if (pipe) {
     e->slot_valid[w] = 1;
+    e->seed_valid[w] = 1;
     e->calls++;
   }
   return 0;
