@@ -34,8 +34,10 @@ struct hz_env {
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
-  uint32_t *seed_mt[2];      // [n][624] seed slots: streams seeded (and pre-twisted) two calls ahead
+  uint32_t *seed_mt[2];      // [n][624] seed slots: streams seeded two calls ahead, first draws run
   int32_t *seed_tag[2];      // [n] episode each seed slot holds
+  uint64_t *seed_pile[2];    // [kAheadWords][n] their partial scripts
+  int32_t *seed_cur[2];      // [kSeedDraws + 1][n] cursors
   int calls;                 // hz_play calls since the last prime
   int primed, slot_valid[2], seed_valid[2];
 };
@@ -326,18 +328,50 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 
 // Chance-ahead preparation, a two-stage pipeline in the blocks of each
 // hz_play launch beyond the playing ones (on CUs those leave idle):
-//   seed blocks  [2 nblk, 3 nblk): the stream of each board's episode two
-//     calls ahead (the episode counter the previous launch left, plus two),
-//     seeded in LDS and pre-twisted, written to a seed slot with its tag;
+//   seed blocks  [2 nblk, 3 nblk): each board's episode two calls ahead (the
+//     episode counter the previous launch left, plus two): the stream seeded
+//     in LDS and pre-twisted, its first kSeedDraws pile draws run, stream,
+//     partial script, cursors and tag written to a seed slot;
 //   draw blocks  [nblk, 2 nblk): each board's next episode (counter plus
-//     one): its stream staged from the seed slot the previous launch wrote
-//     (seeded in place when the tag disagrees), the first `draws` pile draws
-//     run on the initial bag (piles packed 9 bits each, cursor after each
-//     draw), then stream, script and tag written to a play slot.
+//     one): the seed slot the previous launch wrote staged in (everything
+//     redone in place when its tag disagrees), the remaining draws run, and
+//     stream, script (piles packed 9 bits each), cursor after each draw and
+//     tag written to a play slot.
 // Seeding (two serial 623-step chains) and drawing thus run side by side,
-// each on its own CUs, and neither is on the playing blocks' path.
+// each on its own CUs, and neither is on the playing blocks' path;
+// kSeedDraws balances the two stages.
+constexpr int kSeedDraws = 6;
+static_assert(kSeedDraws <= 7 && kSeedDraws <= kAheadDraws, "the seed stage's piles sit in script word 0");
+
+// run script entries [from, to) of a board's chance sequence on its LDS
+// stream, recording packed piles and the cursor after each draw
+__device__ __forceinline__ void run_script(StreamDraw<LdsMT>& d, uint64_t& bag, uint64_t q[kAheadWords],
+                                           int32_t* __restrict__ cur, int n, int b, int from, int to) {
+#pragma unroll
+  for (int i = 0; i < kAheadDraws; i++) {
+    if (i >= from && i < to) {
+      uint32_t p9 = d(bag);
+      if (p9 != 0x1FFu) apply_pile(bag, p9);
+      // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
+      int bit = 9 * i, wd = bit / 64, off = bit % 64;
+      q[wd] |= (uint64_t)p9 << off;
+      if (off > 55) q[wd + 1] |= (uint64_t)p9 >> (64 - off);
+      cur[(size_t)(i + 1) * n + b] = d.m.cursor();
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t initial_bag() {
+  uint64_t bag = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+  return bag;
+}
+
 __device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ out_tag,
-                                           const int32_t *__restrict__ ep_final, int n, uint64_t seed_base) {
+                                           uint64_t *__restrict__ out_pile, int32_t *__restrict__ out_cur,
+                                           const int32_t *__restrict__ ep_final, int n, uint64_t seed_base,
+                                           int draws) {
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b0 = blk * kBlock;
@@ -348,8 +382,13 @@ __device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_m
   if (tid < 64 && act) {
     int e = ep_final[b] + 2;
     mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-    LdsMT m(lane, kMTSeeded);
-    m.twist_ahead(kAheadTwist);  // cursor kMTAhead
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
+    d.m.twist_ahead(kAheadTwist);  // cursor kMTAhead
+    out_cur[b] = d.m.cursor();
+    uint64_t bag = initial_bag(), q[kAheadWords] = {};
+    run_script(d, bag, q, out_cur, n, b, 0, draws < kSeedDraws ? draws : kSeedDraws);
+#pragma unroll
+    for (int w = 0; w < kAheadWords; w++) out_pile[(size_t)w * n + b] = q[w];
     out_tag[b] = e;
   }
   __syncthreads();
@@ -357,7 +396,8 @@ __device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_m
 }
 
 __device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__ in_mt,
-                                           const int32_t *__restrict__ in_tag, uint32_t *__restrict__ out_mt,
+                                           const int32_t *__restrict__ in_tag, const uint64_t *__restrict__ in_pile,
+                                           const int32_t *__restrict__ in_cur, uint32_t *__restrict__ out_mt,
                                            int32_t *__restrict__ tag, uint64_t *__restrict__ pile,
                                            int32_t *__restrict__ cur, const int32_t *__restrict__ ep_final, int n,
                                            uint64_t seed_base, int draws) {
@@ -374,29 +414,32 @@ __device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__
   if (seededmask) stage_mt(const_cast<uint32_t *>(in_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
   __syncthreads();
   if (tid < 64 && act) {
-    if (!seeded) {
+    int k0 = draws < kSeedDraws ? draws : kSeedDraws;
+    uint64_t bag = initial_bag(), q[kAheadWords] = {};
+    int start;
+    if (seeded) {  // continue after the seed stage's draws
+#pragma unroll
+      for (int w = 0; w < kAheadWords; w++) q[w] = in_pile[(size_t)w * n + b];
+#pragma unroll
+      for (int i = 0; i <= kSeedDraws; i++)
+        if (i <= k0) cur[(size_t)i * n + b] = in_cur[(size_t)i * n + b];
+#pragma unroll
+      for (int i = 0; i < kSeedDraws; i++) {
+        if (i < k0) {
+          uint32_t p9 = (uint32_t)(q[0] >> (9 * i)) & 0x1FFu;  // entries 0..6 sit in word 0
+          if (p9 != 0x1FFu) apply_pile(bag, p9);
+        }
+      }
+      start = k0;
+    } else {
       mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
       LdsMT m(lane, kMTSeeded);
       m.twist_ahead(kAheadTwist);
+      cur[b] = m.cursor();
+      start = 0;
     }
-    StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
-    uint64_t bag = 0;
-#pragma unroll
-    for (int t = 0; t < 6; t++) bag = set_bits(bag, 11 + 5 * t, 5, (uint64_t)initial_count(t));
-    uint64_t q[kAheadWords] = {};
-    cur[b] = d.m.cursor();
-#pragma unroll
-    for (int i = 0; i < kAheadDraws; i++) {
-      if (i < draws) {
-        uint32_t p9 = d(bag);
-        if (p9 != 0x1FFu) apply_pile(bag, p9);
-        // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
-        int bit = 9 * i, wd = bit / 64, off = bit % 64;
-        q[wd] |= (uint64_t)p9 << off;
-        if (off > 55) q[wd + 1] |= (uint64_t)p9 >> (64 - off);
-        cur[(size_t)(i + 1) * n + b] = d.m.cursor();
-      }
-    }
+    StreamDraw<LdsMT> d{LdsMT(lane, seeded ? in_cur[(size_t)k0 * n + b] : kMTAhead)};
+    run_script(d, bag, q, cur, n, b, start, draws);
 #pragma unroll
     for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
     tag[b] = e;
@@ -427,15 +470,30 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     const int32_t *__restrict__ prep_ep,
                                                     const uint32_t *__restrict__ seed_in_mt,
                                                     const int32_t *__restrict__ seed_in_tag,
+                                                    const uint64_t *__restrict__ seed_in_pile,
+                                                    const int32_t *__restrict__ seed_in_cur,
                                                     uint32_t *__restrict__ seed_out_mt,
-                                                    int32_t *__restrict__ seed_out_tag) {
+                                                    int32_t *__restrict__ seed_out_tag,
+                                                    uint64_t *__restrict__ seed_out_pile,
+                                                    int32_t *__restrict__ seed_out_cur) {
+#ifdef HZ_DIAG
+  uint64_t role_t0 = __builtin_amdgcn_s_memtime();
+#endif
   if ((int)blockIdx.x >= nblk) {  // chance-ahead roles (uniform per block)
     int blk = (int)blockIdx.x - nblk;
     if (blk < nblk)
-      draw_block(blk, seed_in_mt, seed_in_tag, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base,
-                 ahead_draws);
+      draw_block(blk, seed_in_mt, seed_in_tag, seed_in_pile, seed_in_cur, prep_mt, prep_tag, prep_pile, prep_cur,
+                 prep_ep, n, seed_base, ahead_draws);
     else
-      seed_block(blk - nblk, seed_out_mt, seed_out_tag, prep_ep, n, seed_base);
+      seed_block(blk - nblk, seed_out_mt, seed_out_tag, seed_out_pile, seed_out_cur, prep_ep, n, seed_base,
+                 ahead_draws);
+#ifdef HZ_DIAG
+    {  // role durations: slot 6 (draw blocks), 7 (seed blocks), per board of the block
+      int bb = (blk % nblk) * kBlock + (threadIdx.x & 63);
+      if (g_stamps && threadIdx.x < 64 && bb < n)
+        g_stamps[(size_t)bb * 16 + (blk < nblk ? 6 : 7)] = __builtin_amdgcn_s_memtime() - role_t0;
+    }
+#endif
     return;
   }
   __shared__ uint64_t s_lds_mask, s_recopy_mask;
@@ -572,6 +630,9 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   uint64_t lds_mask = s_lds_mask & actmask, recopy = s_recopy_mask & actmask;
   if (lds_mask) stage_mt(g, nb, tid, lds_mask, false);
   if (recopy) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid, kStageThreads, recopy);
+#ifdef HZ_DIAG
+  if (g_stamps && threadIdx.x < 64 && act) g_stamps[(size_t)b * 16 + 5] = __builtin_amdgcn_s_memtime() - role_t0;
+#endif
 }
 
 // ---------------------------------------------------------- greedy agent
@@ -704,6 +765,8 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->seed_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc(&e->seed_tag[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->seed_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->seed_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
+         hipMalloc(&e->seed_cur[k], n * (kSeedDraws + 1) * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
@@ -725,6 +788,8 @@ void hz_env_destroy(hz_env *e) {
     if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
     if (e->seed_mt[k]) (void)hipFree(e->seed_mt[k]);
     if (e->seed_tag[k]) (void)hipFree(e->seed_tag[k]);
+    if (e->seed_pile[k]) (void)hipFree(e->seed_pile[k]);
+    if (e->seed_cur[k]) (void)hipFree(e->seed_cur[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
   }
   if (e->state) (void)hipFree(e->state);
@@ -856,7 +921,8 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
                      e->ahead_cur[w], e->ep_final[w], e->seed_mt[r], e->seed_valid[r] ? e->seed_tag[r] : nullptr,
-                     e->seed_mt[w], e->seed_tag[w]);
+                     e->seed_pile[r], e->seed_cur[r], e->seed_mt[w], e->seed_tag[w], e->seed_pile[w],
+                     e->seed_cur[w]);
   int err = launch_err();
   if (err) return err;
   if (pipe) {

@@ -30,4 +30,18 @@ for rep in range(3):
            "roll_top_cyc": s[:, 8].mean().item(), "roll_legal_cyc": s[:, 9].mean().item(),
            "roll_pick_cyc": s[:, 10].mean().item(), "roll_step_cyc": s[:, 11].mean().item(),
            "roll_turnend_cyc": s[:, 12].mean().item(), "roll_final_cyc": s[:, 13].mean().item()}
+# steady-state hz_play (chance-ahead primed: boards replay prepared pile scripts)
+for _ in range(3):
+    env.rollout(96, reset=True)
+stamps.zero_()
+f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+f0.record(); env.rollout(96, reset=True); f1.record()
+torch.cuda.synchronize()
+s = stamps.cpu().double()
+out.update({"play_primed_us": f0.elapsed_time(f1) * 1e3,
+            "primed_top_cyc": s[:, 8].mean().item(), "primed_legal_cyc": s[:, 9].mean().item(),
+            "primed_pick_cyc": s[:, 10].mean().item(), "primed_step_cyc": s[:, 11].mean().item(),
+            "primed_turnend_cyc": s[:, 12].mean().item(), "primed_final_cyc": s[:, 13].mean().item(),
+            "role_play_cyc_max": s[:, 5].max().item(), "role_draw_cyc_max": s[:, 6].max().item(),
+            "role_seed_cyc_max": s[:, 7].max().item()})
 print(json.dumps(out))
