@@ -49,8 +49,11 @@ def parse():
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3],
-                    help="2: env kernels (default, the headline); 3: MCTS self-play moves with the network")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+                    help="2: env kernels (default, the headline); 3: MCTS self-play moves with the network; "
+                         "5: whole training iterations (self-play -> buffer -> training -> arena)")
+    ap.add_argument("--iterations", type=int, default=2, help="config 5: training iterations timed")
+    ap.add_argument("--eval-games", type=int, default=32, help="config 5: arena games per evaluation")
     ap.add_argument("--sims", type=int, default=200, help="config 3: MCTS simulations per move")
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     return ap.parse_args()
@@ -78,6 +81,88 @@ def cpu_baseline(boards, seconds):
             "games_per_s": games / dt,
             "sample": f"{k} batches x {boards} rule-driven games ({steps} env steps) in {dt:.1f}s, "
                       f"C oracle with OpenMP, {nthreads} threads"}
+
+
+def bench_loop(args, dev, rank, world):
+    """BASELINE config 5: the reference's main.py loop (trainer.Trainer) on
+    the batched engine, one step = one training iteration: `boards` games per
+    rank of self-play with the best model (MCTS `sims` per move, self-play
+    noise), RCCL all-gather of the records into every rank's replay buffer,
+    rank-0 training (reference training config: Adam, batch 64, 2 epochs over
+    the buffer, buffer 50,000), weight broadcast, checkpoint, buffer file, and
+    every iteration an arena of `eval_games` games between candidate and best
+    (mcts_config_eval with `sims` simulations).  Reports games/hour."""
+    import tempfile
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    from hzamd.trainer import Trainer
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = True
+    model_cfg = dict(DEFAULT, board_size=(5, 7))
+    train_cfg = {"device": str(dev), "optimizer_type": "Adam", "learning_rate": 0.001, "weight_decay": 0.0001,
+                 "value_loss_weight": 1.0, "policy_loss_weight": 1.0, "batch_size": 64, "momentum": 0.9,
+                 "use_scheduler": True, "scheduler_type": "StepLR", "scheduler_step_size": 30,
+                 "scheduler_gamma": 0.5, "force_lr_reset_on_load": False, "new_forced_lr": 0.000125}
+    mcts_cfg = {"num_simulations": args.sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+                "fpu_value": 0.25, "turns_until_tau0": 15, "action_size": 143, "testing": False}
+    tmp = tempfile.mkdtemp(prefix=f"hz_loop_r{rank}_")
+    sp_cfg = {"num_iterations": args.iterations + 1, "num_games_per_iter": args.boards, "epochs_per_iter": 2,
+              "replay_buffer_size": 50000, "checkpoint_folder": os.path.join(tmp, "ck"),
+              "replay_buffer_folder": os.path.join(tmp, "buf"), "replay_buffer_filename": "replay_buffer.pkl",
+              "eval_frequency": 1, "eval_episodes": args.eval_games, "eval_win_rate_threshold": 0.51,
+              "best_model_filename": "best_model.pth.tar"}
+    mm = ModelManager(model_cfg, train_cfg)
+    tr = Trainer(mm, mcts_cfg, sp_cfg, train_cfg, eval_mcts_config={"num_simulations": args.sims},
+                 seed_base=args.seed_base, log=lambda *_: None)
+    # warm-up iteration (kernels, MIOpen algorithm search), then the timed ones
+    tr.iteration = 0
+    tr.execute_self_play_phase(tr.best_model_manager)
+    tr.execute_training_phase()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    phases = {"self_play": 0.0, "training": 0.0, "evaluation": 0.0}
+    games = 0
+    for it in range(1, args.iterations + 1):
+        tr.iteration = it
+        a = time.perf_counter()
+        sp = tr.execute_self_play_phase(tr.best_model_manager)
+        b = time.perf_counter()
+        tr.execute_training_phase()
+        tr.model_manager.step_scheduler()
+        if rank == 0:
+            tr.model_manager.save_checkpoint(folder=sp_cfg["checkpoint_folder"], filename="latest_candidate.pth.tar",
+                                             iteration=it)
+        tr.save_buffer()
+        torch.cuda.synchronize(dev)
+        c = time.perf_counter()
+        tr.evaluate_model()
+        torch.cuda.synchronize(dev)
+        d = time.perf_counter()
+        phases["self_play"] += b - a
+        phases["training"] += c - b
+        phases["evaluation"] += d - c
+        games += sp["games"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "full loop self-play games/hour (self-play -> buffer -> training -> arena)",
+            "value": games / elapsed * 3600.0, "unit": "games/hour", "n_gpus": world, "steps": args.iterations,
+            "warmup": 1, "ms_per_step": elapsed * 1000.0 / args.iterations, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic: random-init network, seeded games",
+            "config": {"workload": f"config5: {args.boards} games/rank/iteration, {args.sims} sims/move, "
+                                   f"arena {args.eval_games} games every iteration, default 128fx8 net",
+                       "boards_per_gpu": args.boards, "sims": args.sims, "parallelism": f"shard{world}"},
+            "phase_seconds": phases, "games": games,
+        }))
 
 
 def bench_selfplay(args, dev, rank, world):
@@ -160,6 +245,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+    if args.config == 5:
+        bench_loop(args, dev, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.config == 3:
         bench_selfplay(args, dev, rank, world)
         if world > 1:

@@ -32,7 +32,7 @@ from . import distributed as hd
 from .manager import ModelManager
 from .mcts import BatchedPredictor
 from .selfplay import SelfPlay
-from .train import RecordSource, training_phase
+from .train import featurize, training_phase
 
 
 def _dist():
@@ -100,7 +100,7 @@ class Trainer:
     def execute_training_phase(self):
         res = None
         if self.rank == 0:
-            res = training_phase(self.model_manager, RecordSource(self.replay_buffer.records()),
+            res = training_phase(self.model_manager, featurize(self.replay_buffer.records()),
                                  self.self_play_config["epochs_per_iter"], self.training_config["batch_size"])
         if _dist():
             hd.broadcast_weights(self.model_manager.model, src=0)
