@@ -51,6 +51,7 @@ __device__ uint64_t *g_stamps;
     if (g_stamps) g_stamps[(size_t)b * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);                                    \
   } while (0)
+#ifndef HZ_DIAG_ROLES_ONLY
 #define HZ_ACC(slot, t0)                                                  \
   do {                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                    \
@@ -59,6 +60,11 @@ __device__ uint64_t *g_stamps;
     t0 = _t;                                                              \
     __builtin_amdgcn_sched_barrier(0);                                    \
   } while (0)
+#else  // role durations only (tools/libhz_roles.so): no stamps inside the ply loop
+#define HZ_ACC(slot, t0) \
+  do {                   \
+  } while (0)
+#endif
 #else
 #define HZ_STAMP(slot) \
   do {                 \

@@ -2,7 +2,9 @@
 (tools/libhz_diag.so): per-lane s_memtime stamps, reported in cycles."""
 import ctypes, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["HZ_LIB"] = os.path.join(ROOT, "tools", "libhz_diag.so")
+# tools/diag.py [roles]: "roles" uses libhz_roles.so (role durations only, no
+# stamps inside the ply loop)
+os.environ.setdefault("HZ_LIB", os.path.join(ROOT, "tools", "libhz_roles.so" if "roles" in sys.argv[1:] else "libhz_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "harmonies-alphazero_amd"))
 import torch
 import hzamd._native as nat
