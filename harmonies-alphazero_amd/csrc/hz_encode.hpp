@@ -22,6 +22,41 @@ namespace {  // each translation unit gets its own copy of the kernels
 // stream is the only HBM traffic.
 constexpr int kEncWaves = 4;  // waves (pairs) per 256-thread block
 
+// 23-bit cell set -> the 35-bit tensor-position set (bit y*7 + x, y = r+2,
+// x = q+3).  A column's cells are consecutive cell indices with consecutive
+// y, i.e. positions 7 apart: one multiply spreads a column's run (v * 0x1041041
+// puts bit i at 7 i, masked by 0x10204081).
+__device__ __forceinline__ uint64_t to_grid35(uint32_t m) {
+  auto col = [&](int c0, int k, int base) -> uint64_t {
+    uint32_t v = (m >> c0) & ((1u << k) - 1);
+    uint32_t sp = k == 1 ? v : (v * 0x1041041u) & 0x10204081u;
+    return (uint64_t)sp << base;
+  };
+  static_assert(grid_bit(0) == 28 && grid_bit(1) == 15 && grid_bit(4) == 2 && grid_bit(9) == 3 &&
+                    grid_bit(14) == 4 && grid_bit(19) == 5 && grid_bit(22) == 6,
+                "column bases");
+  return col(0, 1, 28) | col(1, 3, 15) | col(4, 5, 2) | col(9, 5, 3) | col(14, 5, 4) | col(19, 3, 5) |
+         col(22, 1, 6);
+}
+
+// For channel tile*3 + pos (18 of them): the 13-bit set of stack codes whose
+// tile at height pos is that tile (code 0, the empty stack, never).
+__host__ __device__ constexpr uint32_t code_set(int rem) {
+  constexpr int kTabs[3][13] = {{7, 0, 1, 2, 3, 4, 5, 2, 3, 3, 2, 3, 4},
+                                {7, 7, 7, 7, 7, 7, 7, 1, 3, 3, 4, 4, 4},
+                                {7, 7, 7, 7, 7, 7, 7, 7, 7, 3, 7, 7, 7}};
+  uint32_t s = 0;
+  for (int c = 1; c < 13; c++) s |= (uint32_t)(kTabs[rem % 3][c] == rem / 3) << c;
+  return s;
+}
+__host__ __device__ constexpr uint64_t code_sets(int from, int cnt) {
+  uint64_t r = 0;
+  for (int i = 0; i < cnt; i++) r |= (uint64_t)code_set(from + i) << (13 * i);
+  return r;
+}
+constexpr uint64_t kCodeSetLo = code_sets(0, 4), kCodeSetMid = code_sets(4, 4), kCodeSetHi = code_sets(8, 4),
+                   kCodeSetTop = code_sets(12, 4), kCodeSetEnd = code_sets(16, 2);
+
 __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
                                                       long item_stride, const int32_t *__restrict__ idx, int m,
                                                       float *__restrict__ board) {
@@ -43,19 +78,26 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
         const uint64_t *sb = st + bi * item_stride;
         if (ch < 36) {
           int p = ch >= 18 ? 1 : 0;
-          int rem = ch - 18 * p, t = rem / 3, sp = rem - 3 * t;
+          int rem = ch - 18 * p;  // tile * 3 + stack position
           int sh = 32 * p;
           uint32_t b0 = (uint32_t)(sb[0] >> sh), b1 = (uint32_t)(sb[word_stride] >> sh);
           uint32_t b2 = (uint32_t)(sb[2 * word_stride] >> sh), b3 = (uint32_t)(sb[3 * word_stride] >> sh);
-          uint64_t tab = sp == 0 ? kStackPos0 : sp == 1 ? kStackPos1 : kStackPos2;
+          // the stack codes whose tile at this height is this tile, then the
+          // cells holding one of them (bit-sliced over the 4 code planes)
+          uint32_t set = (uint32_t)(kCodeSetLo >> (13 * (rem < 4 ? rem : 0))) & 0x1FFFu;
+          set = rem >= 4 && rem < 8 ? (uint32_t)(kCodeSetMid >> (13 * (rem - 4))) & 0x1FFFu : set;
+          set = rem >= 8 && rem < 12 ? (uint32_t)(kCodeSetHi >> (13 * (rem - 8))) & 0x1FFFu : set;
+          set = rem >= 12 && rem < 16 ? (uint32_t)(kCodeSetTop >> (13 * (rem - 12))) & 0x1FFFu : set;
+          set = rem >= 16 ? (uint32_t)(kCodeSetEnd >> (13 * (rem - 16))) & 0x1FFFu : set;
+          uint32_t n0 = ~b0, n1 = ~b1, n2 = ~b2, n3 = ~b3, m23 = 0;
 #pragma unroll
-          for (int cell = 0; cell < 23; cell++) {
-            int code = (int)(((b0 >> cell) & 1) | (((b1 >> cell) & 1) << 1) | (((b2 >> cell) & 1) << 2) |
-                             (((b3 >> cell) & 1) << 3));
-            mask |= (uint64_t)((int)((tab >> (3 * code)) & 7) == t) << grid_bit(cell);
+          for (int code = 1; code < 13; code++) {
+            uint32_t hit = ((code & 1) ? b0 : n0) & ((code & 2) ? b1 : n1) & ((code & 4) ? b2 : n2) &
+                           ((code & 8) ? b3 : n3);
+            m23 |= ((set >> code) & 1u) ? hit : 0u;
           }
-          val = 1.f;
-        } else {
+          mask = to_grid35(m23);
+          val = 1.f;        } else {
           uint64_t misc = sb[5 * word_stride];
           mask = kValid35;
           if (ch == 36) {
@@ -74,18 +116,27 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
   if (!live) return;
   int nfl = j0 + 1 < m ? 2660 : 1330;
   float *out = board + j0 * 1330;
+  // element e = 4 q + u of the pair: channel c = 38 (e >= 1330) + el / 35,
+  // position yx = el % 35; tracked incrementally (q advances by 64: e by 256
+  // = 7 channels + 11 positions)
+  int e0 = 4 * lane, c0 = e0 / 35, y0 = e0 - 35 * c0;
   for (int q = lane; q < nfl / 4; q += 64) {
+    // the four elements lie in channel c0 and possibly c0 + 1 (boards
+    // switch at element 1330 = 38 x 35: channel 38 onward is the second)
+    uint64_t ma = smask[w][c0], mb = smask[w][c0 + 1 < 76 ? c0 + 1 : c0];
+    float va = sval[w][c0], vb = sval[w][c0 + 1 < 76 ? c0 + 1 : c0];
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      int e = 4 * q + u;
-      int bsel = e >= 1330 ? 1 : 0;
-      int el = e - 1330 * bsel;
-      int ch = el / 35, yx = el - 35 * ch;
-      int c = 38 * bsel + ch;
-      v[u] = ((smask[w][c] >> yx) & 1) ? sval[w][c] : 0.f;
+      int yx = y0 + u;
+      bool nxt = yx >= 35;
+      int pos = nxt ? yx - 35 : yx;
+      v[u] = (((nxt ? mb : ma) >> pos) & 1) ? (nxt ? vb : va) : 0.f;
     }
     reinterpret_cast<float4 *>(out)[q] = make_float4(v[0], v[1], v[2], v[3]);
+    c0 += 7;
+    y0 += 11;
+    if (y0 >= 35) { y0 -= 35; c0++; }
   }
   if (nfl == 1330 && lane < 2) {  // odd tail: floats 1328, 1329
     int el = 1328 + lane, ch = el / 35, yx = el - 35 * ch;
