@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 # SURVEY.md §8(d) algorithmic bytes per unit
 BYTES_PER_ENV_STEP = 152   # 64 B state read + 64 B state write + 18 B mask + ~6 B RNG
 BYTES_PER_RESET = 2564     # 624x4 B MT init + idx + 64 B state
+BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 
@@ -339,6 +340,7 @@ def main():
     api = None
     if args.api_mode and rank == 0:
         api = api_mode(env, dev, stream)
+    enc = encoder_roofline(dev, n, args.seed_base) if rank == 0 else None
 
     if rank == 0:
         import oracle  # test infrastructure: parity guard + cpu_baseline only
@@ -372,6 +374,7 @@ def main():
                                                  "idle CUs; steady state: one preparation per game in the timed "
                                                  "region", "value_off": (off_steps / off_elapsed) if off_steps else None,
                              "ms_per_step_off": (off_elapsed * 1000.0 / args.steps) if off_steps else None},
+            "encoder_roofline": enc,
             "cpu_baseline": cpu,
             "parity": f"first batch: {first_steps} env steps == C oracle ({ref_total})",
         }
@@ -381,6 +384,33 @@ def main():
     env.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def encoder_roofline(dev, n, seed_base):
+    """hz_encode_states (create_state_tensors) over one batch of recorded game
+    states (every ply of n rule-driven games): output bytes / time vs HBM peak."""
+    from hzamd.env import BatchedEnv
+    from hzamd.selfplay import encode_states
+    env = BatchedEnv(n, seed_base=seed_base + (1 << 40), device=dev)
+    env.reset()
+    _, _, (ts, _, ta) = env.rollout(MAX_PLIES, record=True)
+    states = ts.permute(0, 2, 1).reshape(-1, 6)[(ta >= 0).reshape(-1)].contiguous()
+    m = states.shape[0]
+    for _ in range(3):
+        encode_states(states)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        encode_states(states)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    gbs = m * BYTES_PER_ENCODE / (ms * 1e-3) / 1e9
+    env.close()
+    return {"kernel": "k_encode_board + k_encode_glob", "states": m, "ms": ms, "achieved": gbs,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "bytes_per_state": BYTES_PER_ENCODE}
 
 
 def off_compare(env, one_step, games, args, dev, world):
