@@ -60,6 +60,16 @@ def parse():
     return ap.parse_args()
 
 
+_RED_DEV = None  # device of reduction tensors: the GPU under RCCL, the CPU under gloo
+
+
+def all_reduce(vals, op):
+    """Reduce a list of numbers over ranks (float64: exact for counts)."""
+    t = torch.tensor(vals, dtype=torch.float64, device=_RED_DEV)
+    dist.all_reduce(t, op=op)
+    return t.tolist()
+
+
 def cpu_baseline(boards, seconds):
     """The C oracle (oracle/hz_oracle.c, the bit-exact CPU port of the
     reference engine) playing the same rule-driven 4096-board batches on the
@@ -150,9 +160,7 @@ def bench_loop(args, dev, rank, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     if rank == 0:
         print(json.dumps({
             "metric": "full loop self-play games/hour (self-play -> buffer -> training -> arena)",
@@ -213,9 +221,7 @@ def bench_selfplay(args, dev, rank, world):
     nn_ms = sum(a.elapsed_time(b) for a, b in nn_ev)
     sims_done = n * args.sims * args.steps
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     sims_all = sims_done * world
     per_move = elapsed / args.steps
     avg_plies = 62.4  # mean game length
@@ -241,11 +247,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    # HZ_BENCH_REHEARSAL=1 (tests only): ranks share the visible GPUs
+    # (local % device_count) and reduce over gloo, to exercise the N > 1 path
+    # on a one-GPU box; the real multi-GPU run uses one GPU per rank and RCCL
+    rehearsal = os.environ.get("HZ_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+    global _RED_DEV
+    _RED_DEV = "cpu" if rehearsal else dev
+    if world > 1:
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if args.config == 5:
         bench_loop(args, dev, rank, world)
         if world > 1:
@@ -308,11 +324,8 @@ def main():
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        c = torch.tensor([timed_steps, timed_games], dtype=torch.int64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
+        c = all_reduce([timed_steps, timed_games], dist.ReduceOp.SUM)
         env_steps_all, games_all = int(c[0]), int(c[1])
     else:
         env_steps_all, games_all = timed_steps, timed_games
@@ -432,12 +445,8 @@ def off_compare(env, one_step, games, args, dev, world):
     elapsed = time.perf_counter() - t1
     total = int(steps_o.sum(dtype=torch.int64))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        c = torch.tensor([total], dtype=torch.int64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        total = int(c[0])
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
+        total = int(all_reduce([total], dist.ReduceOp.SUM)[0])
     env.set_seed_ahead(True)
     return total, elapsed
 

@@ -273,6 +273,36 @@ def test_encoder_bit_exact(Env):
     assert (glob2.cpu().numpy() == f["globs"][idx.numpy()]).all()
 
 
+def test_encoder_odd_counts_and_empty_slots(Env):
+    """Pairs kernel edge cases: an odd number of states (the last pair holds
+    one) and idx < 0 entries (all-zero records, MCTS's inactive boards)."""
+    f = load("encoder.npz")
+    refs = f["states"]
+    env = Env(len(refs), device=DEV)
+    import_refstates(env, refs)
+    for m in (1, 3, 63, 129):
+        idx = torch.arange(m, dtype=torch.int32) * 2 % len(refs)
+        idx[1::4] = -1
+        board, glob = env.encode(idx)
+        b, g = board.cpu().numpy(), glob.cpu().numpy()
+        for k in range(m):
+            j = int(idx[k])
+            if j < 0:
+                assert not b[k].any() and not g[k].any(), (m, k)
+            else:
+                assert (b[k] == f["boards"][j]).all() and (g[k] == f["globs"][j]).all(), (m, k)
+
+
+def test_play_partial_blocks(Env):
+    """100 boards (a partial 64-board block in every role of the launch):
+    three consecutive hz_play calls, each bit-exact vs the oracle's episode."""
+    n, base = 100, 9
+    env = Env(n, seed_base=base, device=DEV)
+    for ep in range(3):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+
+
 def test_encoder_game_over_states(Env):
     f = load("env_finals.npz")
     refs = f["finals"][:128]
