@@ -562,24 +562,50 @@ __device__ __forceinline__ void sample3_raw(M& m, uint32_t n, int k, uint32_t j[
   sample3_serial(m, n, k, j, 0);
 }
 
-// LDS stream: branch-free scan of the next 24 twisted words (the wave leaves
-// early once every lane has its picks; a lane needs more than 24 words with
-// probability ~1e-5 and then finishes serially).  The words are read twelve
-// ahead, four more per step of four, at immediate offsets from the lane's
-// cursor row (Clamp: near the end of a generation, rows clamped to 623; the
-// rows past tw are never live).  Unset picks hold a sentinel no value < n
-// equals, so the distinctness test needs no pick count.
+// LDS stream: branch-free scan of the next <= 24 twisted words (the wave
+// leaves early once every lane has its picks; a lane needs more than 24
+// words with probability ~1e-5 and then finishes serially).  The words are
+// read a step ahead at immediate offsets from the lane's cursor row (Clamp:
+// near the end of a generation, rows clamped to 623; the rows past tw are
+// never live).  The reads are volatile so that the compiler issues them
+// where they are written, ahead of the branch that may leave the scan,
+// instead of sinking them to their first use.
+typedef __attribute__((address_space(3))) const volatile uint32_t LdsVolatileWord;
 template <bool Clamp>
 __device__ __forceinline__ uint32_t scan_word(const LdsMT& m, int t) {
+  LdsVolatileWord* lds = (LdsVolatileWord*)hz_lds;
   if (Clamp) {
     int i = m.pos + t < kMT ? m.pos + t : kMT - 1;
-    return hz_lds[i * kLdsStride + m.lane];
+    return lds[i * kLdsStride + m.lane];
   }
-  return hz_lds[(m.pos + t) * kLdsStride + m.lane];
+  return lds[(m.pos + t) * kLdsStride + m.lane];
 }
 
 // the top 14 bits of temper(y): its last step (y ^= y >> 18) leaves them
-// unchanged; every draw keeps at most 7 (the bag never exceeds 120 tiles)
+// unchanged; every draw keeps at most 7 (the bag never exceeds 120 tiles).
+// With the masks held in SGPRs each "y ^= (y << s) & mask" is a shift and
+// one v_bitop3 (a VOP3 op on gfx950 takes no literal).
+__device__ __forceinline__ uint32_t sgpr_const(uint32_t v) {
+  uint32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(v));
+  return r;
+}
+struct TemperMasks {
+  uint32_t b, c;
+  __device__ __forceinline__ TemperMasks() : b(sgpr_const(0x9d2c5680u)), c(sgpr_const(0xefc60000u)) {}
+};
+// (x & m) ^ y in one instruction
+__device__ __forceinline__ uint32_t and_xor(uint32_t x, uint32_t m, uint32_t y) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(x), "s"(m), "v"(y));
+  return r;
+}
+__device__ __forceinline__ uint32_t temper_top14(uint32_t y, const TemperMasks& k) {
+  y ^= y >> 11;
+  y = and_xor(y << 7, k.b, y);
+  y = and_xor(y << 15, k.c, y);
+  return y;
+}
 __device__ __forceinline__ uint32_t temper_top14(uint32_t y) {
   y ^= y >> 11;
   y ^= (y << 7) & 0x9d2c5680u;
@@ -587,54 +613,79 @@ __device__ __forceinline__ uint32_t temper_top14(uint32_t y) {
   return y;
 }
 
-template <bool Clamp, bool Set>
-__device__ __forceinline__ void scan24(const LdsMT& m, uint32_t n, int k, uint32_t& j0, uint32_t& j1,
-                                       uint32_t& j2, int& got, int& used) {
+// Three picks (k = 3, the only size a full bag draws) by a scan of the next
+// <= 24 words in steps of four, the next step's words read while this one's
+// are tested.  Kept values shift through j0 <- j1 <- j2 (j0 the newest), so
+// a word costs one mask for all three selects.  Set method (Pool = false,
+// n > 21): a value is kept when < n and unlike the two kept before it.  Pool
+// method (n <= 21): pick i keeps a value < n - i, read with bit_length(n - i)
+// bits.  Returns the picks in draw order in p0, p1, p2 and the count made;
+// fewer than three when the window ran out (rare; serial continuation).
+template <bool Clamp, bool Pool>
+__device__ __forceinline__ int scan3(LdsMT& m, uint32_t n, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
   int avail = m.tw - m.pos;
-  bool pool = !Set && n <= 21;
-  int sh0 = __clz(n), sh1 = __clz(n > 1 ? n - 1 : 1), sh2 = __clz(n > 2 ? n - 2 : 1);
-  // three segments of eight words; each segment's words are read together
-  // (one LDS wait), the wave stops after a segment once every lane is done
+  uint32_t lim = n;
+  int sh = __clz(n);
+  uint32_t j0 = 0xffffffffu, j1 = 0xffffffffu, j2 = 0xffffffffu;
+  int got = 0, used = 0;
+  TemperMasks tk;
+  uint32_t w[4], nx[4];
 #pragma unroll
-  for (int seg = 0; seg < 3; seg++) {
-    if (seg > 0 && __all(got >= k)) break;
-    uint32_t w[8];
+  for (int u = 0; u < 4; u++) nx[u] = scan_word<Clamp>(m, u);
 #pragma unroll
-    for (int u = 0; u < 8; u++) w[u] = scan_word<Clamp>(m, 8 * seg + u);
+  for (int seg = 0; seg < 6; seg++) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      int t = 8 * seg + u;
-      bool lv = (t < avail) & (got < k);
-      uint32_t v, lim;
-      if (Set) {
-        v = temper_top14(w[u]) >> sh0;  // getrandbits(bit_length(n)), n <= 120
-        lim = n;
-      } else {
-        int sh = pool ? (got == 0 ? sh0 : got == 1 ? sh1 : sh2) : sh0;
-        v = temper_top14(w[u]) >> sh;
-        lim = pool ? n - (uint32_t)got : n;
-      }
-      bool ok = lv & (v < lim) & (pool | ((v != j0) & (v != j1)));  // set method: distinct values
-      j0 = (ok & (got == 0)) ? v : j0;
-      j1 = (ok & (got == 1)) ? v : j1;
-      j2 = (ok & (got == 2)) ? v : j2;
-      used += lv ? 1 : 0;
-      got += ok ? 1 : 0;
+    for (int u = 0; u < 4; u++) w[u] = nx[u];
+    if (seg < 5) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) nx[u] = scan_word<Clamp>(m, 4 * seg + 4 + u);
     }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int t = 4 * seg + u;
+      bool live = got < 3;
+      if (Clamp) live = live && t < avail;
+      uint32_t v = temper_top14(w[u], tk) >> sh;
+      bool ok = live && v < lim;
+      if (!Pool) ok = ok && v != j0 && v != j1;
+      j2 = ok ? j1 : j2;
+      j1 = ok ? j0 : j1;
+      j0 = ok ? v : j0;
+      got += ok ? 1 : 0;
+      used += live ? 1 : 0;
+      if (Pool) {
+        lim -= ok ? 1u : 0u;
+        sh = __clz(lim);
+      }
+    }
+    if (__all(got >= 3)) break;
   }
+  m.pos += used;
+  // newest first -> draw order
+  p0 = got == 3 ? j2 : got == 2 ? j1 : j0;
+  p1 = got == 3 ? j1 : j0;
+  p2 = j0;
+  return got;
 }
 
 __device__ __forceinline__ void sample3_raw(LdsMT& m, uint32_t n, int k, uint32_t j[3]) {
-  uint32_t j0 = 0xffffffffu, j1 = 0xffffffffu, j2 = 0;
-  int got = 0, used = 0;
+  if (k != 3) {  // fewer than three tiles left: only after the bag's count stopped being a multiple of 3
+    sample3_serial(m, n, k, j, 0);
+    return;
+  }
+  uint32_t j0, j1, j2;
+  int got;
   bool far = __any(m.pos > kMT - 24);
   if (__all(n > 21)) {
-    if (far) scan24<true, true>(m, n, k, j0, j1, j2, got, used);
-    else scan24<false, true>(m, n, k, j0, j1, j2, got, used);
-  } else {
-    scan24<true, false>(m, n, k, j0, j1, j2, got, used);
+    if (far) got = scan3<true, false>(m, n, j0, j1, j2);
+    else got = scan3<false, false>(m, n, j0, j1, j2);
+  } else if (__all(n <= 21)) {
+    if (far) got = scan3<true, true>(m, n, j0, j1, j2);
+    else got = scan3<false, true>(m, n, j0, j1, j2);
+  } else {  // a wave whose bags differ in method (boards out of lockstep)
+    if (n > 21) got = scan3<true, false>(m, n, j0, j1, j2);
+    else got = scan3<true, true>(m, n, j0, j1, j2);
   }
-  m.pos += used;
   j[0] = j0; j[1] = j1; j[2] = j2;
   if (got < k) sample3_serial(m, n, k, j, got);  // window exhausted (rare)
 }
@@ -1146,6 +1197,168 @@ __device__ __forceinline__ int rule_pick_k(uint64_t key, int ply, int n_legal) {
 }
 __device__ __forceinline__ int rule_pick(uint64_t seed, int ply, int n_legal) {
   return rule_pick_k(rule_key(seed), ply, n_legal);
+}
+
+// ------------------------------------------------ turn-structured rollout
+// Every turn is exactly four plies: choose a pile (always three tiles: the
+// bag starts at 120 and every draw takes three), then place the three
+// (harmonies_engine.py:210-298); the turn ends after place_tile_3.  Boards
+// started together therefore move in lockstep: within a turn the phase, and
+// across a pair of turns the player, are compile-time constants, so a
+// placement works on the mover's 32-bit plane halves directly and the hand
+// lives in a register until the turn ends.  turn_pair_safe() admits a board
+// only when both turns of the pair are sure to complete their four plies.
+template <int P>
+__device__ __forceinline__ uint32_t half(uint64_t w) {
+  return P ? (uint32_t)(w >> 32) : (uint32_t)w;
+}
+template <int P>
+__device__ __forceinline__ uint64_t with_half(uint64_t w, uint32_t v) {
+  return P ? (w & 0xFFFFFFFFull) | ((uint64_t)v << 32) : (w & 0xFFFFFFFF00000000ull) | (uint64_t)v;
+}
+
+// player 0 to choose a pile, game running, >= 1 pile and every pile full,
+// bag a multiple of three (so every later pile is full), and three empty
+// cells on each board (so each placement has a legal cell).  All of it holds
+// for every reachable state at a pair boundary.
+__device__ __forceinline__ bool turn_pair_safe(const State& s) {
+  uint64_t m = s.misc;
+  bool ok = (m & ((1ull << 41) | (7ull << 42) | (1ull << 45))) == 0;  // player 0, choose_pile, not over
+  int np = npiles_of(s.piles);
+  uint64_t p = s.piles;
+  uint64_t absent = p & (p >> 1) & (p >> 2) & 0x1249249249249ull & ((1ull << (9 * np)) - 1);  // a slot == 7
+  ok = ok && np >= 1 && absent == 0;
+  int bag = bag_total(m);
+  ok = ok && bag % 3 == 0;
+  uint64_t occ = s.pl[0] | s.pl[1] | s.pl[2] | s.pl[3];
+  ok = ok && __popc((uint32_t)occ) <= kCells - 3 && __popc((uint32_t)(occ >> 32)) <= kCells - 3;
+  return ok;
+}
+
+// legal cells for tile t: an empty cell, or plant on wood, stone on one or two
+// stones, building on wood / stone / building (harmonies_engine.py:183-194)
+struct PlaceMasks {
+  uint32_t empty, xplant, xstone, xbldg;
+  __device__ __forceinline__ uint32_t of(uint32_t t) const {
+    uint32_t m = empty;
+    m |= t == PLANT ? xplant : 0u;
+    m |= t == STONE ? xstone : 0u;
+    m |= t == BUILDING ? xbldg : 0u;
+    return m;
+  }
+};
+
+__device__ __forceinline__ PlaceMasks place_masks(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  PlaceMasks r;
+  uint32_t o01 = b0 | b1;
+  r.empty = ~(o01 | b2 | b3) & kAll23;
+  uint32_t wood1 = b0 & b1 & ~(b2 | b3);       // code 3
+  uint32_t stone1 = b2 & ~(o01 | b3);          // code 4
+  uint32_t stone2 = b3 & ~(o01 | b2);          // code 8
+  uint32_t bld1 = b0 & b2 & ~(b1 | b3);        // code 5
+  r.xplant = wood1;
+  r.xstone = stone1 | stone2;
+  r.xbldg = wood1 | stone1 | bld1;
+  return r;
+}
+
+// One placement ply of player P with NH tiles in hand (hand9: NH 3-bit tiles
+// in hand order): the rule's action is the k-th legal move, k = (h * L) >> 32,
+// in ascending action order = tile-major over the hand's distinct tiles
+// (get_action_index, process_game_state.py:156-179), then the placement and
+// hand.remove(tile) of apply_move (:244-276).
+template <int P, int NH>
+__device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h) {
+  uint32_t b0 = half<P>(s.pl[0]), b1 = half<P>(s.pl[1]), b2 = half<P>(s.pl[2]), b3 = half<P>(s.pl[3]);
+  PlaceMasks pm = place_masks(b0, b1, b2, b3);
+  uint32_t t0 = hand9 & 7u, t1 = (hand9 >> 3) & 7u, t2 = (hand9 >> 6) & 7u;
+  uint32_t tile, m;
+  int idx;
+  if constexpr (NH == 1) {
+    m = pm.of(t0);
+    idx = (int)(((uint64_t)h * (uint32_t)__popc(m)) >> 32);
+    tile = t0;
+  } else if constexpr (NH == 2) {
+    uint32_t lo = t0 < t1 ? t0 : t1, hi = t0 < t1 ? t1 : t0;
+    uint32_t mlo = pm.of(lo), mhi = pm.of(hi);
+    int c0 = __popc(mlo), c1 = hi != lo ? __popc(mhi) : 0;
+    int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1)) >> 32);
+    bool up = k >= c0;
+    tile = up ? hi : lo;
+    m = up ? mhi : mlo;
+    idx = up ? k - c0 : k;
+  } else {
+    uint32_t u0 = t0, u1 = t1, u2 = t2;
+    sort3(u0, u1, u2);
+    uint32_t m0 = pm.of(u0), m1 = pm.of(u1), m2 = pm.of(u2);
+    int c0 = __popc(m0), c1 = u1 != u0 ? __popc(m1) : 0, c2 = u2 != u1 ? __popc(m2) : 0;
+    int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1 + c2)) >> 32);
+    bool up1 = k >= c0, up2 = k >= c0 + c1;
+    tile = up2 ? u2 : up1 ? u1 : u0;
+    m = up2 ? m2 : up1 ? m1 : m0;
+    idx = up2 ? k - c0 - c1 : up1 ? k - c0 : k;
+  }
+  int c = select32(m, idx);
+  // place_code for a legal placement (see step_trusted)
+  uint32_t code = ((b0 >> c) & 1u) | (((b1 >> c) & 1u) << 1) | (((b2 >> c) & 1u) << 2) | (((b3 >> c) & 1u) << 3);
+  uint32_t nc = tile == PLANT ? 7u : tile == STONE ? (code == 4u ? 8u : 9u) : code + 7u;
+  nc = code == 0u ? 1u + tile : nc;
+  uint32_t d = code ^ nc;
+  b0 ^= (d & 1u) << c;
+  b1 ^= ((d >> 1) & 1u) << c;
+  b2 ^= ((d >> 2) & 1u) << c;
+  b3 ^= ((d >> 3) & 1u) << c;
+  s.pl[0] = with_half<P>(s.pl[0], b0);
+  s.pl[1] = with_half<P>(s.pl[1], b1);
+  s.pl[2] = with_half<P>(s.pl[2], b2);
+  s.pl[3] = with_half<P>(s.pl[3], b3);
+  // hand.remove(tile): the first entry equal to it, the rest keep their order
+  if constexpr (NH == 2) {
+    hand9 = t0 == tile ? t1 : t0;
+  } else if constexpr (NH == 3) {
+    hand9 = t0 == tile ? (t1 | (t2 << 3)) : t1 == tile ? (t0 | (t2 << 3)) : (t0 | (t1 << 3));
+  }
+}
+
+// _end_turn_actions (:301-329) for player P after a full turn (hand empty)
+template <int P, class Draw>
+__device__ __forceinline__ void end_turn_fast(State& s, Draw& draw) {
+  uint32_t occ = half<P>(s.pl[0] | s.pl[1] | s.pl[2] | s.pl[3]);
+  bool player_trigger = __popc(occ) >= kCells - 2;
+  bool bag_empty_before = (s.misc & (((1ull << 30) - 1) << 11)) == 0;
+  replenish(s, draw);
+  bool bag_trigger = bag_empty_before && npiles_of(s.piles) == 0;
+  bool end = player_trigger || bag_trigger;
+  uint64_t m = s.misc;
+  bool over = over_flag(m);
+  // next: the other player chooses; P0's trigger sets game_over and gives
+  // P1 its last turn; P1's trigger (or a turn after game_over) ends the game
+  bool fin = P ? (end || over) : over;
+  bool flag = end && !over;
+  m = (m & ~((1ull << 41) | (7ull << 42))) | ((uint64_t)(1 - P) << 41);  // player switch, choose_pile
+  m |= flag ? (1ull << 45) : 0ull;
+  m = fin ? (m & ~(1ull << 41)) | ((uint64_t)P << 41) | ((uint64_t)PH_OVER << 42) : m;  // mark_over, player kept
+  s.misc = m;
+}
+
+// One whole turn of player P (the rule policy at plies g_ply .. g_ply + 3).
+template <int P, class Draw>
+__device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, int g_ply) {
+  uint32_t hand9;
+  {  // choose_pile: the pile leaves the row, later piles shift down (:221)
+    uint32_t h = rule_h32(rkey, g_ply);
+    int np = npiles_of(s.piles);
+    int a = (int)(((uint64_t)h * (uint32_t)np) >> 32);
+    hand9 = (uint32_t)(s.piles >> (9 * a)) & 0x1FF;
+    uint64_t lower = s.piles & ((1ull << (9 * a)) - 1);
+    uint64_t upper = (s.piles & ((1ull << 45) - 1)) >> (9 * (a + 1));
+    s.piles = lower | (upper << (9 * a)) | (0x1FFull << 36) | ((uint64_t)(np - 1) << 45);
+  }
+  place_fast<P, 3>(s, hand9, rule_h32(rkey, g_ply + 1));
+  place_fast<P, 2>(s, hand9, rule_h32(rkey, g_ply + 2));
+  place_fast<P, 1>(s, hand9, rule_h32(rkey, g_ply + 3));
+  s.misc = (s.misc & ~0x7FFull) | 0x1FFull;  // empty hand
+  end_turn_fast<P>(s, draw);
 }
 
 // ------------------------------------------------------------ SoA access

@@ -65,9 +65,19 @@ __device__ uint64_t *g_stamps;
   do {                   \
   } while (0)
 #endif
+// phase boundary inside a preparation role: cycles since the role began
+#define HZ_PHASE(slot, t0, b)                                                                 \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (g_stamps) g_stamps[(size_t)(b) * 16 + (slot)] = __builtin_amdgcn_s_memtime() - (t0); \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
 #else
 #define HZ_STAMP(slot) \
   do {                 \
+  } while (0)
+#define HZ_PHASE(slot, t0, b) \
+  do {                        \
   } while (0)
 #define HZ_ACC(slot, t0) \
   do {                   \
@@ -276,6 +286,38 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
 constexpr int kAheadDraws = 24;             // 5 opening + 19 turn ends (rule games: at most 23)
 constexpr int kAheadWords = (9 * kAheadDraws + 63) / 64;  // 4 u64: the piles, 9 bits each
 
+// The draws that do not come from the script (boards not prepared ahead, and
+// a script's rare overrun) live out of line: one copy of the sampling code
+// instead of one per refill site keeps the ply loop's code small.  State
+// goes in and out by value so the caller's copy stays in registers.
+struct SlowDrawOut {
+  uint32_t p9;
+  int mpos, mtw, gpos, gtw;
+};
+
+__device__ __noinline__ SlowDrawOut play_draw_slow(uint64_t misc, int lane, int mpos, int mtw, int scripted,
+                                                    uint32_t *gw, int gcursor) {
+  SlowDrawOut o;
+  uint32_t p9;
+  if (scripted) {
+    MT gm(gw, gcursor);
+    o.p9 = draw_pile(misc, gm, p9) ? p9 : 0x1FFu;
+    o.mpos = mpos;
+    o.mtw = mtw;
+    o.gpos = gm.pos;
+    o.gtw = gm.tw;
+  } else {
+    LdsMT m(lane, mpos | (mtw << 16));
+    m.prefetch();
+    o.p9 = draw_pile(misc, m, p9) ? p9 : 0x1FFu;
+    o.mpos = m.pos;
+    o.mtw = m.tw;
+    o.gpos = gcursor & 0xFFFF;
+    o.gtw = gcursor >> 16;
+  }
+  return o;
+}
+
 struct PlayDraw {
   LdsMT m;                 // stream in LDS (boards not prepared ahead, auto-reset games)
   bool scripted;           // replaying the prepared pile script
@@ -287,28 +329,27 @@ struct PlayDraw {
   const int32_t *cur_tail; // cursor after the last scripted draw (global)
 
   __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
-    if (scripted) {
-      if (d < nd) {
-        // pop the next 9-bit entry: a shift queue (a select over the four
-        // words would become a dynamic index into a scratch copy)
-        uint32_t p9 = (uint32_t)q0 & 0x1FFu;
-        q0 = (q0 >> 9) | (q1 << 55);
-        q1 = (q1 >> 9) | (q2 << 55);
-        q2 = (q2 >> 9) | (q3 << 55);
-        q3 >>= 9;
-        d++;
-        return p9;
-      }
-      if (!fell) {
-        gm = MT(gm.w, *cur_tail);
-        fell = true;
-      }
-      uint32_t p9;
-      return draw_pile(misc, gm, p9) ? p9 : 0x1FFu;
+    if (scripted && d < nd) {
+      // pop the next 9-bit entry: a shift queue (a select over the four
+      // words would become a dynamic index into a scratch copy)
+      uint32_t p9 = (uint32_t)q0 & 0x1FFu;
+      q0 = (q0 >> 9) | (q1 << 55);
+      q1 = (q1 >> 9) | (q2 << 55);
+      q2 = (q2 >> 9) | (q3 << 55);
+      q3 >>= 9;
+      d++;
+      return p9;
     }
-    m.prefetch();  // the one point where the wave's refills line up
-    uint32_t p9;
-    return draw_pile(misc, m, p9) ? p9 : 0x1FFu;
+    if (scripted && !fell) {
+      gm = MT(gm.w, *cur_tail);
+      fell = true;
+    }
+    SlowDrawOut o = play_draw_slow(misc, m.lane, m.pos, m.tw, scripted, gm.w, gm.cursor());
+    m.pos = o.mpos;
+    m.tw = o.mtw;
+    gm.pos = o.gpos;
+    gm.tw = o.gtw;
+    return o.p9;
   }
 };
 
@@ -351,20 +392,27 @@ static_assert(kSeedDraws <= 7 && kSeedDraws <= kAheadDraws, "the seed stage's pi
 
 // run script entries [from, to) of a board's chance sequence on its LDS
 // stream, recording packed piles and the cursor after each draw
+// (a rolled loop: one copy of the sampling code, so the instruction cache
+// holds it; the script word is picked by selects, not by a dynamic index)
 __device__ __forceinline__ void run_script(StreamDraw<LdsMT>& d, uint64_t& bag, uint64_t q[kAheadWords],
                                            int32_t* __restrict__ cur, int n, int b, int from, int to) {
-#pragma unroll
-  for (int i = 0; i < kAheadDraws; i++) {
-    if (i >= from && i < to) {
-      uint32_t p9 = d(bag);
-      if (p9 != 0x1FFu) apply_pile(bag, p9);
-      // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
-      int bit = 9 * i, wd = bit / 64, off = bit % 64;
-      q[wd] |= (uint64_t)p9 << off;
-      if (off > 55) q[wd + 1] |= (uint64_t)p9 >> (64 - off);
-      cur[(size_t)(i + 1) * n + b] = d.m.cursor();
-    }
+  static_assert(kAheadWords == 4, "script words");
+  uint64_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+#pragma unroll 1
+  for (int i = from; i < to; i++) {
+    uint32_t p9 = d(bag);
+    if (p9 != 0x1FFu) apply_pile(bag, p9);
+    // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
+    int bit = 9 * i, wd = bit >> 6, off = bit & 63;
+    uint64_t lo = (uint64_t)p9 << off;
+    uint64_t hi = off > 55 ? (uint64_t)p9 >> (64 - off) : 0ull;
+    q0 |= wd == 0 ? lo : 0ull;
+    q1 |= wd == 1 ? lo : wd == 0 ? hi : 0ull;
+    q2 |= wd == 2 ? lo : wd == 1 ? hi : 0ull;
+    q3 |= wd == 3 ? lo : wd == 2 ? hi : 0ull;
+    cur[(size_t)(i + 1) * n + b] = d.m.cursor();
   }
+  q[0] = q0; q[1] = q1; q[2] = q2; q[3] = q3;
 }
 
 __device__ __forceinline__ uint64_t initial_bag() {
@@ -385,14 +433,20 @@ __device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_m
   bool act = b < n;
   uint64_t actmask = __ballot(act);
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
+#ifdef HZ_DIAG
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
   if (tid < 64 && act) {
     int e = ep_final[b] + 2;
     mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
+    HZ_PHASE(0, t0, b);
     StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
     d.m.twist_ahead(kAheadTwist);  // cursor kMTAhead
+    HZ_PHASE(1, t0, b);
     out_cur[b] = d.m.cursor();
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
     run_script(d, bag, q, out_cur, n, b, 0, draws < kSeedDraws ? draws : kSeedDraws);
+    HZ_PHASE(2, t0, b);
 #pragma unroll
     for (int w = 0; w < kAheadWords; w++) out_pile[(size_t)w * n + b] = q[w];
     out_tag[b] = e;
@@ -415,10 +469,14 @@ __device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__
   uint64_t actmask = __ballot(act);
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
   int e = act ? ep_final[b] + 1 : 0;
+#ifdef HZ_DIAG
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
   bool seeded = act && in_tag && in_tag[b] == e;
   uint64_t seededmask = __ballot(seeded);
   if (seededmask) stage_mt(const_cast<uint32_t *>(in_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
   __syncthreads();
+  if (tid < 64 && act) HZ_PHASE(3, t0, b);
   if (tid < 64 && act) {
     int k0 = draws < kSeedDraws ? draws : kSeedDraws;
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
@@ -445,7 +503,9 @@ __device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__
       start = 0;
     }
     StreamDraw<LdsMT> d{LdsMT(lane, seeded ? in_cur[(size_t)k0 * n + b] : kMTAhead)};
+    HZ_PHASE(4, t0, b);
     run_script(d, bag, q, cur, n, b, start, draws);
+    HZ_PHASE(14, t0, b);
 #pragma unroll
     for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
     tag[b] = e;
@@ -554,6 +614,23 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #endif
     bool lds_used = !seeded;  // the LDS copy of the stream is live
     for (int i = 0; i < max_plies; i++) {
+      if constexpr (!Record) {
+        // a pair of whole turns at once while every board of the wave is at
+        // a pair boundary (always, for boards reset together)
+        if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
+          play_turn<0>(s, draw, rkey, g_ply);
+          int done = 4;
+          if (phase_of(s.misc) != PH_OVER) {
+            play_turn<1>(s, draw, rkey, g_ply + 4);
+            done = 8;
+          }
+          g_ply += done;
+          steps += done;
+          i += done - 1;
+          if (phase_of(s.misc) == PH_OVER) games++;
+          continue;
+        }
+      }
       if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
         if constexpr (!AutoReset) {
           if (Record && traj_action) {
