@@ -1218,49 +1218,29 @@ __device__ __forceinline__ uint64_t with_half(uint64_t w, uint32_t v) {
 }
 
 // player 0 to choose a pile, game running, >= 1 pile and every pile full,
-// bag a multiple of three (so every later pile is full), and three empty
-// cells on each board (so each placement has a legal cell).  All of it holds
-// for every reachable state at a pair boundary.
+// bag a multiple of three (so every later pile is full) and either five
+// piles or an empty bag (so a turn end draws at most one pile), and three
+// empty cells on each board (so each placement has a legal cell).  All of it
+// holds for every reachable state at a pair boundary.
 __device__ __forceinline__ bool turn_pair_safe(const State& s) {
   uint64_t m = s.misc;
   bool ok = (m & ((1ull << 41) | (7ull << 42) | (1ull << 45))) == 0;  // player 0, choose_pile, not over
   int np = npiles_of(s.piles);
   uint64_t p = s.piles;
   uint64_t absent = p & (p >> 1) & (p >> 2) & 0x1249249249249ull & ((1ull << (9 * np)) - 1);  // a slot == 7
-  ok = ok && np >= 1 && absent == 0;
   int bag = bag_total(m);
-  ok = ok && bag % 3 == 0;
+  ok = ok && np >= 1 && absent == 0 && bag % 3 == 0 && (np == 5 || bag == 0);
   uint64_t occ = s.pl[0] | s.pl[1] | s.pl[2] | s.pl[3];
   ok = ok && __popc((uint32_t)occ) <= kCells - 3 && __popc((uint32_t)(occ >> 32)) <= kCells - 3;
   return ok;
 }
 
-// legal cells for tile t: an empty cell, or plant on wood, stone on one or two
-// stones, building on wood / stone / building (harmonies_engine.py:183-194)
-struct PlaceMasks {
-  uint32_t empty, xplant, xstone, xbldg;
-  __device__ __forceinline__ uint32_t of(uint32_t t) const {
-    uint32_t m = empty;
-    m |= t == PLANT ? xplant : 0u;
-    m |= t == STONE ? xstone : 0u;
-    m |= t == BUILDING ? xbldg : 0u;
-    return m;
-  }
-};
-
-__device__ __forceinline__ PlaceMasks place_masks(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
-  PlaceMasks r;
-  uint32_t o01 = b0 | b1;
-  r.empty = ~(o01 | b2 | b3) & kAll23;
-  uint32_t wood1 = b0 & b1 & ~(b2 | b3);       // code 3
-  uint32_t stone1 = b2 & ~(o01 | b3);          // code 4
-  uint32_t stone2 = b3 & ~(o01 | b2);          // code 8
-  uint32_t bld1 = b0 & b2 & ~(b1 | b3);        // code 5
-  r.xplant = wood1;
-  r.xstone = stone1 | stone2;
-  r.xbldg = wood1 | stone1 | bld1;
-  return r;
-}
+// Legal cells by tile class (harmonies_engine.py:183-194): water, wood and
+// field go on an empty cell (class 0); plant also on wood (1); stone also on
+// one or two stones (2); building also on wood, stone or building (3).
+// kTileClass5: the class of tile t times 8 in bits 5t..5t+4.
+constexpr uint32_t kTileClass5 = (0u << 0) | (8u << 5) | (0u << 10) | (16u << 15) | (24u << 20) | (0u << 25);
+__device__ __forceinline__ uint32_t class_off(uint32_t t) { return __builtin_amdgcn_ubfe(kTileClass5, 5 * t, 5); }
 
 // One placement ply of player P with NH tiles in hand (hand9: NH 3-bit tiles
 // in hand order): the rule's action is the k-th legal move, k = (h * L) >> 32,
@@ -1270,44 +1250,57 @@ __device__ __forceinline__ PlaceMasks place_masks(uint32_t b0, uint32_t b1, uint
 template <int P, int NH>
 __device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h) {
   uint32_t b0 = half<P>(s.pl[0]), b1 = half<P>(s.pl[1]), b2 = half<P>(s.pl[2]), b3 = half<P>(s.pl[3]);
-  PlaceMasks pm = place_masks(b0, b1, b2, b3);
+  uint32_t o01 = b0 | b1, o23 = b2 | b3;
+  uint32_t mE = ~(o01 | o23) & kAll23;
+  uint32_t wood1 = b0 & b1 & ~o23;             // code 3
+  uint32_t stone1 = b2 & ~(o01 | b3);          // code 4
+  uint32_t stone2 = b3 & ~(o01 | b2);          // code 8
+  uint32_t bld1 = b0 & b2 & ~(b1 | b3);        // code 5
+  uint32_t mP = mE | wood1, mS = mE | stone1 | stone2, mB = mP | stone1 | bld1;
+  // legal-cell counts of the four classes, one byte each
+  uint32_t cw = (uint32_t)__popc(mE) | ((uint32_t)__popc(mP) << 8) | ((uint32_t)__popc(mS) << 16) |
+                ((uint32_t)__popc(mB) << 24);
   uint32_t t0 = hand9 & 7u, t1 = (hand9 >> 3) & 7u, t2 = (hand9 >> 6) & 7u;
-  uint32_t tile, m;
+  uint32_t tile;
   int idx;
   if constexpr (NH == 1) {
-    m = pm.of(t0);
-    idx = (int)(((uint64_t)h * (uint32_t)__popc(m)) >> 32);
+    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(t0), 8);
+    idx = (int)(((uint64_t)h * (uint32_t)c0) >> 32);
     tile = t0;
   } else if constexpr (NH == 2) {
-    uint32_t lo = t0 < t1 ? t0 : t1, hi = t0 < t1 ? t1 : t0;
-    uint32_t mlo = pm.of(lo), mhi = pm.of(hi);
-    int c0 = __popc(mlo), c1 = hi != lo ? __popc(mhi) : 0;
+    uint32_t lo = min(t0, t1), hi = max(t0, t1);
+    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(lo), 8);
+    int c1 = hi != lo ? (int)__builtin_amdgcn_ubfe(cw, class_off(hi), 8) : 0;
     int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1)) >> 32);
     bool up = k >= c0;
     tile = up ? hi : lo;
-    m = up ? mhi : mlo;
     idx = up ? k - c0 : k;
   } else {
     uint32_t u0 = t0, u1 = t1, u2 = t2;
     sort3(u0, u1, u2);
-    uint32_t m0 = pm.of(u0), m1 = pm.of(u1), m2 = pm.of(u2);
-    int c0 = __popc(m0), c1 = u1 != u0 ? __popc(m1) : 0, c2 = u2 != u1 ? __popc(m2) : 0;
+    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(u0), 8);
+    int c1 = u1 != u0 ? (int)__builtin_amdgcn_ubfe(cw, class_off(u1), 8) : 0;
+    int c2 = u2 != u1 ? (int)__builtin_amdgcn_ubfe(cw, class_off(u2), 8) : 0;
     int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1 + c2)) >> 32);
     bool up1 = k >= c0, up2 = k >= c0 + c1;
     tile = up2 ? u2 : up1 ? u1 : u0;
-    m = up2 ? m2 : up1 ? m1 : m0;
     idx = up2 ? k - c0 - c1 : up1 ? k - c0 : k;
   }
+  uint32_t off = class_off(tile);
+  uint32_t m = off == 0 ? mE : off == 8 ? mP : off == 16 ? mS : mB;
   int c = select32(m, idx);
-  // place_code for a legal placement (see step_trusted)
-  uint32_t code = ((b0 >> c) & 1u) | (((b1 >> c) & 1u) << 1) | (((b2 >> c) & 1u) << 2) | (((b3 >> c) & 1u) << 3);
-  uint32_t nc = tile == PLANT ? 7u : tile == STONE ? (code == 4u ? 8u : 9u) : code + 7u;
-  nc = code == 0u ? 1u + tile : nc;
+  // place_code for a legal placement (see step_trusted): empty -> 1 + t;
+  // plant on wood 3 -> 7; stone on 4 -> 8, on 8 -> 9; building on 3/4/5 -> +7
+  uint32_t code = __builtin_amdgcn_ubfe(b0, c, 1) | (__builtin_amdgcn_ubfe(b1, c, 1) << 1) |
+                  (__builtin_amdgcn_ubfe(b2, c, 1) << 2) | (__builtin_amdgcn_ubfe(b3, c, 1) << 3);
+  uint32_t add = tile == BUILDING ? 7u : (tile == PLANT || code == 4u) ? 4u : 1u;
+  uint32_t nc = code == 0u ? 1u + tile : code + add;
   uint32_t d = code ^ nc;
-  b0 ^= (d & 1u) << c;
-  b1 ^= ((d >> 1) & 1u) << c;
-  b2 ^= ((d >> 2) & 1u) << c;
-  b3 ^= ((d >> 3) & 1u) << c;
+  uint32_t bit = 1u << c;
+  b0 ^= (d & 1u) ? bit : 0u;
+  b1 ^= (d & 2u) ? bit : 0u;
+  b2 ^= (d & 4u) ? bit : 0u;
+  b3 ^= (d & 8u) ? bit : 0u;
   s.pl[0] = with_half<P>(s.pl[0], b0);
   s.pl[1] = with_half<P>(s.pl[1], b1);
   s.pl[2] = with_half<P>(s.pl[2], b2);
@@ -1320,16 +1313,25 @@ __device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h
   }
 }
 
-// _end_turn_actions (:301-329) for player P after a full turn (hand empty)
+// _end_turn_actions (:301-329) for player P after a full turn (hand empty).
+// Under turn_pair_safe the refill is at most one pile: four piles are left
+// unless the bag ran dry at an earlier refill.
 template <int P, class Draw>
 __device__ __forceinline__ void end_turn_fast(State& s, Draw& draw) {
   uint32_t occ = half<P>(s.pl[0] | s.pl[1] | s.pl[2] | s.pl[3]);
   bool player_trigger = __popc(occ) >= kCells - 2;
-  bool bag_empty_before = (s.misc & (((1ull << 30) - 1) << 11)) == 0;
-  replenish(s, draw);
-  bool bag_trigger = bag_empty_before && npiles_of(s.piles) == 0;
-  bool end = player_trigger || bag_trigger;
   uint64_t m = s.misc;
+  bool bag_empty_before = (m & (((1ull << 30) - 1) << 11)) == 0;
+  int np = npiles_of(s.piles);
+  if (np < 5 && !bag_empty_before) {
+    uint32_t pile9 = draw(m);
+    apply_pile(m, pile9);  // a full pile: the bag holds a multiple of three
+    s.piles = (s.piles & ~((0x1FFull << (9 * np)) | (7ull << 45))) | ((uint64_t)pile9 << (9 * np)) |
+              ((uint64_t)(np + 1) << 45);
+    np++;
+  }
+  bool bag_trigger = bag_empty_before && np == 0;
+  bool end = player_trigger || bag_trigger;
   bool over = over_flag(m);
   // next: the other player chooses; P0's trigger sets game_over and gives
   // P1 its last turn; P1's trigger (or a turn after game_over) ends the game
@@ -1342,11 +1344,17 @@ __device__ __forceinline__ void end_turn_fast(State& s, Draw& draw) {
 }
 
 // One whole turn of player P (the rule policy at plies g_ply .. g_ply + 3).
-template <int P, class Draw>
+// (CheapRule: a multiplicative stand-in for the rule hash, for the
+// microbenchmarks in tools/ only.)
+template <int P, bool CheapRule = false>
+__device__ __forceinline__ uint32_t turn_rule(uint64_t rkey, int ply) {
+  return CheapRule ? ((uint32_t)rkey + (uint32_t)ply) * 0x9E3779B9u : rule_h32(rkey, ply);
+}
+template <int P, class Draw, bool CheapRule = false>
 __device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, int g_ply) {
   uint32_t hand9;
   {  // choose_pile: the pile leaves the row, later piles shift down (:221)
-    uint32_t h = rule_h32(rkey, g_ply);
+    uint32_t h = turn_rule<P, CheapRule>(rkey, g_ply);
     int np = npiles_of(s.piles);
     int a = (int)(((uint64_t)h * (uint32_t)np) >> 32);
     hand9 = (uint32_t)(s.piles >> (9 * a)) & 0x1FF;
@@ -1354,9 +1362,9 @@ __device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, i
     uint64_t upper = (s.piles & ((1ull << 45) - 1)) >> (9 * (a + 1));
     s.piles = lower | (upper << (9 * a)) | (0x1FFull << 36) | ((uint64_t)(np - 1) << 45);
   }
-  place_fast<P, 3>(s, hand9, rule_h32(rkey, g_ply + 1));
-  place_fast<P, 2>(s, hand9, rule_h32(rkey, g_ply + 2));
-  place_fast<P, 1>(s, hand9, rule_h32(rkey, g_ply + 3));
+  place_fast<P, 3>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 1));
+  place_fast<P, 2>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 2));
+  place_fast<P, 1>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 3));
   s.misc = (s.misc & ~0x7FFull) | 0x1FFull;  // empty hand
   end_turn_fast<P>(s, draw);
 }

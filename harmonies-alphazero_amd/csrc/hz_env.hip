@@ -354,19 +354,21 @@ struct PlayDraw {
 };
 
 // copy the streams of boards in `mask` from `src` to `dst` (both board-major
-// spans of nb x 624 words), threads [t0, t0 + nt) of the block
+// spans of nb x 624 words), threads [t0, t0 + nt) of the block; eight 16-B
+// loads in flight per thread
 __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int nb,
                                              int t, int nt, uint64_t mask) {
+  constexpr int U = 8;
   int total4 = nb * (kMT / 4);
-  for (int q0 = 0; q0 < total4; q0 += nt * 4) {
-    uint4 v[4];
+  for (int q0 = 0; q0 < total4; q0 += nt * U) {
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {  // unconditional (clamped) loads: the values stay in registers
+    for (int u = 0; u < U; u++) {  // unconditional (clamped) loads: the values stay in registers
       int q = q0 + u * nt + t;
       v[u] = reinterpret_cast<const uint4 *>(src)[q < total4 ? q : total4 - 1];
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       int q = q0 + u * nt + t;
       if (q < total4 && ((mask >> ((q * 4) / kMT)) & 1)) reinterpret_cast<uint4 *>(dst)[q] = v[u];
     }
@@ -614,23 +616,6 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #endif
     bool lds_used = !seeded;  // the LDS copy of the stream is live
     for (int i = 0; i < max_plies; i++) {
-      if constexpr (!Record) {
-        // a pair of whole turns at once while every board of the wave is at
-        // a pair boundary (always, for boards reset together)
-        if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
-          play_turn<0>(s, draw, rkey, g_ply);
-          int done = 4;
-          if (phase_of(s.misc) != PH_OVER) {
-            play_turn<1>(s, draw, rkey, g_ply + 4);
-            done = 8;
-          }
-          g_ply += done;
-          steps += done;
-          i += done - 1;
-          if (phase_of(s.misc) == PH_OVER) games++;
-          continue;
-        }
-      }
       if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
         if constexpr (!AutoReset) {
           if (Record && traj_action) {
@@ -649,6 +634,23 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         lds_used = true;
         reset_state(s, draw);
         g_ply = 0;
+      }
+      if constexpr (!Record) {
+        // a pair of whole turns at once while every board of the wave still
+        // playing is at a pair boundary (always, for boards reset together)
+        if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
+          play_turn<0>(s, draw, rkey, g_ply);
+          int done = 4;
+          if (phase_of(s.misc) != PH_OVER) {
+            play_turn<1>(s, draw, rkey, g_ply + 4);
+            done = 8;
+          }
+          g_ply += done;
+          steps += done;
+          i += done - 1;
+          if (phase_of(s.misc) == PH_OVER) games++;
+          continue;
+        }
       }
       int a;
       HZ_ACC(8, t0);

@@ -148,3 +148,62 @@ extern "C" int micro_draws_lds(void *mt, int n, int reps, void *sink, void *cyc,
                      reps, (uint32_t *)sink, (uint64_t *)cyc, mode);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// Turn-structured play in isolation (k_rollout's fast path): pairs of turns
+// from a reset state, the piles coming from a fixed cyclic script, restarted
+// when the game ends.  mode 0: as in k_rollout; 1: rule hash replaced by a
+// multiply (hash cost); 2: no end-of-turn refill draw (draw cost).
+struct CycleDraw {
+  uint32_t k;
+  __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
+    if (bag_total(misc) < 3) return 0x1FFu;
+    // three tiles the bag still holds, cycling through the types
+    uint32_t p9 = 0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      uint32_t t = (k + i) % 6;
+#pragma unroll
+      for (int s = 0; s < 6; s++) {
+        uint32_t tt = (k + i + s) % 6;
+        t = bag_n(misc, (int)t) > i ? t : tt;
+      }
+      p9 |= t << (3 * i);
+    }
+    k++;
+    return p9;
+  }
+};
+
+template <int Mode>
+__global__ void __launch_bounds__(64) k_turns(int n, int pairs, uint32_t *sink, uint64_t *cyc) {
+  int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
+  CycleDraw d{(uint32_t)b};
+  State s0;
+  reset_state(s0, d);
+  State s = s0;
+  uint64_t rkey = rule_key((uint64_t)b);
+  int g = 0;
+  uint32_t acc = 0;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < pairs; r++) {
+    if (phase_of(s.misc) == PH_OVER) {
+      acc += (uint32_t)s.pl[0];
+      s = s0;
+      g = 0;
+    }
+    play_turn<0, CycleDraw, Mode == 1>(s, d, rkey, g);
+    if (phase_of(s.misc) != PH_OVER) play_turn<1, CycleDraw, Mode == 1>(s, d, rkey, g + 4);
+    g += 8;
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  sink[b] = acc + (uint32_t)s.pl[1];
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+extern "C" int micro_turns(int mode, int n, int pairs, void *sink, void *cyc, void *stream) {
+  dim3 g((n + 63) / 64), blk(64);
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == 0) hipLaunchKernelGGL(k_turns<0>, g, blk, 0, st, n, pairs, (uint32_t *)sink, (uint64_t *)cyc);
+  if (mode == 1) hipLaunchKernelGGL(k_turns<1>, g, blk, 0, st, n, pairs, (uint32_t *)sink, (uint64_t *)cyc);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

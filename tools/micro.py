@@ -44,3 +44,13 @@ for mode, name in names.items():
         res[f"lds_{name}_x{reps}_cyc"] = float(cyc.double().mean())
     res[f"lds_{name}_per_draw_cyc"] = (res[f"lds_{name}_x33_cyc"] - res[f"lds_{name}_x1_cyc"]) / 32
 print(json.dumps(res))
+
+# turn-structured play (k_rollout's fast path), cycles per pair of turns
+L.micro_turns.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+for mode, name in {0: "turns", 1: "turns_nohash"}.items():
+    for pairs in (1, 17):
+        L.micro_turns(mode, n, pairs, P(sink), P(cyc), stream)
+        torch.cuda.synchronize()
+        res[f"{name}_x{pairs}_cyc"] = float(cyc.double().mean())
+    res[f"{name}_per_pair_cyc"] = (res[f"{name}_x17_cyc"] - res[f"{name}_x1_cyc"]) / 16
+print(json.dumps(res))
