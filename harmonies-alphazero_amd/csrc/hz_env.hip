@@ -26,20 +26,22 @@ struct hz_env {
   int32_t *episode;  // [n]
   uint64_t *seed;    // [n]
   // chance-ahead (hz_play): extra blocks of the same launch prepare each
-  // board's next episode into a double-buffered slot while the playing
-  // blocks play the current one (see launch_rollout)
+  // board's next episodes (seed, draw1, draw2 stages; see the stages and
+  // launch_rollout) while the playing blocks play the current one
   int seed_ahead;            // scripted draws prepared per board (0: off; default kAheadDraws)
   uint32_t *ahead_mt[2];     // [n][624] seeded streams
   int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
-  uint32_t *seed_mt[2];      // [n][624] seed slots: streams seeded two calls ahead, first draws run
-  int32_t *seed_tag[2];      // [n] episode each seed slot holds
-  uint64_t *seed_pile[2];    // [kAheadWords][n] their partial scripts
-  int32_t *seed_cur[2];      // [kSeedDraws + 1][n] cursors
-  int calls;                 // hz_play calls since the last prime
-  int primed, slot_valid[2], seed_valid[2];
+  size_t nrow;               // n rounded up to 64: row stride of the ring slots
+  uint32_t *ring_mt[3];      // [624][nrow] word-major streams, three calls / two calls ahead
+  int32_t *ring_tag[3];      // [nrow] episode * 4 + stage done
+  uint64_t *ring_pile[3];    // [3][nrow] draw1's partial scripts
+  int32_t *ring_cur[3];      // [kD1Draws + 1][nrow] cursors
+  int32_t *ring_k1[3];       // [nrow] draws draw1 completed
+  int calls;                 // hz_play calls (ring and play-slot rotation)
+  int primed, slot_valid[2];
 };
 
 #ifdef HZ_DIAG
@@ -375,34 +377,95 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
   }
 }
 
-// Chance-ahead preparation, a two-stage pipeline in the blocks of each
-// hz_play launch beyond the playing ones (on CUs those leave idle):
-//   seed blocks  [2 nblk, 3 nblk): each board's episode two calls ahead (the
-//     episode counter the previous launch left, plus two): the stream seeded
-//     in LDS and pre-twisted, its first kSeedDraws pile draws run, stream,
-//     partial script, cursors and tag written to a seed slot;
-//   draw blocks  [nblk, 2 nblk): each board's next episode (counter plus
-//     one): the seed slot the previous launch wrote staged in (everything
-//     redone in place when its tag disagrees), the remaining draws run, and
-//     stream, script (piles packed 9 bits each), cursor after each draw and
-//     tag written to a play slot.
-// Seeding (two serial 623-step chains) and drawing thus run side by side,
-// each on its own CUs, and neither is on the playing blocks' path;
-// kSeedDraws balances the two stages.
-constexpr int kSeedDraws = 6;
-static_assert(kSeedDraws <= 7 && kSeedDraws <= kAheadDraws, "the seed stage's piles sit in script word 0");
+// Chance-ahead preparation: a three-stage pipeline in the blocks of each
+// hz_play launch beyond the playing ones (4 x 64 blocks of 162 KB LDS: one
+// per CU, every CU of the chip).  Stage k works on each board's episode k
+// calls ahead (the episode counter the previous launch left, plus k):
+//   seed  (k = 3) blocks [3 nblk, 4 nblk): the stream seeded in LDS, then
+//     stored by all four waves to a word-major ring slot, rows
+//     [0, kAheadTwist) twisted on the way (every source still old: no
+//     serial chain);
+//   draw1 (k = 2) blocks [2 nblk, 3 nblk): the slot's twisted rows staged
+//     into LDS, the first kD1Draws pile draws run (a lane stops at a draw
+//     that would twist past the staged rows; the next stage redoes it), the
+//     partial script, cursors and draw count written beside the slot;
+//   draw2 (k = 1) blocks [nblk, 2 nblk): the whole slot staged, the
+//     remaining draws run, and stream (board-major), script, cursors and tag
+//     written to the play slot the next call's playing blocks replay.
+// Each ring slot carries one tag per board, episode * 4 + stage done, so a
+// stage only continues work its predecessor finished for the same
+// episode; otherwise it redoes the earlier stages itself in LDS.  A slot's
+// contents depend only on (board, episode), so a matching tag is always
+// right, whatever happened between the calls.
+constexpr int kD1Draws = 16;
+constexpr int kRing = 3;
+static_assert(kD1Draws <= kAheadDraws && 9 * kD1Draws <= 192, "draw1's script sits in words 0-2");
+
+// one ring slot: the stream word-major (row r of board b at mt[r * nrow + b],
+// nrow = n rounded up to 64, so a wave's row is 256 contiguous bytes), and
+// per board the tag, draw1's script, cursors and draw count
+struct Ring {
+  uint32_t *mt;
+  int32_t *tag;   // [nrow] episode * 4 + stage (1 seeded, 2 draw1 done); -1 none
+  uint64_t *pile; // [kAheadWords][nrow]
+  int32_t *cur;   // [kD1Draws + 1][nrow] cursor before draw 0 and after each draw
+  int32_t *k1;    // [nrow] draws draw1 completed
+};
+
+// rows [r0, r1) of the block's 64 boards, word-major HBM -> LDS [row][65];
+// 16 B per thread-load, eight in flight (conflict-free LDS writes: a wave
+// covers four rows, whose banks are shifted by one)
+__device__ __forceinline__ void stage_rows(const uint32_t *__restrict__ slot, size_t nrow, int b0, int r0, int r1,
+                                           int tid) {
+  constexpr int U = 8;
+  int total = (r1 - r0) * 16;
+  for (int q0 = 0; q0 < total; q0 += kStageThreads * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      q = q < total ? q : total - 1;
+      v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)(r0 + (q >> 4)) * nrow + b0 + (q & 15) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      if (q < total) {
+        uint32_t *d = hz_lds + (r0 + (q >> 4)) * kLdsStride + (q & 15) * 4;
+        d[0] = v[u].x;
+        d[1] = v[u].y;
+        d[2] = v[u].z;
+        d[3] = v[u].w;
+      }
+    }
+  }
+}
+
+// all rows of the boards in `mask`, LDS -> word-major HBM (coalesced rows)
+__device__ __forceinline__ void unstage_rows(uint32_t *__restrict__ slot, size_t nrow, int b0, int tid,
+                                             uint64_t mask) {
+  int lane = tid & 63;
+  if (!((mask >> lane) & 1)) return;
+  for (int r = tid >> 6; r < kMT; r += kStageThreads / 64)
+    slot[(size_t)r * nrow + b0 + lane] = hz_lds[r * kLdsStride + lane];
+}
 
 // run script entries [from, to) of a board's chance sequence on its LDS
-// stream, recording packed piles and the cursor after each draw
-// (a rolled loop: one copy of the sampling code, so the instruction cache
-// holds it; the script word is picked by selects, not by a dynamic index)
-__device__ __forceinline__ void run_script(StreamDraw<LdsMT>& d, uint64_t& bag, uint64_t q[kAheadWords],
-                                           int32_t* __restrict__ cur, int n, int b, int from, int to) {
+// stream, recording packed piles and the cursor after each draw at
+// cur[(i + 1) * cs] (a rolled loop: one copy of the sampling code, so the
+// instruction cache holds it; the script word is picked by selects, not by
+// a dynamic index).  StopOnTwist: end before a draw that twisted (the rows
+// past the staged ones are not in LDS).  Returns the entries completed.
+template <bool StopOnTwist = false>
+__device__ __forceinline__ int run_script(StreamDraw<LdsMT> &d, uint64_t &bag, uint64_t q[kAheadWords],
+                                          int32_t *__restrict__ cur, size_t cs, int from, int to) {
   static_assert(kAheadWords == 4, "script words");
   uint64_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  int i = from;
 #pragma unroll 1
-  for (int i = from; i < to; i++) {
+  for (; i < to; i++) {
     uint32_t p9 = d(bag);
+    if (StopOnTwist && d.m.tw != kAheadTwist) break;
     if (p9 != 0x1FFu) apply_pile(bag, p9);
     // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
     int bit = 9 * i, wd = bit >> 6, off = bit & 63;
@@ -412,9 +475,10 @@ __device__ __forceinline__ void run_script(StreamDraw<LdsMT>& d, uint64_t& bag, 
     q1 |= wd == 1 ? lo : wd == 0 ? hi : 0ull;
     q2 |= wd == 2 ? lo : wd == 1 ? hi : 0ull;
     q3 |= wd == 3 ? lo : wd == 2 ? hi : 0ull;
-    cur[(size_t)(i + 1) * n + b] = d.m.cursor();
+    cur[(size_t)(i + 1) * cs] = d.m.cursor();
   }
   q[0] = q0; q[1] = q1; q[2] = q2; q[3] = q3;
+  return i;
 }
 
 __device__ __forceinline__ uint64_t initial_bag() {
@@ -424,45 +488,102 @@ __device__ __forceinline__ uint64_t initial_bag() {
   return bag;
 }
 
-__device__ __forceinline__ void seed_block(int blk, uint32_t *__restrict__ out_mt, int32_t *__restrict__ out_tag,
-                                           uint64_t *__restrict__ out_pile, int32_t *__restrict__ out_cur,
-                                           const int32_t *__restrict__ ep_final, int n, uint64_t seed_base,
-                                           int draws) {
-  int tid = threadIdx.x;
-  int lane = tid & 63;
-  int b0 = blk * kBlock;
-  int b = b0 + lane;
-  bool act = b < n;
-  uint64_t actmask = __ballot(act);
-  int nb = n - b0 < kBlock ? n - b0 : kBlock;
-#ifdef HZ_DIAG
-  uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
-  if (tid < 64 && act) {
-    int e = ep_final[b] + 2;
-    mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-    HZ_PHASE(0, t0, b);
-    StreamDraw<LdsMT> d{LdsMT(lane, kMTSeeded)};
-    d.m.twist_ahead(kAheadTwist);  // cursor kMTAhead
-    HZ_PHASE(1, t0, b);
-    out_cur[b] = d.m.cursor();
-    uint64_t bag = initial_bag(), q[kAheadWords] = {};
-    run_script(d, bag, q, out_cur, n, b, 0, draws < kSeedDraws ? draws : kSeedDraws);
-    HZ_PHASE(2, t0, b);
-#pragma unroll
-    for (int w = 0; w < kAheadWords; w++) out_pile[(size_t)w * n + b] = q[w];
-    out_tag[b] = e;
-  }
-  __syncthreads();
-  stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
+__device__ __forceinline__ uint64_t episode_seed(uint64_t seed_base, int b, int e) {
+  return seed_base + (uint64_t)b + ((uint64_t)e << 32);
 }
 
-__device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__ in_mt,
-                                           const int32_t *__restrict__ in_tag, const uint64_t *__restrict__ in_pile,
-                                           const int32_t *__restrict__ in_cur, uint32_t *__restrict__ out_mt,
-                                           int32_t *__restrict__ tag, uint64_t *__restrict__ pile,
-                                           int32_t *__restrict__ cur, const int32_t *__restrict__ ep_final, int n,
-                                           uint64_t seed_base, int draws) {
+// a board's stream seeded and pre-twisted in its LDS column (cursor kMTAhead)
+__device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
+  mt_seed(hz_lds + lane, kLdsStride, sd);
+  LdsMT m(lane, kMTSeeded);
+  m.twist_ahead(kAheadTwist);
+}
+
+__device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const int32_t *__restrict__ ep_final,
+                                           int n, uint64_t seed_base) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  int b = blk * kBlock + lane;
+  bool act = b < n;
+#ifdef HZ_DIAG
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  int e = act ? ep_final[b] + 3 : 0;
+  if (tid < 64 && act) {
+    mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e));
+    HZ_PHASE(0, t0, b);
+  }
+  __syncthreads();
+  // all four waves, four boards of a row per thread (16 B stores, a wave
+  // covers four rows: conflict-free LDS reads): rows [0, kAheadTwist) of the
+  // next generation (sources i, i + 1 <= 224 and i + 397 <= 620 are all
+  // still old, so the rows are independent), the rest as seeded.  Columns
+  // past n hold whatever LDS held; the next stages never read them.
+  int c4 = (tid & 15) * 4;
+  uint32_t *out = rs.mt + (size_t)blk * kBlock + c4;
+#pragma unroll 2
+  for (int r = tid >> 4; r < kMT; r += kStageThreads / 16) {
+    const uint32_t *L = hz_lds + r * kLdsStride + c4;
+    uint4 v;
+    if (r < kAheadTwist) {
+      const uint32_t *L1 = L + kLdsStride, *Lf = L + 397 * kLdsStride;
+      v.x = twist_word(L[0], L1[0], Lf[0]);
+      v.y = twist_word(L[1], L1[1], Lf[1]);
+      v.z = twist_word(L[2], L1[2], Lf[2]);
+      v.w = twist_word(L[3], L1[3], Lf[3]);
+    } else {
+      v = uint4{L[0], L[1], L[2], L[3]};
+    }
+    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = v;
+  }
+  if (!act) return;
+  if (tid < 64) {
+    rs.tag[b] = e * 4 + 1;
+    HZ_PHASE(1, t0, b);
+  }
+}
+
+__device__ __forceinline__ void draw1_stage(int blk, Ring r1, size_t nrow, const int32_t *__restrict__ ep_final,
+                                            int n, uint64_t seed_base, int draws) {
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  int b0 = blk * kBlock;
+  int b = b0 + lane;
+  bool act = b < n;
+#ifdef HZ_DIAG
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  int e = act ? ep_final[b] + 2 : 0;
+  bool seeded = act && r1.tag[b] == e * 4 + 1;
+  uint64_t smask = __ballot(seeded), fmask = __ballot(act && !seeded);  // the same in every wave
+  if (smask) stage_rows(r1.mt, nrow, b0, 0, kAheadTwist, tid);
+  __syncthreads();
+  if (tid < 64 && act) {
+    HZ_PHASE(2, t0, b);
+    if (!seeded) seed_in_lds(lane, episode_seed(seed_base, b, e));
+    StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
+    uint64_t bag = initial_bag(), q[kAheadWords] = {};
+    int32_t *cur = r1.cur + b;
+    cur[0] = kMTAhead;
+    int k = draws < kD1Draws ? draws : kD1Draws;
+    // a seeded lane holds only the twisted rows: it stops before a twist
+    int k1 = seeded ? run_script<true>(d, bag, q, cur, nrow, 0, k) : run_script<false>(d, bag, q, cur, nrow, 0, k);
+#pragma unroll
+    for (int w = 0; w < 3; w++) r1.pile[(size_t)w * nrow + b] = q[w];
+    r1.k1[b] = k1;
+    r1.tag[b] = e * 4 + 2;
+    HZ_PHASE(3, t0, b);
+  }
+  if (fmask) {  // boards seeded here: their whole stream to the slot
+    __syncthreads();
+    unstage_rows(r1.mt, nrow, b0, tid, fmask);
+  }
+}
+
+__device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint32_t *__restrict__ out_mt,
+                                            int32_t *__restrict__ tag, uint64_t *__restrict__ pile,
+                                            int32_t *__restrict__ cur, const int32_t *__restrict__ ep_final, int n,
+                                            uint64_t seed_base, int draws) {
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b0 = blk * kBlock;
@@ -470,43 +591,40 @@ __device__ __forceinline__ void draw_block(int blk, const uint32_t *__restrict__
   bool act = b < n;
   uint64_t actmask = __ballot(act);
   int nb = n - b0 < kBlock ? n - b0 : kBlock;
-  int e = act ? ep_final[b] + 1 : 0;
 #ifdef HZ_DIAG
   uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  bool seeded = act && in_tag && in_tag[b] == e;
-  uint64_t seededmask = __ballot(seeded);
-  if (seededmask) stage_mt(const_cast<uint32_t *>(in_mt) + (size_t)b0 * kMT, nb, tid, seededmask, true);
+  int e = act ? ep_final[b] + 1 : 0;
+  bool ok = act && r2.tag[b] == e * 4 + 2;
+  uint64_t okmask = __ballot(ok);
+  if (okmask) stage_rows(r2.mt, nrow, b0, 0, kMT, tid);
   __syncthreads();
-  if (tid < 64 && act) HZ_PHASE(3, t0, b);
+  if (tid < 64 && act) HZ_PHASE(4, t0, b);
   if (tid < 64 && act) {
-    int k0 = draws < kSeedDraws ? draws : kSeedDraws;
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
-    int start;
-    if (seeded) {  // continue after the seed stage's draws
+    int start = 0, c0 = kMTAhead;
+    if (ok) {  // continue after draw1's draws
+      int k1 = r2.k1[b];
 #pragma unroll
-      for (int w = 0; w < kAheadWords; w++) q[w] = in_pile[(size_t)w * n + b];
-#pragma unroll
-      for (int i = 0; i <= kSeedDraws; i++)
-        if (i <= k0) cur[(size_t)i * n + b] = in_cur[(size_t)i * n + b];
-#pragma unroll
-      for (int i = 0; i < kSeedDraws; i++) {
-        if (i < k0) {
-          uint32_t p9 = (uint32_t)(q[0] >> (9 * i)) & 0x1FFu;  // entries 0..6 sit in word 0
-          if (p9 != 0x1FFu) apply_pile(bag, p9);
-        }
+      for (int w = 0; w < 3; w++) q[w] = r2.pile[(size_t)w * nrow + b];
+      uint64_t a0 = q[0], a1 = q[1], a2 = q[2];
+#pragma unroll 1
+      for (int i = 0; i < k1; i++) {
+        cur[(size_t)i * n + b] = r2.cur[(size_t)i * nrow + b];
+        uint32_t p9 = (uint32_t)a0 & 0x1FFu;
+        if (p9 != 0x1FFu) apply_pile(bag, p9);
+        a0 = (a0 >> 9) | (a1 << 55);
+        a1 = (a1 >> 9) | (a2 << 55);
+        a2 >>= 9;
       }
-      start = k0;
+      c0 = r2.cur[(size_t)k1 * nrow + b];
+      start = k1;
     } else {
-      mt_seed(hz_lds + lane, kLdsStride, seed_base + (uint64_t)b + ((uint64_t)e << 32));
-      LdsMT m(lane, kMTSeeded);
-      m.twist_ahead(kAheadTwist);
-      cur[b] = m.cursor();
-      start = 0;
+      seed_in_lds(lane, episode_seed(seed_base, b, e));
     }
-    StreamDraw<LdsMT> d{LdsMT(lane, seeded ? in_cur[(size_t)k0 * n + b] : kMTAhead)};
-    HZ_PHASE(4, t0, b);
-    run_script(d, bag, q, cur, n, b, start, draws);
+    cur[(size_t)start * n + b] = c0;
+    StreamDraw<LdsMT> d{LdsMT(lane, c0)};
+    run_script(d, bag, q, cur + b, n, start, draws);
     HZ_PHASE(14, t0, b);
 #pragma unroll
     for (int w = 0; w < kAheadWords; w++) pile[(size_t)w * n + b] = q[w];
@@ -535,31 +653,26 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     int32_t *__restrict__ ep_final, int nblk,
                                                     uint32_t *__restrict__ prep_mt, int32_t *__restrict__ prep_tag,
                                                     uint64_t *__restrict__ prep_pile, int32_t *__restrict__ prep_cur,
-                                                    const int32_t *__restrict__ prep_ep,
-                                                    const uint32_t *__restrict__ seed_in_mt,
-                                                    const int32_t *__restrict__ seed_in_tag,
-                                                    const uint64_t *__restrict__ seed_in_pile,
-                                                    const int32_t *__restrict__ seed_in_cur,
-                                                    uint32_t *__restrict__ seed_out_mt,
-                                                    int32_t *__restrict__ seed_out_tag,
-                                                    uint64_t *__restrict__ seed_out_pile,
-                                                    int32_t *__restrict__ seed_out_cur) {
+                                                    const int32_t *__restrict__ prep_ep, Ring rs, Ring r1,
+                                                    Ring r2, long nrow) {
 #ifdef HZ_DIAG
   uint64_t role_t0 = __builtin_amdgcn_s_memtime();
 #endif
   if ((int)blockIdx.x >= nblk) {  // chance-ahead roles (uniform per block)
     int blk = (int)blockIdx.x - nblk;
-    if (blk < nblk)
-      draw_block(blk, seed_in_mt, seed_in_tag, seed_in_pile, seed_in_cur, prep_mt, prep_tag, prep_pile, prep_cur,
-                 prep_ep, n, seed_base, ahead_draws);
+    int role = blk / nblk;
+    blk -= role * nblk;
+    if (role == 0)
+      draw2_stage(blk, r2, (size_t)nrow, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base, ahead_draws);
+    else if (role == 1)
+      draw1_stage(blk, r1, (size_t)nrow, prep_ep, n, seed_base, ahead_draws);
     else
-      seed_block(blk - nblk, seed_out_mt, seed_out_tag, seed_out_pile, seed_out_cur, prep_ep, n, seed_base,
-                 ahead_draws);
+      seed_stage(blk, rs, (size_t)nrow, prep_ep, n, seed_base);
 #ifdef HZ_DIAG
-    {  // role durations: slot 6 (draw blocks), 7 (seed blocks), per board of the block
-      int bb = (blk % nblk) * kBlock + (threadIdx.x & 63);
+    {  // role durations: slot 6 (draw2 blocks), 15 (draw1), 7 (seed), per board of the block
+      int bb = blk * kBlock + (threadIdx.x & 63);
       if (g_stamps && threadIdx.x < 64 && bb < n)
-        g_stamps[(size_t)bb * 16 + (blk < nblk ? 6 : 7)] = __builtin_amdgcn_s_memtime() - role_t0;
+        g_stamps[(size_t)bb * 16 + (role == 0 ? 6 : role == 1 ? 15 : 7)] = __builtin_amdgcn_s_memtime() - role_t0;
     }
 #endif
     return;
@@ -847,13 +960,18 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
          hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
-         hipMalloc(&e->seed_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
-         hipMalloc(&e->seed_tag[k], n * sizeof(int32_t)) == hipSuccess &&
-         hipMemset(e->seed_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess &&
-         hipMalloc(&e->seed_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
-         hipMalloc(&e->seed_cur[k], n * (kSeedDraws + 1) * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
+  }
+  e->nrow = (n + kBlock - 1) / kBlock * kBlock;
+  for (int k = 0; ok && k < kRing; k++) {
+    size_t nr = e->nrow;
+    ok = hipMalloc(&e->ring_mt[k], nr * kMT * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc(&e->ring_tag[k], nr * sizeof(int32_t)) == hipSuccess &&
+         hipMemset(e->ring_tag[k], 0xff, nr * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->ring_pile[k], nr * 3 * sizeof(uint64_t)) == hipSuccess &&
+         hipMalloc(&e->ring_cur[k], nr * (kD1Draws + 1) * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->ring_k1[k], nr * sizeof(int32_t)) == hipSuccess;
   }
   ok = ok && hipDeviceSynchronize() == hipSuccess;
   e->seed_ahead = kAheadDraws;
@@ -871,11 +989,14 @@ void hz_env_destroy(hz_env *e) {
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
     if (e->ahead_pile[k]) (void)hipFree(e->ahead_pile[k]);
     if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
-    if (e->seed_mt[k]) (void)hipFree(e->seed_mt[k]);
-    if (e->seed_tag[k]) (void)hipFree(e->seed_tag[k]);
-    if (e->seed_pile[k]) (void)hipFree(e->seed_pile[k]);
-    if (e->seed_cur[k]) (void)hipFree(e->seed_cur[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
+  }
+  for (int k = 0; k < kRing; k++) {
+    if (e->ring_mt[k]) (void)hipFree(e->ring_mt[k]);
+    if (e->ring_tag[k]) (void)hipFree(e->ring_tag[k]);
+    if (e->ring_pile[k]) (void)hipFree(e->ring_pile[k]);
+    if (e->ring_cur[k]) (void)hipFree(e->ring_cur[k]);
+    if (e->ring_k1[k]) (void)hipFree(e->ring_k1[k]);
   }
   if (e->state) (void)hipFree(e->state);
   if (e->mt) (void)hipFree(e->mt);
@@ -904,6 +1025,9 @@ int hz_env_set_seed_ahead(hz_env *e, int32_t draws) {
   if (!e || draws < 0) return -1;
   e->seed_ahead = draws > kAheadDraws ? kAheadDraws : draws;
   e->primed = 0;
+  // draw1's work depends on the draw count: start the ring afresh
+  for (int k = 0; k < kRing; k++)
+    if (hipMemsetAsync(e->ring_tag[k], 0xff, e->nrow * sizeof(int32_t), e->stream)) return 1;
   return 0;
 }
 
@@ -955,18 +1079,19 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
   return launch_err();
 }
 
-// hz_play's chance-ahead pipeline: one launch per call, blocks [0, nblk)
-// play from play slot r = calls & 1, blocks [nblk, 2 nblk) fill play slot
-// w = r ^ 1 for the next call from seed slot r, blocks [2 nblk, 3 nblk)
-// fill seed slot w for the call after.  Launch order on the stream is the
-// only synchronisation: a slot written by call i is read by call i+1; the
-// preparing blocks read ep_final[w], written by call i-1's playing blocks
-// (the episode counter each board ended with).  The
-// prediction (call i+1 resets to that counter plus one) only decides which
-// boards skip seeding and drawing: a board replays a slot only when the
-// slot's tag equals its episode counter, so results never depend on it.
-// Anything else that moves episode counters (hz_reset, hz_rollout) makes
-// the next call re-prime ep_final from the counters.
+// hz_play's chance-ahead pipeline: one launch per call c.  Blocks [0, nblk)
+// play from play slot r = c & 1; draw2 blocks [nblk, 2 nblk) fill play slot
+// w = r ^ 1 for call c + 1 from ring slot (c + 1) % 3; draw1 blocks
+// continue ring slot (c + 2) % 3 for call c + 2; seed blocks refill ring
+// slot c % 3 for call c + 3.  Launch order on the stream is the only
+// synchronisation: a slot written by call c is read by call c + 1; the
+// preparing blocks read ep_final[w], written by call c - 1's playing blocks
+// (the episode counter each board ended with).  The prediction (call c + k
+// resets to that counter plus k) only decides which boards skip seeding and
+// drawing: a board replays a slot only when the slot's tag equals its
+// episode counter, so results never depend on it.  Anything else that moves
+// episode counters (hz_reset, hz_rollout) makes the next call re-prime
+// ep_final from the counters.
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
@@ -978,13 +1103,14 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   int nblk = grid_for(e->n), grid = nblk;
   bool pipe = reset_first && e->seed_ahead > 0;
   int r = e->calls & 1, w = r ^ 1;
+  int c3 = e->calls % kRing;
+  auto ring = [e](int k) { return Ring{e->ring_mt[k], e->ring_tag[k], e->ring_pile[k], e->ring_cur[k], e->ring_k1[k]}; };
   if (pipe) {
     size_t n = (size_t)e->n;
     if (!e->primed) {
       if (hipMemcpyAsync(e->ep_final[w], e->episode, n * sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream))
         return 1;
       e->slot_valid[r] = 0;
-      e->seed_valid[r] = 0;
       e->primed = 1;
     }
     if (e->slot_valid[r]) {
@@ -994,7 +1120,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
       ahead_cur = e->ahead_cur[r];
     }
     ep_final = e->ep_final[r];
-    grid = 3 * nblk;
+    grid = 4 * nblk;
   } else {
     e->primed = 0;
   }
@@ -1005,14 +1131,12 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      e->episode, e->seed, e->n, e->seed_base, max_plies, auto_reset, reset_first, traj_state,
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
-                     e->ahead_cur[w], e->ep_final[w], e->seed_mt[r], e->seed_valid[r] ? e->seed_tag[r] : nullptr,
-                     e->seed_pile[r], e->seed_cur[r], e->seed_mt[w], e->seed_tag[w], e->seed_pile[w],
-                     e->seed_cur[w]);
+                     e->ahead_cur[w], e->ep_final[w], ring(c3), ring((c3 + 2) % kRing), ring((c3 + 1) % kRing),
+                     (long)e->nrow);
   int err = launch_err();
   if (err) return err;
   if (pipe) {
     e->slot_valid[w] = 1;
-    e->seed_valid[w] = 1;
     e->calls++;
   }
   return 0;

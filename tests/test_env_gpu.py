@@ -165,23 +165,25 @@ def _check_episode(env, base, ep, steps, nthreads=8):
         assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b], (ep, b)
 
 
-@pytest.mark.parametrize("ahead,draws", [(True, 24), (True, 3), (True, 19), (False, 0)])
+@pytest.mark.parametrize("ahead,draws", [(True, 24), (True, 3), (True, 16), (True, 19), (False, 0)])
 def test_play_seed_ahead_pipeline(Env, ahead, draws):
-    """Consecutive hz_play calls (episodes 0, 1, 2 from prepared slots),
-    an hz_reset + hz_rollout in between (episode 3, re-primes the pipeline),
-    then episodes 4 and 5: every game bit-exact vs the oracle's episode.
-    draws < 19 makes every game (19-23 draws) run past its pile script onto
-    the prepared stream; 19 covers the boundary."""
+    """Consecutive hz_play calls (episodes 0-4: the first three fill the
+    seed -> draw1 -> draw2 pipeline, the rest replay fully prepared slots),
+    an hz_reset + hz_rollout in between (episode 5, re-primes the pipeline;
+    the ring slots then hold stale episodes), then episodes 6-10: every game
+    bit-exact vs the oracle's episode.  draws < 19 makes every game (19-23
+    draws) run past its pile script onto the prepared stream; 19 covers the
+    boundary; 16 leaves draw2 nothing to draw."""
     n, base = 4096, 2024
     env = Env(n, seed_base=base, device=DEV)
     env.set_seed_ahead(ahead, draws)
-    for ep in range(3):
+    for ep in range(5):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
     env.reset()
     _, steps, _ = env.rollout(200)
-    _check_episode(env, base, 3, steps)
-    for ep in (4, 5):
+    _check_episode(env, base, 5, steps)
+    for ep in range(6, 11):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
 

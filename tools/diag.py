@@ -44,10 +44,11 @@ out.update({"play_primed_us": f0.elapsed_time(f1) * 1e3,
             "primed_top_cyc": s[:, 8].mean().item(), "primed_legal_cyc": s[:, 9].mean().item(),
             "primed_pick_cyc": s[:, 10].mean().item(), "primed_step_cyc": s[:, 11].mean().item(),
             "primed_turnend_cyc": s[:, 12].mean().item(), "primed_final_cyc": s[:, 13].mean().item(),
-            "role_play_cyc_max": s[:, 5].max().item(), "role_draw_cyc_max": s[:, 6].max().item(),
+            "role_play_cyc_max": s[:, 5].max().item(), "role_draw2_cyc_max": s[:, 6].max().item(),
             "role_seed_cyc_max": s[:, 7].max().item(),
             # preparation phases, cycles since the role began (max over boards)
+            "role_draw1_cyc_max": s[:, 15].max().item(),
             "seed_after_seed": s[:, 0].max().item(), "seed_after_twist": s[:, 1].max().item(),
-            "seed_after_draws": s[:, 2].max().item(), "draw_after_stage_in": s[:, 3].max().item(),
-            "draw_before_draws": s[:, 4].max().item(), "draw_after_draws": s[:, 14].max().item()})
+            "draw1_after_stage_in": s[:, 2].max().item(), "draw1_after_draws": s[:, 3].max().item(),
+            "draw2_after_stage_in": s[:, 4].max().item(), "draw2_after_draws": s[:, 14].max().item()})
 print(json.dumps(out))

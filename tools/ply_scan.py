@@ -22,5 +22,6 @@ for P in (8, 16, 32, 48, 64, 96):
     env.rollout(P, reset=True)
     torch.cuda.synchronize()
     s = stamps.cpu().double()
-    out[P] = {"play_max": s[:, 5].max().item(), "draw_max": s[:, 6].max().item(), "seed_max": s[:, 7].max().item()}
+    out[P] = {"play_max": s[:, 5].max().item(), "draw2_max": s[:, 6].max().item(), "draw1_max": s[:, 15].max().item(),
+              "seed_max": s[:, 7].max().item()}
 print(json.dumps(out))
