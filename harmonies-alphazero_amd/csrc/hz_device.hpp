@@ -461,9 +461,14 @@ __constant__ InitGen kInitGen = make_init_gen();
 // init_by_array with key = the seed's 32-bit words) into w[i * stride].
 // Both passes are serial recurrences; the code keeps each step to its five
 // dependent ALU ops (key selection unrolled by two, pass-1 words read eight
-// ahead in pass 2).  The stream's cursor afterwards is kMTSeeded.
-template <class Ptr>
-__device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed) {
+// ahead in pass 2).  The stream's cursor afterwards is kMTSeeded.  After
+// each group of pass 2, `prog(r)` reports rows [2, r) final (the seed stage
+// publishes them to waves that store them meanwhile).
+struct NoProgress {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <class Ptr, class Prog = NoProgress>
+__device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed, Prog prog = Prog()) {
   uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   // key[j] + j for j = (i - 1) % keylen: odd i -> kA, even i -> kB
   uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
@@ -511,6 +516,7 @@ __device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed) {
       w[(g + u) * stride] = v;
       prev = v;
     }
+    prog(g + 8);
 #pragma unroll
     for (int u = 0; u < 8; u++) cur[u] = nx[u];
   }

@@ -381,10 +381,10 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 // hz_play launch beyond the playing ones (4 x 64 blocks of 162 KB LDS: one
 // per CU, every CU of the chip).  Stage k works on each board's episode k
 // calls ahead (the episode counter the previous launch left, plus k):
-//   seed  (k = 3) blocks [3 nblk, 4 nblk): the stream seeded in LDS, then
-//     stored by all four waves to a word-major ring slot, rows
-//     [0, kAheadTwist) twisted on the way (every source still old: no
-//     serial chain);
+//   seed  (k = 3) blocks [3 nblk, 4 nblk): the stream seeded in LDS and
+//     stored to a word-major ring slot (most rows by waves 1-3 while wave 0
+//     still seeds), rows [0, kAheadTwist) twisted on the way (every source
+//     still old: no serial chain);
 //   draw1 (k = 2) blocks [2 nblk, 3 nblk): the slot's twisted rows staged
 //     into LDS, the first kD1Draws pile draws run (a lane stops at a draw
 //     that would twist past the staged rows; the next stage redoes it), the
@@ -499,8 +499,22 @@ __device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
   m.twist_ahead(kAheadTwist);
 }
 
+// pass-2 progress of the seed stage's wave 0, published to waves 1-3 in
+// LDS every 64 rows (release: the rows' LDS writes are complete first).
+// mt_seed reports rows = 10, 18, ..., 618; published: 66, 130, ..., 578.
+constexpr int kLastPub = 2 + (618 - 2) / 64 * 64;
+constexpr int kSeedChunk = (kStageThreads - 64) / 16;  // rows per pass of waves 1-3
+constexpr int kOverlapEnd = kAheadTwist + (kLastPub - kAheadTwist) / kSeedChunk * kSeedChunk;
+struct SeedProgress {
+  int *flag;
+  __device__ __forceinline__ void operator()(int rows) const {
+    if ((rows & 63) == 2) __hip_atomic_store(flag, rows, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
 __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const int32_t *__restrict__ ep_final,
                                            int n, uint64_t seed_base) {
+  __shared__ int s_rows;  // pass-2 rows [2, s_rows) of every board are final
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b = blk * kBlock + lane;
@@ -509,35 +523,56 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
   int e = act ? ep_final[b] + 3 : 0;
-  if (tid < 64 && act) {
-    mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e));
-    HZ_PHASE(0, t0, b);
-  }
+  if (tid == 0) s_rows = 0;
   __syncthreads();
-  // all four waves, four boards of a row per thread (16 B stores, a wave
-  // covers four rows: conflict-free LDS reads): rows [0, kAheadTwist) of the
-  // next generation (sources i, i + 1 <= 224 and i + 397 <= 620 are all
-  // still old, so the rows are independent), the rest as seeded.  Columns
-  // past n hold whatever LDS held; the next stages never read them.
+  // Stores: four boards of a row per thread (16 B, a wave covers four rows:
+  // conflict-free LDS reads).  Rows [kAheadTwist, 624) stay as seeded:
+  // waves 1-3 store [kAheadTwist, kOverlapEnd) while wave 0's pass 2 is
+  // still running, as it publishes them.  After the barrier all four waves
+  // store the rest, and rows [0, kAheadTwist) of the next generation,
+  // twisted on the way (sources i, i + 1 <= 224 and i + 397 <= 620 are all
+  // still old, so the rows are independent).  Columns past n hold whatever
+  // LDS held; the next stages never read them.
   int c4 = (tid & 15) * 4;
   uint32_t *out = rs.mt + (size_t)blk * kBlock + c4;
-#pragma unroll 2
-  for (int r = tid >> 4; r < kMT; r += kStageThreads / 16) {
-    const uint32_t *L = hz_lds + r * kLdsStride + c4;
-    uint4 v;
-    if (r < kAheadTwist) {
-      const uint32_t *L1 = L + kLdsStride, *Lf = L + 397 * kLdsStride;
-      v.x = twist_word(L[0], L1[0], Lf[0]);
-      v.y = twist_word(L[1], L1[1], Lf[1]);
-      v.z = twist_word(L[2], L1[2], Lf[2]);
-      v.w = twist_word(L[3], L1[3], Lf[3]);
-    } else {
-      v = uint4{L[0], L[1], L[2], L[3]};
+  if (tid < 64) {
+    if (act) {
+      mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
+      HZ_PHASE(0, t0, b);
     }
+  } else {
+    int done = 0;
+#pragma unroll 1
+    for (int r0 = kAheadTwist; r0 < kOverlapEnd; r0 += kSeedChunk) {
+      // wave 0 publishes every row up to kLastPub; the bound only guards
+      // against a hang should that ever change
+      for (int spin = 0; done < r0 + kSeedChunk && spin < (1 << 22); spin++) {
+        __builtin_amdgcn_s_sleep(1);
+        done = __hip_atomic_load(&s_rows, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      int r = r0 + ((tid - 64) >> 4);
+      const uint32_t *L = hz_lds + r * kLdsStride + c4;
+      *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = uint4{L[0], L[1], L[2], L[3]};
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int r = kOverlapEnd + (tid >> 4); r < kMT; r += kStageThreads / 16) {
+    const uint32_t *L = hz_lds + r * kLdsStride + c4;
+    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = uint4{L[0], L[1], L[2], L[3]};
+  }
+#pragma unroll 2
+  for (int r = tid >> 4; r < kAheadTwist; r += kStageThreads / 16) {
+    const uint32_t *L = hz_lds + r * kLdsStride + c4;
+    const uint32_t *L1 = L + kLdsStride, *Lf = L + 397 * kLdsStride;
+    uint4 v;
+    v.x = twist_word(L[0], L1[0], Lf[0]);
+    v.y = twist_word(L[1], L1[1], Lf[1]);
+    v.z = twist_word(L[2], L1[2], Lf[2]);
+    v.w = twist_word(L[3], L1[3], Lf[3]);
     *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = v;
   }
-  if (!act) return;
-  if (tid < 64) {
+  if (tid < 64 && act) {
     rs.tag[b] = e * 4 + 1;
     HZ_PHASE(1, t0, b);
   }
