@@ -531,6 +531,78 @@ __device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed, Prog p
   w[0] = 0x80000000U;
 }
 
+// mt_seed with init_genrand's table read from an LDS copy (`tab`, 624
+// words, the same for every board: broadcast reads) instead of through the
+// scalar cache, whose waits also drain the pending LDS stores; rows at
+// w[i * S] (S a compile-time stride).
+template <int S, class Prog = NoProgress>
+__device__ __forceinline__ void mt_seed_tab(uint32_t *w, const uint32_t *tab, uint64_t seed, Prog prog = Prog()) {
+  // volatile reads: issued where written, a group ahead of their use (plain
+  // reads get scheduled next to the use, exposing the LDS latency per step)
+  typedef __attribute__((address_space(3))) const volatile uint32_t VW;
+  VW *vt = (VW *)tab;
+  VW *vw = (VW *)w;
+  uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
+  uint32_t prev = 19650218u;
+  uint32_t iv[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) iv[u] = vt[1 + u];
+#pragma unroll 2
+  for (int g = 1; g < kMT - 7; g += 8) {  // i = 1..616
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = vt[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      w[(g + u) * S] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = nx[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // i = 617..623
+    uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(617 + u) * S] = v;
+    prev = v;
+  }
+  uint32_t m1 = w[1 * S];
+  prev = (m1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+  w[1 * S] = prev;
+  uint32_t first1 = prev;
+  uint32_t cur[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) cur[u] = vw[(2 + u) * S];
+#pragma unroll 2
+  for (int g = 2; g < kMT - 6; g += 8) {  // i = 2..617
+    uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = vw[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      // (cur ^ p) - (g + u) as one v_xad_u32 with the offset in an SGPR
+      uint32_t p = (prev ^ (prev >> 30)) * 1566083941U, v;
+      asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
+      w[(g + u) * S] = v;
+      prev = v;
+    }
+    prog(g + 8);
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 6; u++) {  // i = 618..623
+    uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(618 + u);
+    w[(618 + u) * S] = v;
+    prev = v;
+  }
+  w[1 * S] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
+  w[0] = 0x80000000U;
+}
+
 template <class M>
 __device__ __forceinline__ uint32_t randbelow(M& m, uint32_t n) {
   if (!n) return 0;

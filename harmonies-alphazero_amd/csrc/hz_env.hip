@@ -512,6 +512,12 @@ struct SeedProgress {
   }
 };
 
+// The seed stage's LDS: the 64 streams as [624][64] (row-major, so four
+// boards of a row are one aligned 16-B read) and init_genrand's table after
+// them (kMT * 64 + kMT words = the block's 162,240 B).
+constexpr int kSeedStride = 64;
+static_assert((kMT * kSeedStride + kMT) * 4 <= (int)kResetLds, "seed stage LDS");
+
 __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const int32_t *__restrict__ ep_final,
                                            int n, uint64_t seed_base) {
   __shared__ int s_rows;  // pass-2 rows [2, s_rows) of every board are final
@@ -523,21 +529,24 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
   int e = act ? ep_final[b] + 3 : 0;
+  uint32_t *tab = hz_lds + kMT * kSeedStride;
+  for (int i = tid; i < kMT; i += kStageThreads) tab[i] = kInitGen.v[i];
   if (tid == 0) s_rows = 0;
   __syncthreads();
-  // Stores: four boards of a row per thread (16 B, a wave covers four rows:
-  // conflict-free LDS reads).  Rows [kAheadTwist, 624) stay as seeded:
-  // waves 1-3 store [kAheadTwist, kOverlapEnd) while wave 0's pass 2 is
-  // still running, as it publishes them.  After the barrier all four waves
-  // store the rest, and rows [0, kAheadTwist) of the next generation,
+  // Stores: four boards of a row per thread (one 16-B LDS read, one 16-B
+  // store; a wave covers four rows).  Rows [kAheadTwist, 624) stay as
+  // seeded: waves 1-3 store [kAheadTwist, kOverlapEnd) while wave 0's pass 2
+  // is still running, as it publishes them.  After the barrier all four
+  // waves store the rest, and rows [0, kAheadTwist) of the next generation,
   // twisted on the way (sources i, i + 1 <= 224 and i + 397 <= 620 are all
   // still old, so the rows are independent).  Columns past n hold whatever
   // LDS held; the next stages never read them.
   int c4 = (tid & 15) * 4;
   uint32_t *out = rs.mt + (size_t)blk * kBlock + c4;
+  auto row4 = [&](int r) { return *reinterpret_cast<const uint4 *>(hz_lds + r * kSeedStride + c4); };
   if (tid < 64) {
     if (act) {
-      mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
+      mt_seed_tab<kSeedStride>(hz_lds + lane, tab, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
       HZ_PHASE(0, t0, b);
     }
   } else {
@@ -551,25 +560,18 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
         done = __hip_atomic_load(&s_rows, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       int r = r0 + ((tid - 64) >> 4);
-      const uint32_t *L = hz_lds + r * kLdsStride + c4;
-      *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = uint4{L[0], L[1], L[2], L[3]};
+      *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
     }
   }
   __syncthreads();
 #pragma unroll 1
-  for (int r = kOverlapEnd + (tid >> 4); r < kMT; r += kStageThreads / 16) {
-    const uint32_t *L = hz_lds + r * kLdsStride + c4;
-    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = uint4{L[0], L[1], L[2], L[3]};
-  }
+  for (int r = kOverlapEnd + (tid >> 4); r < kMT; r += kStageThreads / 16)
+    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
 #pragma unroll 2
   for (int r = tid >> 4; r < kAheadTwist; r += kStageThreads / 16) {
-    const uint32_t *L = hz_lds + r * kLdsStride + c4;
-    const uint32_t *L1 = L + kLdsStride, *Lf = L + 397 * kLdsStride;
-    uint4 v;
-    v.x = twist_word(L[0], L1[0], Lf[0]);
-    v.y = twist_word(L[1], L1[1], Lf[1]);
-    v.z = twist_word(L[2], L1[2], Lf[2]);
-    v.w = twist_word(L[3], L1[3], Lf[3]);
+    uint4 c = row4(r), c1 = row4(r + 1), f = row4(r + 397);
+    uint4 v{twist_word(c.x, c1.x, f.x), twist_word(c.y, c1.y, f.y), twist_word(c.z, c1.z, f.z),
+            twist_word(c.w, c1.w, f.w)};
     *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = v;
   }
   if (tid < 64 && act) {

@@ -1,0 +1,156 @@
+// Dependent-chain cycle costs of the integer ops the MT seeding recurrence
+// can be built from (tools/alu_chain.py): one wave per SIMD, 1024 steps.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+// v_mul_u32_u24 as an opaque op (the compiler would fold the pieces back
+// into one v_mul_lo_u32)
+__device__ __forceinline__ uint32_t mul24(uint32_t c, uint32_t a) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(c), "v"(a));
+  return r;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t step(uint32_t x, uint32_t k) {
+  if constexpr (K == 0) {  // v_mul_lo_u32 chain
+    return x * 1664525u;
+  } else if constexpr (K == 1) {  // v_mul_u32_u24 chain
+    return mul24(1664525u, x);
+  } else if constexpr (K == 2) {  // xor-shift chain (2 plain ops)
+    return x ^ (x >> 3);
+  } else if constexpr (K == 3) {  // the seeding step as written
+    return ((x ^ (x >> 30)) * 1664525u ^ k) + 7u;
+  } else if constexpr (K == 4) {  // the seeding step, multiply by 24-bit halves
+    uint32_t t = x ^ (x >> 30);
+    uint32_t p = mul24(1664525u, t) + (mul24(1664525u, t >> 24) << 24);
+    return (p ^ k) + 7u;
+  } else if constexpr (K == 5) {  // pass-2 step as written
+    return ((x ^ (x >> 30)) * 1566083941u ^ k) - 7u;
+  } else {  // pass-2 step, multiply by 24-bit pieces (C = lo24 + hi8 << 24)
+    uint32_t t = x ^ (x >> 30);
+    constexpr uint32_t lo = 1566083941u & 0xFFFFFFu, hi = 1566083941u >> 24;
+    uint32_t p = mul24(lo, t) + ((mul24(lo, t >> 24) + mul24(hi, t)) << 24);
+    return (p ^ k) - 7u;
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_chain(uint32_t *out, uint64_t *cyc, uint32_t k) {
+  uint32_t x = threadIdx.x * 2654435761u + 1;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 64
+  for (int i = 0; i < 1024; i++) x = step<K>(x, k);
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * 64 + threadIdx.x] = x;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+extern "C" int alu_chain(int kind, void *out, void *cyc, int blocks) {
+  dim3 g(blocks), b(64);
+  uint32_t k = 0x12345u;
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(k_chain<0>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 1: hipLaunchKernelGGL(k_chain<1>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 2: hipLaunchKernelGGL(k_chain<2>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 3: hipLaunchKernelGGL(k_chain<3>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 4: hipLaunchKernelGGL(k_chain<4>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 5: hipLaunchKernelGGL(k_chain<5>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    case 6: hipLaunchKernelGGL(k_chain<6>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, k); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// ---- seeding variants (cycles per wave for one 64-board seeding)
+#include "../harmonies-alphazero_amd/csrc/hz_device.hpp"
+using namespace hz;
+
+// pass 1 as mt_seed runs it, with or without the LDS stores
+template <bool Store>
+__device__ __forceinline__ uint32_t pass1(uint32_t *w, int stride, uint32_t kA, uint32_t kB) {
+  uint32_t prev = 19650218u, acc = 0;
+  uint32_t iv[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[1 + u];
+  for (int g = 1; g < kMT - 7; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      if (Store) w[(g + u) * stride] = v;
+      else acc ^= v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = nx[u];
+  }
+  return prev ^ acc;
+}
+
+// pass 1 with the table words read from LDS (a block copy) instead of SMEM
+__device__ __forceinline__ uint32_t pass1_ldstab(uint32_t *w, int stride, const uint32_t *tab, uint32_t kA,
+                                                 uint32_t kB) {
+  uint32_t prev = 19650218u;
+  for (int g = 1; g < kMT - 7; g += 8) {
+    uint32_t iv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = tab[g + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      w[(g + u) * stride] = v;
+      prev = v;
+    }
+  }
+  return prev;
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) k_seedvar(uint32_t *out, uint64_t *cyc) {
+  extern __shared__ uint32_t lds[];
+  __shared__ uint32_t tab[kMT];
+  int lane = threadIdx.x;
+  for (int i = lane; i < kMT; i += 64) tab[i] = kInitGen.v[i];
+  __syncthreads();
+  uint64_t sd = 1234 + blockIdx.x * 64 + lane;
+  uint32_t kA = (uint32_t)sd, kB = (uint32_t)(sd >> 32) ? (uint32_t)(sd >> 32) + 1 : kA;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  uint32_t r = 0;
+  if constexpr (V == 0) mt_seed(hz_lds + lane, 64, sd);
+  if constexpr (V == 1) r = pass1<true>(hz_lds + lane, 64, kA, kB);
+  if constexpr (V == 2) r = pass1<false>(hz_lds + lane, 64, kA, kB);
+  if constexpr (V == 3) r = pass1_ldstab(hz_lds + lane, 64, tab, kA, kB);
+  if constexpr (V == 4) mt_seed_tab<64>(hz_lds + lane, tab, sd);
+  if constexpr (V == 5) mt_seed_tab<65>(hz_lds + lane, tab, sd);
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * 64 + lane] = r ^ hz_lds[7 * 64 + lane];
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+extern "C" int seed_var(int v, void *out, void *cyc, int blocks) {
+  dim3 g(blocks), b(64);
+  size_t lds = (size_t)kMT * 64 * 4;
+  static bool init = false;
+  if (!init) {
+    hipFuncSetAttribute((const void *)k_seedvar<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    init = true;
+  }
+  switch (v) {
+    case 0: hipLaunchKernelGGL(k_seedvar<0>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 1: hipLaunchKernelGGL(k_seedvar<1>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 2: hipLaunchKernelGGL(k_seedvar<2>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 3: hipLaunchKernelGGL(k_seedvar<3>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 4: hipLaunchKernelGGL(k_seedvar<4>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 6: hipLaunchKernelGGL(k_seedvar<0>, dim3(256), b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 7: hipLaunchKernelGGL(k_seedvar<4>, dim3(256), b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

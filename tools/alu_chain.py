@@ -1,0 +1,34 @@
+"""Cycles per dependent step of the candidate seeding-recurrence forms
+(tools/alu_chain.hip), one wave per SIMD, and a check that the 24-bit
+multiply forms equal the plain ones."""
+import ctypes, json, os
+import numpy as np
+import torch
+lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalu.so"))
+names = ["mul_lo", "mul_u24", "xorshift", "seed1", "seed1_u24", "seed2", "seed2_u24"]
+res, outs = {}, {}
+for k, nm in enumerate(names):
+    out = torch.zeros(64 * 64, dtype=torch.int32, device="cuda")
+    cyc = torch.zeros(64, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        assert lib.alu_chain(k, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(cyc.data_ptr()), 64) == 0
+    torch.cuda.synchronize()
+    res[nm] = float(cyc.double().median().item()) / 1024
+    outs[nm] = out.cpu().numpy()
+res["seed1_u24_equal"] = bool((outs["seed1"] == outs["seed1_u24"]).all())
+res["seed2_u24_equal"] = bool((outs["seed2"] == outs["seed2_u24"]).all())
+print(json.dumps(res))
+sv = {}
+outs = {}
+for v, nm in [(0, "mt_seed_lds"), (1, "pass1_lds"), (2, "pass1_nostore"), (3, "pass1_ldstab"), (4, "mt_seed_tab64"),
+              (6, "mt_seed_lds_256blk"), (7, "mt_seed_tab64_256blk")]:
+    out = torch.zeros(256 * 64, dtype=torch.int32, device="cuda")
+    cyc = torch.zeros(256, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        assert lib.seed_var(v, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(cyc.data_ptr()), 64) == 0
+    torch.cuda.synchronize()
+    nb = 256 if v >= 6 else 64
+    sv[nm] = float(cyc[:nb].double().median().item())
+    outs[nm] = out[:64 * 64].cpu().numpy()
+sv["tab_equal"] = bool((outs["mt_seed_lds"] == outs["mt_seed_tab64"]).all())
+print(json.dumps(sv))
