@@ -824,6 +824,18 @@ __device__ __forceinline__ int draw_pile(uint64_t misc, M& m, uint32_t& pile9) {
   return k;
 }
 
+// apply_pile without branches: each drawn tile's count field minus one (a
+// tile drawn is in the bag, so no field borrows); 7 = none
+__device__ __forceinline__ void apply_pile_fast(uint64_t& misc, uint32_t pile9) {
+  uint64_t dec = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    uint32_t t = (pile9 >> (3 * i)) & 7u;
+    dec += t < 6u ? 1ull << (11 + 5 * t) : 0ull;
+  }
+  misc -= dec;
+}
+
 // Every drawn tile decrements the bag (:126-129).
 __device__ __forceinline__ void apply_pile(uint64_t& misc, uint32_t pile9) {
 #pragma unroll
@@ -1319,7 +1331,15 @@ __device__ __forceinline__ bool turn_pair_safe(const State& s) {
 // kTileClass5: the class of tile t times 8 in bits 5t..5t+4.
 constexpr uint32_t kTileClass5 = (0u << 0) | (8u << 5) | (0u << 10) | (16u << 15) | (24u << 20) | (0u << 25);
 __device__ __forceinline__ uint32_t class_off(uint32_t t) { return __builtin_amdgcn_ubfe(kTileClass5, 5 * t, 5); }
+// place_code step of a tile onto a non-empty legal cell (code + add): plant
+// on wood 3 -> 7 (+4), building on 3/4/5 -> +7, stone on 8 -> 9 (+1) and on
+// 4 -> 8 (+4, patched below); 4 bits per tile
+constexpr uint32_t kAddTab = 1u | (4u << 4) | (1u << 8) | (1u << 12) | (7u << 16) | (1u << 20);
 
+// The turn path below is branch-free by construction: every choice among
+// more than two values is a bit-field extract from a packed word, never a
+// chain of selects (which the compiler turns into divergent branches).
+//
 // One placement ply of player P with NH tiles in hand (hand9: NH 3-bit tiles
 // in hand order): the rule's action is the k-th legal move, k = (h * L) >> 32,
 // in ascending action order = tile-major over the hand's distinct tiles
@@ -1339,55 +1359,64 @@ __device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h
   uint32_t cw = (uint32_t)__popc(mE) | ((uint32_t)__popc(mP) << 8) | ((uint32_t)__popc(mS) << 16) |
                 ((uint32_t)__popc(mB) << 24);
   uint32_t t0 = hand9 & 7u, t1 = (hand9 >> 3) & 7u, t2 = (hand9 >> 6) & 7u;
-  uint32_t tile;
-  int idx;
+  uint32_t tile, idx;
   if constexpr (NH == 1) {
-    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(t0), 8);
-    idx = (int)(((uint64_t)h * (uint32_t)c0) >> 32);
+    uint32_t c0 = __builtin_amdgcn_ubfe(cw, class_off(t0), 8);
+    idx = (uint32_t)(((uint64_t)h * c0) >> 32);
     tile = t0;
   } else if constexpr (NH == 2) {
     uint32_t lo = min(t0, t1), hi = max(t0, t1);
-    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(lo), 8);
-    int c1 = hi != lo ? (int)__builtin_amdgcn_ubfe(cw, class_off(hi), 8) : 0;
-    int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1)) >> 32);
+    uint32_t c0 = __builtin_amdgcn_ubfe(cw, class_off(lo), 8);
+    uint32_t c1 = __builtin_amdgcn_ubfe(cw, class_off(hi), 8) & (0u - (uint32_t)(hi != lo));
+    uint32_t k = (uint32_t)(((uint64_t)h * (c0 + c1)) >> 32);
     bool up = k >= c0;
     tile = up ? hi : lo;
-    idx = up ? k - c0 : k;
+    idx = k - (up ? c0 : 0u);
   } else {
-    uint32_t u0 = t0, u1 = t1, u2 = t2;
-    sort3(u0, u1, u2);
-    int c0 = (int)__builtin_amdgcn_ubfe(cw, class_off(u0), 8);
-    int c1 = u1 != u0 ? (int)__builtin_amdgcn_ubfe(cw, class_off(u1), 8) : 0;
-    int c2 = u2 != u1 ? (int)__builtin_amdgcn_ubfe(cw, class_off(u2), 8) : 0;
-    int k = (int)(((uint64_t)h * (uint32_t)(c0 + c1 + c2)) >> 32);
-    bool up1 = k >= c0, up2 = k >= c0 + c1;
-    tile = up2 ? u2 : up1 ? u1 : u0;
-    idx = up2 ? k - c0 - c1 : up1 ? k - c0 : k;
+    // the distinct tiles ascending (min/max network), their counts, the
+    // k-th move's tile (w = how many prefixes k passes) by one extract
+    uint32_t a = min(t0, t1), bb = max(t0, t1);
+    uint32_t u2 = max(bb, t2), m12 = min(bb, t2);
+    uint32_t u0 = min(a, m12), u1 = max(a, m12);
+    uint32_t c0 = __builtin_amdgcn_ubfe(cw, class_off(u0), 8);
+    uint32_t c1 = __builtin_amdgcn_ubfe(cw, class_off(u1), 8) & (0u - (uint32_t)(u1 != u0));
+    uint32_t c2 = __builtin_amdgcn_ubfe(cw, class_off(u2), 8) & (0u - (uint32_t)(u2 != u1));
+    uint32_t c01 = c0 + c1;
+    uint32_t k = (uint32_t)(((uint64_t)h * (c01 + c2)) >> 32);
+    uint32_t w = (uint32_t)(k >= c0) + (uint32_t)(k >= c01);
+    tile = __builtin_amdgcn_ubfe(u0 | (u1 << 3) | (u2 << 6), 3 * w, 3);
+    idx = k - __builtin_amdgcn_ubfe((c0 << 8) | (c01 << 16), 8 * w, 8);
   }
-  uint32_t off = class_off(tile);
-  uint32_t m = off == 0 ? mE : off == 8 ? mP : off == 16 ? mS : mB;
-  int c = select32(m, idx);
+  // the tile's legal cells: class bits q1 (plant, building), q2 (stone, building)
+  uint32_t cls = class_off(tile) >> 3;
+  uint32_t q1 = 0u - (cls & 1u), q2 = 0u - (cls >> 1);
+  uint32_t m = mE | (wood1 & q1) | (stone1 & q2) | (stone2 & q2 & ~q1) | (bld1 & q2 & q1);
+  int c = select32(m, (int)idx);
   // place_code for a legal placement (see step_trusted): empty -> 1 + t;
-  // plant on wood 3 -> 7; stone on 4 -> 8, on 8 -> 9; building on 3/4/5 -> +7
+  // otherwise code + add (kAddTab), stone on one stone 4 -> 8
   uint32_t code = __builtin_amdgcn_ubfe(b0, c, 1) | (__builtin_amdgcn_ubfe(b1, c, 1) << 1) |
                   (__builtin_amdgcn_ubfe(b2, c, 1) << 2) | (__builtin_amdgcn_ubfe(b3, c, 1) << 3);
-  uint32_t add = tile == BUILDING ? 7u : (tile == PLANT || code == 4u) ? 4u : 1u;
+  uint32_t add = __builtin_amdgcn_ubfe(kAddTab, 4 * tile, 4);
+  add += (code == 4u && add == 1u) ? 3u : 0u;
   uint32_t nc = code == 0u ? 1u + tile : code + add;
   uint32_t d = code ^ nc;
   uint32_t bit = 1u << c;
-  b0 ^= (d & 1u) ? bit : 0u;
-  b1 ^= (d & 2u) ? bit : 0u;
-  b2 ^= (d & 4u) ? bit : 0u;
-  b3 ^= (d & 8u) ? bit : 0u;
+  b0 ^= bit & (0u - (d & 1u));
+  b1 ^= bit & (0u - ((d >> 1) & 1u));
+  b2 ^= bit & (0u - ((d >> 2) & 1u));
+  b3 ^= bit & (0u - ((d >> 3) & 1u));
   s.pl[0] = with_half<P>(s.pl[0], b0);
   s.pl[1] = with_half<P>(s.pl[1], b1);
   s.pl[2] = with_half<P>(s.pl[2], b2);
   s.pl[3] = with_half<P>(s.pl[3], b3);
-  // hand.remove(tile): the first entry equal to it, the rest keep their order
+  // hand.remove(tile): the first entry equal to it goes, the rest keep
+  // their order (field p = 0, 1 or 2 removed by one bit-field insert)
   if constexpr (NH == 2) {
     hand9 = t0 == tile ? t1 : t0;
   } else if constexpr (NH == 3) {
-    hand9 = t0 == tile ? (t1 | (t2 << 3)) : t1 == tile ? (t0 | (t2 << 3)) : (t0 | (t1 << 3));
+    uint32_t p = (1u - (uint32_t)(t0 == tile)) * (2u - (uint32_t)(t1 == tile));
+    uint32_t low = (1u << (3 * p)) - 1u;
+    hand9 = (hand9 & low) | ((hand9 >> 3) & ~low);
   }
 }
 
@@ -1401,13 +1430,13 @@ __device__ __forceinline__ void end_turn_fast(State& s, Draw& draw) {
   uint64_t m = s.misc;
   bool bag_empty_before = (m & (((1ull << 30) - 1) << 11)) == 0;
   int np = npiles_of(s.piles);
-  if (np < 5 && !bag_empty_before) {
-    uint32_t pile9 = draw(m);
-    apply_pile(m, pile9);  // a full pile: the bag holds a multiple of three
-    s.piles = (s.piles & ~((0x1FFull << (9 * np)) | (7ull << 45))) | ((uint64_t)pile9 << (9 * np)) |
-              ((uint64_t)(np + 1) << 45);
-    np++;
-  }
+  bool want = np < 5 && !bag_empty_before;
+  uint32_t pile9 = draw.take(m, want);  // a full pile (the bag holds a multiple of three); 0x1FF if !want
+  apply_pile_fast(m, pile9);
+  uint64_t refilled = (s.piles & ~((0x1FFull << (9 * np)) | (7ull << 45))) | ((uint64_t)pile9 << (9 * np)) |
+                      ((uint64_t)(np + 1) << 45);
+  s.piles = want ? refilled : s.piles;
+  np += want ? 1 : 0;
   bool bag_trigger = bag_empty_before && np == 0;
   bool end = player_trigger || bag_trigger;
   bool over = over_flag(m);

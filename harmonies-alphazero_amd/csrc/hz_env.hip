@@ -353,6 +353,26 @@ struct PlayDraw {
     gm.tw = o.gtw;
     return o.p9;
   }
+
+  // a draw by the lanes with `want` (0x1FF for the others): while every such
+  // lane replays its script (wave-uniform test) a plain masked pop, else the
+  // general per-lane path
+  __device__ __forceinline__ uint32_t take(uint64_t misc, bool want) {
+    bool fast = scripted && d < nd;
+    if (__all(!want || fast)) {
+      uint32_t p9 = want ? (uint32_t)q0 & 0x1FFu : 0x1FFu;
+      uint64_t n0 = (q0 >> 9) | (q1 << 55), n1 = (q1 >> 9) | (q2 << 55), n2 = (q2 >> 9) | (q3 << 55);
+      q0 = want ? n0 : q0;
+      q1 = want ? n1 : q1;
+      q2 = want ? n2 : q2;
+      q3 = want ? q3 >> 9 : q3;
+      d += want ? 1 : 0;
+      return p9;
+    }
+    uint32_t p9 = 0x1FFu;
+    if (want) p9 = (*this)(misc);
+    return p9;
+  }
 };
 
 // copy the streams of boards in `mask` from `src` to `dst` (both board-major

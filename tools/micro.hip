@@ -172,6 +172,7 @@ struct CycleDraw {
     k++;
     return p9;
   }
+  __device__ __forceinline__ uint32_t take(uint64_t misc, bool want) { return want ? (*this)(misc) : 0x1FFu; }
 };
 
 template <int Mode>
