@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--eval-games", type=int, default=32, help="config 5: arena games per evaluation")
     ap.add_argument("--sims", type=int, default=200, help="config 3: MCTS simulations per move")
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
+    ap.add_argument("--full-game", action="store_true",
+                    help="config 3: time one complete game on every board (games/s measured, not estimated)")
     return ap.parse_args()
 
 
@@ -201,6 +203,8 @@ def bench_selfplay(args, dev, rank, world):
     cfg = {"num_simulations": args.sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
            "turns_until_tau0": 15, "testing": False}
     sp = SelfPlay(n, evaluator, cfg, seed_base=args.seed_base + rank * n, device=dev)
+    if args.full_game:
+        return bench_selfplay_games(args, sp, nn_ev, dev, rank, world)
     sp.env.reset()
     for w in range(args.warmup):
         sp.move(w)
@@ -239,6 +243,56 @@ def bench_selfplay(args, dev, rank, world):
             "nn_ms_per_move": nn_ms / args.steps, "tree_ms_per_move": per_move * 1e3 - nn_ms / args.steps,
             "nn_tflops": fl * n * args.sims * args.steps / (nn_ms * 1e-3) / 1e12,
             "note": "games/s estimated from ms per move x mean game length 62.4 plies",
+        }))
+
+
+def bench_selfplay_games(args, sp, nn_ev, dev, rank, world):
+    """Config 3, measured end to end: after `warmup` moves of a throw-away
+    game, every board plays one whole self-play game (search + choice + env
+    step per ply, records kept on the device as SelfPlay.play does); games/s
+    = boards of all ranks / the slowest rank's time."""
+    from hzamd.net import flops_per_eval
+    n = sp.n
+    sp.env.reset()
+    for w in range(args.warmup):
+        sp.move(w)
+    torch.cuda.synchronize(dev)
+    nn_ev.clear()
+    plies = [0]
+    orig_move = sp.move
+
+    def move(ply, done=None):  # progress on stderr (a long run must not look hung)
+        out = orig_move(ply, done)
+        plies[0] = ply + 1
+        if ply % 8 == 0:
+            print(f"[config3 full game] ply {ply}", file=sys.stderr, flush=True)
+        return out
+
+    sp.move = move
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    rec = sp.play(reset=True)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    sp.move = orig_move
+    evals = int(rec["valid"].sum().item()) * args.sims
+    nn_ms = sum(a.elapsed_time(b) for a, b in nn_ev)
+    if world > 1:
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "self-play games/sec @4096 boards x 200 MCTS sims (complete games, measured)",
+            "value": world * n / elapsed, "unit": "games/s", "n_gpus": world, "steps": 1, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
+            "config": {"workload": f"config3: {n} boards x {args.sims} sims/move, one whole game per board",
+                       "boards_per_gpu": n, "sims": args.sims, "parallelism": f"shard{world}"},
+            "plies": rec["plies"], "moves": int(rec["valid"].sum().item()),
+            "sims_per_s": world * evals / elapsed, "nn_s": nn_ms * 1e-3,
+            "nn_tflops": flops_per_eval() * n * args.sims * len(nn_ev) / args.sims / (nn_ms * 1e-3) / 1e12
+            if nn_ms else None,
         }))
 
 

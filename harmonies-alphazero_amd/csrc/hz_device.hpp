@@ -537,22 +537,17 @@ __device__ __forceinline__ void mt_seed(Ptr w, int stride, uint64_t seed, Prog p
 // w[i * S] (S a compile-time stride).
 template <int S, class Prog = NoProgress>
 __device__ __forceinline__ void mt_seed_tab(uint32_t *w, const uint32_t *tab, uint64_t seed, Prog prog = Prog()) {
-  // volatile reads: issued where written, a group ahead of their use (plain
-  // reads get scheduled next to the use, exposing the LDS latency per step)
-  typedef __attribute__((address_space(3))) const volatile uint32_t VW;
-  VW *vt = (VW *)tab;
-  VW *vw = (VW *)w;
   uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
   uint32_t prev = 19650218u;
   uint32_t iv[8];
 #pragma unroll
-  for (int u = 0; u < 8; u++) iv[u] = vt[1 + u];
+  for (int u = 0; u < 8; u++) iv[u] = tab[1 + u];
 #pragma unroll 2
   for (int g = 1; g < kMT - 7; g += 8) {  // i = 1..616
     uint32_t nx[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) nx[u] = vt[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+    for (int u = 0; u < 8; u++) nx[u] = tab[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
@@ -574,13 +569,13 @@ __device__ __forceinline__ void mt_seed_tab(uint32_t *w, const uint32_t *tab, ui
   uint32_t first1 = prev;
   uint32_t cur[8];
 #pragma unroll
-  for (int u = 0; u < 8; u++) cur[u] = vw[(2 + u) * S];
+  for (int u = 0; u < 8; u++) cur[u] = w[(2 + u) * S];
 #pragma unroll 2
   for (int g = 2; g < kMT - 6; g += 8) {  // i = 2..617
     uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
     uint32_t nx[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) nx[u] = vw[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
+    for (int u = 0; u < 8; u++) nx[u] = w[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       // (cur ^ p) - (g + u) as one v_xad_u32 with the offset in an SGPR
@@ -1457,23 +1452,28 @@ template <int P, bool CheapRule = false>
 __device__ __forceinline__ uint32_t turn_rule(uint64_t rkey, int ply) {
   return CheapRule ? ((uint32_t)rkey + (uint32_t)ply) * 0x9E3779B9u : rule_h32(rkey, ply);
 }
-template <int P, class Draw, bool CheapRule = false>
-__device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, int g_ply) {
+// ... given the four rule hashes of its plies (h[j] for ply g_ply + j)
+template <int P, class Draw>
+__device__ __forceinline__ void play_turn_h(State& s, Draw& draw, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3) {
   uint32_t hand9;
   {  // choose_pile: the pile leaves the row, later piles shift down (:221)
-    uint32_t h = turn_rule<P, CheapRule>(rkey, g_ply);
     int np = npiles_of(s.piles);
-    int a = (int)(((uint64_t)h * (uint32_t)np) >> 32);
+    int a = (int)(((uint64_t)h0 * (uint32_t)np) >> 32);
     hand9 = (uint32_t)(s.piles >> (9 * a)) & 0x1FF;
     uint64_t lower = s.piles & ((1ull << (9 * a)) - 1);
     uint64_t upper = (s.piles & ((1ull << 45) - 1)) >> (9 * (a + 1));
     s.piles = lower | (upper << (9 * a)) | (0x1FFull << 36) | ((uint64_t)(np - 1) << 45);
   }
-  place_fast<P, 3>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 1));
-  place_fast<P, 2>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 2));
-  place_fast<P, 1>(s, hand9, turn_rule<P, CheapRule>(rkey, g_ply + 3));
+  place_fast<P, 3>(s, hand9, h1);
+  place_fast<P, 2>(s, hand9, h2);
+  place_fast<P, 1>(s, hand9, h3);
   s.misc = (s.misc & ~0x7FFull) | 0x1FFull;  // empty hand
   end_turn_fast<P>(s, draw);
+}
+template <int P, class Draw, bool CheapRule = false>
+__device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, int g_ply) {
+  play_turn_h<P>(s, draw, turn_rule<P, CheapRule>(rkey, g_ply), turn_rule<P, CheapRule>(rkey, g_ply + 1),
+                 turn_rule<P, CheapRule>(rkey, g_ply + 2), turn_rule<P, CheapRule>(rkey, g_ply + 3));
 }
 
 // ------------------------------------------------------------ SoA access

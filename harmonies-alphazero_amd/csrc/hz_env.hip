@@ -33,6 +33,7 @@ struct hz_env {
   int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
+  uint32_t *ahead_rule[2];   // [kRulePlies][n] rule hashes (top 32 bits) per ply
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
   size_t nrow;               // n rounded up to 64: row stride of the ring slots
   uint32_t *ring_mt[3];      // [624][nrow] word-major streams, three calls / two calls ahead
@@ -45,8 +46,10 @@ struct hz_env {
 };
 
 #ifdef HZ_DIAG
-// diagnostic build only (tools/diag.py): per-lane phase clocks
+// diagnostic build only (tools/diag.py): per-lane phase clocks; g_role_only
+// >= 0 runs only that k_rollout role (0 draw2, 1 draw1, 2 seed, 3 play)
 __device__ uint64_t *g_stamps;
+__device__ int g_role_only = -1;
 #define HZ_STAMP(slot)                                                    \
   do {                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                    \
@@ -330,7 +333,10 @@ struct PlayDraw {
   MT gm;                   // slot stream (valid once fell)
   const int32_t *cur_tail; // cursor after the last scripted draw (global)
 
-  __device__ __forceinline__ uint32_t operator()(uint64_t misc) {
+  __device__ __forceinline__ uint32_t operator()(uint64_t misc) { return take(misc, true); }
+
+  // one draw per lane, any source
+  __device__ __forceinline__ uint32_t draw_one(uint64_t misc) {
     if (scripted && d < nd) {
       // pop the next 9-bit entry: a shift queue (a select over the four
       // words would become a dynamic index into a scratch copy)
@@ -354,6 +360,24 @@ struct PlayDraw {
     return o.p9;
   }
 
+  // reset_state when the lane replays a script of >= 5 entries
+  __device__ __forceinline__ void scripted_reset(State &s) {
+    s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
+    uint64_t open = q0 & ((1ull << 45) - 1);
+    s.piles = open | (5ull << 45);
+    uint64_t misc = 0x1FF;  // empty hand, player 0, choose_pile
+#pragma unroll
+    for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+#pragma unroll
+    for (int i = 0; i < 5; i++) apply_pile_fast(misc, (uint32_t)(open >> (9 * i)) & 0x1FFu);
+    s.misc = misc;
+    q0 = (q0 >> 45) | (q1 << 19);
+    q1 = (q1 >> 45) | (q2 << 19);
+    q2 = (q2 >> 45) | (q3 << 19);
+    q3 >>= 45;
+    d = 5;
+  }
+
   // a draw by the lanes with `want` (0x1FF for the others): while every such
   // lane replays its script (wave-uniform test) a plain masked pop, else the
   // general per-lane path
@@ -370,7 +394,7 @@ struct PlayDraw {
       return p9;
     }
     uint32_t p9 = 0x1FFu;
-    if (want) p9 = (*this)(misc);
+    if (want) p9 = draw_one(misc);
     return p9;
   }
 };
@@ -389,6 +413,10 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
       int q = q0 + u * nt + t;
       v[u] = reinterpret_cast<const uint4 *>(src)[q < total4 ? q : total4 - 1];
     }
+    // consumed here, unconditionally: otherwise each load is sunk into its
+    // guarded store's block and waited for alone (one load in flight)
+#pragma unroll
+    for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
 #pragma unroll
     for (int u = 0; u < U; u++) {
       int q = q0 + u * nt + t;
@@ -418,6 +446,10 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 // contents depend only on (board, episode), so a matching tag is always
 // right, whatever happened between the calls.
 constexpr int kD1Draws = 16;
+// the rule hashes of an episode's first kRulePlies plies (rule games end by
+// ply 72), computed by draw2's otherwise idle waves 1-3 and read by the
+// playing wave a turn pair ahead; plies past them are hashed in place
+constexpr int kRulePlies = 80;
 constexpr int kRing = 3;
 static_assert(kD1Draws <= kAheadDraws && 9 * kD1Draws <= 192, "draw1's script sits in words 0-2");
 
@@ -520,21 +552,32 @@ __device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
 }
 
 // pass-2 progress of the seed stage's wave 0, published to waves 1-3 in
-// LDS every 64 rows (release: the rows' LDS writes are complete first).
-// mt_seed reports rows = 10, 18, ..., 618; published: 66, 130, ..., 578.
-constexpr int kLastPub = 2 + (618 - 2) / 64 * 64;
+// LDS every 32 rows and at the end of the group loop.  A wave's LDS
+// operations execute in order, so a plain store of the counter after the
+// rows' stores is seen after them (the empty asm only keeps the compiler
+// from reordering; a release fence would wait for every pending LDS read
+// of the prefetch); readers load it with acquire.  mt_seed_tab reports
+// rows = 10, 18, ..., 618; published: 34, 66, ..., 610, 618.
+constexpr int kLastPub = 618;
 constexpr int kSeedChunk = (kStageThreads - 64) / 16;  // rows per pass of waves 1-3
 constexpr int kOverlapEnd = kAheadTwist + (kLastPub - kAheadTwist) / kSeedChunk * kSeedChunk;
 struct SeedProgress {
   int *flag;
   __device__ __forceinline__ void operator()(int rows) const {
-    if ((rows & 63) == 2) __hip_atomic_store(flag, rows, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifndef HZ_SEED_PUB_MASK
+#define HZ_SEED_PUB_MASK 31
+#endif
+    if ((rows & HZ_SEED_PUB_MASK) == 2 || rows == kLastPub) {
+      asm volatile("" ::: "memory");
+      __hip_atomic_store(flag, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
 };
 
-// The seed stage's LDS: the 64 streams as [624][64] (row-major, so four
-// boards of a row are one aligned 16-B read) and init_genrand's table after
-// them (kMT * 64 + kMT words = the block's 162,240 B).
+// The seed stage's LDS: init_genrand's table at offset 0 (its reads are
+// immediate offsets) and the 64 streams after it as [624][64] (row-major,
+// so four boards of a row are one aligned 16-B read): kMT + kMT * 64 words
+// = the block's 162,240 B.
 constexpr int kSeedStride = 64;
 static_assert((kMT * kSeedStride + kMT) * 4 <= (int)kResetLds, "seed stage LDS");
 
@@ -549,24 +592,32 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
   int e = act ? ep_final[b] + 3 : 0;
-  uint32_t *tab = hz_lds + kMT * kSeedStride;
+  uint32_t *tab = hz_lds, *rows = hz_lds + kMT;
   for (int i = tid; i < kMT; i += kStageThreads) tab[i] = kInitGen.v[i];
   if (tid == 0) s_rows = 0;
   __syncthreads();
   // Stores: four boards of a row per thread (one 16-B LDS read, one 16-B
   // store; a wave covers four rows).  Rows [kAheadTwist, 624) stay as
-  // seeded: waves 1-3 store [kAheadTwist, kOverlapEnd) while wave 0's pass 2
-  // is still running, as it publishes them.  After the barrier all four
-  // waves store the rest, and rows [0, kAheadTwist) of the next generation,
-  // twisted on the way (sources i, i + 1 <= 224 and i + 397 <= 620 are all
-  // still old, so the rows are independent).  Columns past n hold whatever
-  // LDS held; the next stages never read them.
+  // seeded; rows [0, kAheadTwist) become the next generation's, twisted on
+  // the way: row i from rows i, i + 1 (<= 224) and i + 397 (<= 620), all
+  // still old, so the rows are independent and row i is ready as soon as
+  // pass 2 has made row i + 397.  Waves 1-3 store, chunk by chunk as wave 0
+  // publishes its progress, plain rows [r0, r0 + 12) and twisted rows
+  // [r0 - 397, r0 - 385) (those >= 2); after the barrier all four waves
+  // store what is left (the last rows and twisted rows 0, 1, which need
+  // row 1, final last).  Columns past n hold whatever LDS held; the next
+  // stages never read them.
   int c4 = (tid & 15) * 4;
   uint32_t *out = rs.mt + (size_t)blk * kBlock + c4;
-  auto row4 = [&](int r) { return *reinterpret_cast<const uint4 *>(hz_lds + r * kSeedStride + c4); };
+  auto row4 = [&](int r) { return *reinterpret_cast<const uint4 *>(rows + r * kSeedStride + c4); };
+  auto twisted4 = [&](int r) {
+    uint4 c = row4(r), c1 = row4(r + 1), f = row4(r + 397);
+    return uint4{twist_word(c.x, c1.x, f.x), twist_word(c.y, c1.y, f.y), twist_word(c.z, c1.z, f.z),
+                 twist_word(c.w, c1.w, f.w)};
+  };
   if (tid < 64) {
     if (act) {
-      mt_seed_tab<kSeedStride>(hz_lds + lane, tab, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
+      mt_seed_tab<kSeedStride>(rows + lane, tab, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
       HZ_PHASE(0, t0, b);
     }
   } else {
@@ -581,18 +632,30 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
       }
       int r = r0 + ((tid - 64) >> 4);
       *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
+#ifndef HZ_SEED_NO_PROG_TWIST
+      int t = r - 397;
+      if (t >= 2) *reinterpret_cast<uint4 *>(out + (size_t)t * nrow) = twisted4(t);
+#endif
     }
+#ifdef HZ_DIAG_ROLES_ONLY
+    if (tid < 128 && act) HZ_PHASE(11, t0, b);
+#endif
   }
   __syncthreads();
+#ifdef HZ_DIAG_ROLES_ONLY
+  if (tid < 64 && act) HZ_PHASE(12, t0, b);
+#endif
+#ifndef HZ_SEED_NO_PROG_TWIST
+  constexpr int kTwistDone = kOverlapEnd - 397;  // twisted rows [2, kTwistDone) are stored
+#else
+  constexpr int kTwistDone = 2;
+#endif
 #pragma unroll 1
   for (int r = kOverlapEnd + (tid >> 4); r < kMT; r += kStageThreads / 16)
     *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
-#pragma unroll 2
-  for (int r = tid >> 4; r < kAheadTwist; r += kStageThreads / 16) {
-    uint4 c = row4(r), c1 = row4(r + 1), f = row4(r + 397);
-    uint4 v{twist_word(c.x, c1.x, f.x), twist_word(c.y, c1.y, f.y), twist_word(c.z, c1.z, f.z),
-            twist_word(c.w, c1.w, f.w)};
-    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = v;
+  for (int i = tid >> 4; i < 2 + (kAheadTwist - kTwistDone); i += kStageThreads / 16) {
+    int t = i < 2 ? i : kTwistDone + i - 2;
+    *reinterpret_cast<uint4 *>(out + (size_t)t * nrow) = twisted4(t);
   }
   if (tid < 64 && act) {
     rs.tag[b] = e * 4 + 1;
@@ -639,8 +702,9 @@ __device__ __forceinline__ void draw1_stage(int blk, Ring r1, size_t nrow, const
 
 __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint32_t *__restrict__ out_mt,
                                             int32_t *__restrict__ tag, uint64_t *__restrict__ pile,
-                                            int32_t *__restrict__ cur, const int32_t *__restrict__ ep_final, int n,
-                                            uint64_t seed_base, int draws) {
+                                            int32_t *__restrict__ cur, uint32_t *__restrict__ rule,
+                                            const int32_t *__restrict__ ep_final, int n, uint64_t seed_base,
+                                            int draws) {
   int tid = threadIdx.x;
   int lane = tid & 63;
   int b0 = blk * kBlock;
@@ -657,24 +721,33 @@ __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint3
   if (okmask) stage_rows(r2.mt, nrow, b0, 0, kMT, tid);
   __syncthreads();
   if (tid < 64 && act) HZ_PHASE(4, t0, b);
+  if (tid >= 64 && act) {  // waves 1-3, while wave 0 draws: the episode's rule hashes
+    uint64_t rk = rule_key(episode_seed(seed_base, b, e));
+#pragma unroll 1
+    for (int j = (tid >> 6) - 1; j < kRulePlies; j += 3) rule[(size_t)j * n + b] = rule_h32(rk, j);
+  }
   if (tid < 64 && act) {
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
     int start = 0, c0 = kMTAhead;
     if (ok) {  // continue after draw1's draws
       int k1 = r2.k1[b];
+      c0 = r2.cur[(size_t)k1 * nrow + b];
 #pragma unroll
       for (int w = 0; w < 3; w++) q[w] = r2.pile[(size_t)w * nrow + b];
-      uint64_t a0 = q[0], a1 = q[1], a2 = q[2];
-#pragma unroll 1
-      for (int i = 0; i < k1; i++) {
-        cur[(size_t)i * n + b] = r2.cur[(size_t)i * nrow + b];
-        uint32_t p9 = (uint32_t)a0 & 0x1FFu;
-        if (p9 != 0x1FFu) apply_pile(bag, p9);
-        a0 = (a0 >> 9) | (a1 << 55);
-        a1 = (a1 >> 9) | (a2 << 55);
-        a2 >>= 9;
+      // draw1's cursors over (all loads issued before the stores) and the
+      // bag replayed from its script; entries past k1 unused
+      int32_t cv[kD1Draws];
+#pragma unroll
+      for (int i = 0; i < kD1Draws; i++) cv[i] = r2.cur[(size_t)i * nrow + b];
+#pragma unroll
+      for (int i = 0; i < kD1Draws; i++)
+        if (i < k1) cur[(size_t)i * n + b] = cv[i];
+#pragma unroll
+      for (int i = 0; i < kD1Draws; i++) {
+        uint32_t p9 = (uint32_t)(q[(9 * i) >> 6] >> ((9 * i) & 63));
+        if ((9 * i & 63) > 55) p9 |= (uint32_t)(q[((9 * i) >> 6) + 1] << (64 - ((9 * i) & 63)));
+        apply_pile_fast(bag, i < k1 ? p9 & 0x1FFu : 0x1FFu);
       }
-      c0 = r2.cur[(size_t)k1 * nrow + b];
       start = k1;
     } else {
       seed_in_lds(lane, episode_seed(seed_base, b, e));
@@ -711,7 +784,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     uint32_t *__restrict__ prep_mt, int32_t *__restrict__ prep_tag,
                                                     uint64_t *__restrict__ prep_pile, int32_t *__restrict__ prep_cur,
                                                     const int32_t *__restrict__ prep_ep, Ring rs, Ring r1,
-                                                    Ring r2, long nrow) {
+                                                    Ring r2, long nrow, const uint32_t *__restrict__ ahead_rule,
+                                                    uint32_t *__restrict__ prep_rule) {
 #ifdef HZ_DIAG
   uint64_t role_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -719,8 +793,15 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     int blk = (int)blockIdx.x - nblk;
     int role = blk / nblk;
     blk -= role * nblk;
+#ifdef HZ_PREP_DELAY
+    if (role < 2) __builtin_amdgcn_s_sleep(HZ_PREP_DELAY);
+#endif
+#ifdef HZ_DIAG
+    if (g_role_only >= 0 && g_role_only != role) return;
+#endif
     if (role == 0)
-      draw2_stage(blk, r2, (size_t)nrow, prep_mt, prep_tag, prep_pile, prep_cur, prep_ep, n, seed_base, ahead_draws);
+      draw2_stage(blk, r2, (size_t)nrow, prep_mt, prep_tag, prep_pile, prep_cur, prep_rule, prep_ep, n, seed_base,
+                  ahead_draws);
     else if (role == 1)
       draw1_stage(blk, r1, (size_t)nrow, prep_ep, n, seed_base, ahead_draws);
     else
@@ -734,6 +815,9 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #endif
     return;
   }
+#ifdef HZ_DIAG
+  if (g_role_only >= 0 && g_role_only != 3) return;
+#endif
   __shared__ uint64_t s_lds_mask, s_recopy_mask;
   int tid = threadIdx.x;
   int lane = tid & 63;
@@ -746,10 +830,35 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   uint32_t *g = mt + (size_t)b0 * kMT;
   // reset_first: a board whose episode was prepared ahead plays its pile
   // script; the others seed their stream in LDS below
-  bool seeded = reset_first && act && ahead_tag && ahead_tag[b] == episode[b];
+  // the script words are read with the tag (one memory round trip); they
+  // are used only when the tag matches
+  uint64_t pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;
+  if (reset_first && act && ahead_pile && w0) {
+    pq0 = ahead_pile[b];
+    pq1 = ahead_pile[(size_t)n + b];
+    pq2 = ahead_pile[(size_t)2 * n + b];
+    pq3 = ahead_pile[(size_t)3 * n + b];
+  }
+  int ep0 = act ? episode[b] : 0;
+  bool seeded = reset_first && act && ahead_tag && ahead_tag[b] == ep0;
   uint64_t seededmask = __ballot(seeded);
+  // the episode's rule hashes into rows [0, kRulePlies) of each seeded
+  // lane's LDS column (a seeded lane replays its script and never keeps its
+  // stream in LDS), all four waves, issued with the tag loads
+  if (reset_first && ahead_rule) {
+    uint32_t hv[kRulePlies / 4];
+#pragma unroll
+    for (int j = 0; j < kRulePlies / 4; j++) hv[j] = act ? ahead_rule[(size_t)(4 * j + (tid >> 6)) * n + b] : 0u;
+    if (seeded) {
+#pragma unroll
+      for (int j = 0; j < kRulePlies / 4; j++) hz_lds[(4 * j + (tid >> 6)) * kLdsStride + lane] = hv[j];
+    }
+  }
   if (!reset_first) stage_mt(g, nb, tid, actmask, true);
   __syncthreads();
+#ifdef HZ_DIAG_ROLES_ONLY
+  if (w0 && act) HZ_PHASE(13, role_t0, b);
+#endif
   if (!w0) {
     // waves 1-3: the prepared streams become the boards' streams while wave 0 plays
     if (seededmask) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid - 64, kStageThreads - 64, seededmask);
@@ -758,22 +867,32 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                   MT(ahead_mt ? ahead_mt + (size_t)b * kMT : nullptr, 0),
                   ahead_cur ? ahead_cur + (size_t)ahead_draws * n + b : nullptr};
     if (seeded) {
-      draw.q0 = ahead_pile[b];
-      draw.q1 = ahead_pile[(size_t)n + b];
-      draw.q2 = ahead_pile[(size_t)2 * n + b];
-      draw.q3 = ahead_pile[(size_t)3 * n + b];
+      draw.q0 = pq0;
+      draw.q1 = pq1;
+      draw.q2 = pq2;
+      draw.q3 = pq3;
     }
     State s;
     int g_ply, games = 0, steps = 0;
     uint64_t sd, rkey;
     if (reset_first) {
-      int e = episode[b];
+      int e = ep0;
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
       rkey = rule_key(sd);
       episode[b] = e + 1;
       if (!seeded) mt_seed(hz_lds + lane, kLdsStride, sd);
-      reset_state(s, draw);
+      if (__all(seeded) && ahead_draws >= 5) {
+        // HarmoniesGameState() from the script: its first five entries are
+        // the opening piles (a full bag always fills them), 45 bits laid out
+        // as the piles word
+        draw.scripted_reset(s);
+      } else {
+        reset_state(s, draw);
+      }
       g_ply = 0;
+#ifdef HZ_DIAG_ROLES_ONLY
+      HZ_PHASE(8, role_t0, b);
+#endif
     } else {
       s = load_state(st, n, b);
       g_ply = ply[b];
@@ -785,6 +904,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     uint64_t acc8 = 0, acc9 = 0, acc10 = 0, acc11 = 0, acc12 = 0, acc13 = 0;
 #endif
     bool lds_used = !seeded;  // the LDS copy of the stream is live
+    bool pre = seeded && ahead_rule != nullptr;  // the episode's rule hashes are in LDS
     for (int i = 0; i < max_plies; i++) {
       if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
         if constexpr (!AutoReset) {
@@ -802,6 +922,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         draw.m = LdsMT(lane, kMTSeeded);
         draw.scripted = false;
         lds_used = true;
+        pre = false;
         reset_state(s, draw);
         g_ply = 0;
       }
@@ -809,10 +930,18 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         // a pair of whole turns at once while every board of the wave still
         // playing is at a pair boundary (always, for boards reset together)
         if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
-          play_turn<0>(s, draw, rkey, g_ply);
+          uint32_t h[8];
+          if (__all(pre && g_ply + 8 <= kRulePlies)) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) h[j] = hz_lds[(g_ply + j) * kLdsStride + lane];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) h[j] = rule_h32(rkey, g_ply + j);
+          }
+          play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
           int done = 4;
           if (phase_of(s.misc) != PH_OVER) {
-            play_turn<1>(s, draw, rkey, g_ply + 4);
+            play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
             done = 8;
           }
           g_ply += done;
@@ -853,8 +982,14 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       steps++;
       if (phase_of(s.misc) == PH_OVER) games++;
     }
+#ifdef HZ_DIAG_ROLES_ONLY
+    HZ_PHASE(9, role_t0, b);
+#endif
     // final scoring of the games that ended in this call, the whole wave at once
     if (score_pending(s.misc)) finish_game(s);
+#ifdef HZ_DIAG_ROLES_ONLY
+    HZ_PHASE(10, role_t0, b);
+#endif
     HZ_ACC(13, t0);
     store_state(st, n, b, s);
     if (lds_used) pos[b] = draw.m.cursor();
@@ -862,7 +997,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     else pos[b] = ahead_cur[(size_t)draw.d * n + b];
     ply[b] = g_ply;
     seed[b] = sd;
-#ifdef HZ_DIAG
+#if defined(HZ_DIAG) && !defined(HZ_DIAG_ROLES_ONLY)
     if (g_stamps) {
       uint64_t *o = g_stamps + (size_t)b * 16;
       o[8] = acc8; o[9] = acc9; o[10] = acc10; o[11] = acc11; o[12] = acc12; o[13] = acc13;
@@ -1017,6 +1152,7 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
          hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
+         hipMalloc(&e->ahead_rule[k], n * kRulePlies * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
@@ -1046,6 +1182,7 @@ void hz_env_destroy(hz_env *e) {
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
     if (e->ahead_pile[k]) (void)hipFree(e->ahead_pile[k]);
     if (e->ahead_cur[k]) (void)hipFree(e->ahead_cur[k]);
+    if (e->ahead_rule[k]) (void)hipFree(e->ahead_rule[k]);
     if (e->ep_final[k]) (void)hipFree(e->ep_final[k]);
   }
   for (int k = 0; k < kRing; k++) {
@@ -1156,6 +1293,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   const int32_t *ahead_tag = nullptr;
   const uint64_t *ahead_pile = nullptr;
   const int32_t *ahead_cur = nullptr;
+  const uint32_t *ahead_rule = nullptr;
   int32_t *ep_final = nullptr;
   int nblk = grid_for(e->n), grid = nblk;
   bool pipe = reset_first && e->seed_ahead > 0;
@@ -1175,6 +1313,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
       ahead_tag = e->ahead_tag[r];
       ahead_pile = e->ahead_pile[r];
       ahead_cur = e->ahead_cur[r];
+      ahead_rule = e->ahead_rule[r];
     }
     ep_final = e->ep_final[r];
     grid = 4 * nblk;
@@ -1189,7 +1328,7 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
                      e->ahead_cur[w], e->ep_final[w], ring(c3), ring((c3 + 2) % kRing), ring((c3 + 1) % kRing),
-                     (long)e->nrow);
+                     (long)e->nrow, ahead_rule, e->ahead_rule[w]);
   int err = launch_err();
   if (err) return err;
   if (pipe) {
@@ -1265,6 +1404,9 @@ const char *hz_version(void) { return "hz 0.1 gfx950"; }
 #ifdef HZ_DIAG
 int hz_diag_set_stamps(uint64_t *p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+int hz_diag_set_role_only(int r) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_role_only), &r, sizeof(r)) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -48,6 +48,10 @@ out.update({"play_primed_us": f0.elapsed_time(f1) * 1e3,
             "role_seed_cyc_max": s[:, 7].max().item(),
             # preparation phases, cycles since the role began (max over boards)
             "role_draw1_cyc_max": s[:, 15].max().item(),
+            # play role (roles build): cycles since the role began, max over boards
+            "play_after_barrier": s[:, 13].max().item(), "play_after_reset": s[:, 8].max().item(), "play_after_loop": s[:, 9].max().item(),
+            "play_after_final_scoring": s[:, 10].max().item(),
+            "seed_waves13_overlap_done": s[:, 11].max().item(), "seed_after_barrier": s[:, 12].max().item(),
             "seed_after_seed": s[:, 0].max().item(), "seed_after_twist": s[:, 1].max().item(),
             "draw1_after_stage_in": s[:, 2].max().item(), "draw1_after_draws": s[:, 3].max().item(),
             "draw2_after_stage_in": s[:, 4].max().item(), "draw2_after_draws": s[:, 14].max().item()})
