@@ -1391,9 +1391,11 @@ __device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h
   // otherwise code + add (kAddTab), stone on one stone 4 -> 8
   uint32_t code = __builtin_amdgcn_ubfe(b0, c, 1) | (__builtin_amdgcn_ubfe(b1, c, 1) << 1) |
                   (__builtin_amdgcn_ubfe(b2, c, 1) << 2) | (__builtin_amdgcn_ubfe(b3, c, 1) << 3);
+  // (as arithmetic on 0/1 values: a select here was sunk into a branch)
   uint32_t add = __builtin_amdgcn_ubfe(kAddTab, 4 * tile, 4);
-  add += (code == 4u && add == 1u) ? 3u : 0u;
-  uint32_t nc = code == 0u ? 1u + tile : code + add;
+  uint32_t empty = (uint32_t)(code == 0u);
+  add += 3u * ((uint32_t)(code == 4u) & (uint32_t)(add == 1u));
+  uint32_t nc = code + add + empty * (1u + tile - add);  // empty: 0 + (1 + tile)
   uint32_t d = code ^ nc;
   uint32_t bit = 1u << c;
   b0 ^= bit & (0u - (d & 1u));
@@ -1417,16 +1419,19 @@ __device__ __forceinline__ void place_fast(State& s, uint32_t& hand9, uint32_t h
 
 // _end_turn_actions (:301-329) for player P after a full turn (hand empty).
 // Under turn_pair_safe the refill is at most one pile: four piles are left
-// unless the bag ran dry at an earlier refill.
-template <int P, class Draw>
+// unless the bag ran dry at an earlier refill.  Pop: the caller guarantees
+// the refill happens and comes from the draw's script (draw.pop()).
+template <int P, class Draw, bool Pop = false>
 __device__ __forceinline__ void end_turn_fast(State& s, Draw& draw) {
   uint32_t occ = half<P>(s.pl[0] | s.pl[1] | s.pl[2] | s.pl[3]);
   bool player_trigger = __popc(occ) >= kCells - 2;
   uint64_t m = s.misc;
   bool bag_empty_before = (m & (((1ull << 30) - 1) << 11)) == 0;
   int np = npiles_of(s.piles);
-  bool want = np < 5 && !bag_empty_before;
-  uint32_t pile9 = draw.take(m, want);  // a full pile (the bag holds a multiple of three); 0x1FF if !want
+  bool want = Pop || (np < 5 && !bag_empty_before);
+  uint32_t pile9;  // a full pile (the bag holds a multiple of three); 0x1FF if !want
+  if constexpr (Pop) pile9 = draw.pop();
+  else pile9 = draw.take(m, want);
   apply_pile_fast(m, pile9);
   uint64_t refilled = (s.piles & ~((0x1FFull << (9 * np)) | (7ull << 45))) | ((uint64_t)pile9 << (9 * np)) |
                       ((uint64_t)(np + 1) << 45);
@@ -1453,7 +1458,7 @@ __device__ __forceinline__ uint32_t turn_rule(uint64_t rkey, int ply) {
   return CheapRule ? ((uint32_t)rkey + (uint32_t)ply) * 0x9E3779B9u : rule_h32(rkey, ply);
 }
 // ... given the four rule hashes of its plies (h[j] for ply g_ply + j)
-template <int P, class Draw>
+template <int P, class Draw, bool Pop = false>
 __device__ __forceinline__ void play_turn_h(State& s, Draw& draw, uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3) {
   uint32_t hand9;
   {  // choose_pile: the pile leaves the row, later piles shift down (:221)
@@ -1468,7 +1473,7 @@ __device__ __forceinline__ void play_turn_h(State& s, Draw& draw, uint32_t h0, u
   place_fast<P, 2>(s, hand9, h2);
   place_fast<P, 1>(s, hand9, h3);
   s.misc = (s.misc & ~0x7FFull) | 0x1FFull;  // empty hand
-  end_turn_fast<P>(s, draw);
+  end_turn_fast<P, Draw, Pop>(s, draw);
 }
 template <int P, class Draw, bool CheapRule = false>
 __device__ __forceinline__ void play_turn(State& s, Draw& draw, uint64_t rkey, int g_ply) {

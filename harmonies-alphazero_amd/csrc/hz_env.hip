@@ -360,6 +360,21 @@ struct PlayDraw {
     return o.p9;
   }
 
+  // the next script entry, unconditionally (the caller checked d < nd)
+  __device__ __forceinline__ uint32_t pop() {
+    uint32_t p9 = (uint32_t)q0 & 0x1FFu;
+    q0 = (q0 >> 9) | (q1 << 55);
+    q1 = (q1 >> 9) | (q2 << 55);
+    q2 = (q2 >> 9) | (q3 << 55);
+    q3 >>= 9;
+    d++;
+    return p9;
+  }
+  // both refills of a turn pair come from the script: two entries left (a
+  // script holds <= 24 draws, so the bag still has >= 48 tiles and every
+  // turn end refills exactly one pile)
+  __device__ __forceinline__ bool pair_pops() const { return scripted && d + 2 <= nd; }
+
   // reset_state when the lane replays a script of >= 5 entries
   __device__ __forceinline__ void scripted_reset(State &s) {
     s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
@@ -938,11 +953,19 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #pragma unroll
             for (int j = 0; j < 8; j++) h[j] = rule_h32(rkey, g_ply + j);
           }
-          play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
           int done = 4;
-          if (phase_of(s.misc) != PH_OVER) {
-            play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
-            done = 8;
+          if (__all(draw.pair_pops())) {  // the refills are plain pops
+            play_turn_h<0, PlayDraw, true>(s, draw, h[0], h[1], h[2], h[3]);
+            if (phase_of(s.misc) != PH_OVER) {
+              play_turn_h<1, PlayDraw, true>(s, draw, h[4], h[5], h[6], h[7]);
+              done = 8;
+            }
+          } else {
+            play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
+            if (phase_of(s.misc) != PH_OVER) {
+              play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
+              done = 8;
+            }
           }
           g_ply += done;
           steps += done;
