@@ -108,6 +108,33 @@ __device__ __forceinline__ uint32_t pass1_ldstab(uint32_t *w, int stride, const 
   return prev;
 }
 
+// pass 2 alone over an already seeded column: Mode 0 as mt_seed_tab, 1 no
+// stores (values folded into a register), 2 no loads (a register stands in)
+template <int Mode>
+__device__ __forceinline__ uint32_t pass2(uint32_t *w, uint32_t prev) {
+  constexpr int S = 64;
+  uint32_t acc = 0;
+  uint32_t cur[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) cur[u] = Mode == 2 ? prev + u : w[(2 + u) * S];
+#pragma unroll 2
+  for (int g = 2; g < kMT - 6; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = Mode == 2 ? cur[u] ^ 0x9e3779b9u : w[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
+      if (Mode == 1) acc ^= v;
+      else w[(g + u) * S] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
+  }
+  return prev ^ acc;
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) k_seedvar(uint32_t *out, uint64_t *cyc) {
   extern __shared__ uint32_t lds[];
@@ -124,6 +151,11 @@ __global__ void __launch_bounds__(64) k_seedvar(uint32_t *out, uint64_t *cyc) {
   if constexpr (V == 2) r = pass1<false>(hz_lds + lane, 64, kA, kB);
   if constexpr (V == 3) r = pass1_ldstab(hz_lds + lane, 64, tab, kA, kB);
   if constexpr (V == 4) mt_seed_tab<64>(hz_lds + lane, tab, sd);
+  if constexpr (V >= 8 && V <= 10) {
+    mt_seed_tab<64>(hz_lds + lane, tab, sd);
+    t0 = __builtin_amdgcn_s_memtime();
+    r = pass2<V - 8>(hz_lds + lane, kA);
+  }
   if constexpr (V == 5) mt_seed_tab<65>(hz_lds + lane, tab, sd);
   uint64_t t1 = __builtin_amdgcn_s_memtime();
   out[blockIdx.x * 64 + lane] = r ^ hz_lds[7 * 64 + lane];
@@ -140,6 +172,9 @@ extern "C" int seed_var(int v, void *out, void *cyc, int blocks) {
     hipFuncSetAttribute((const void *)k_seedvar<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void *)k_seedvar<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void *)k_seedvar<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<9>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void *)k_seedvar<10>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     init = true;
   }
   switch (v) {
@@ -150,6 +185,9 @@ extern "C" int seed_var(int v, void *out, void *cyc, int blocks) {
     case 4: hipLaunchKernelGGL(k_seedvar<4>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
     case 6: hipLaunchKernelGGL(k_seedvar<0>, dim3(256), b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
     case 7: hipLaunchKernelGGL(k_seedvar<4>, dim3(256), b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 8: hipLaunchKernelGGL(k_seedvar<8>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 9: hipLaunchKernelGGL(k_seedvar<9>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
+    case 10: hipLaunchKernelGGL(k_seedvar<10>, g, b, lds, 0, (uint32_t *)out, (uint64_t *)cyc); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;

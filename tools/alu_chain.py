@@ -21,13 +21,14 @@ print(json.dumps(res))
 sv = {}
 outs = {}
 for v, nm in [(0, "mt_seed_lds"), (1, "pass1_lds"), (2, "pass1_nostore"), (3, "pass1_ldstab"), (4, "mt_seed_tab64"),
-              (6, "mt_seed_lds_256blk"), (7, "mt_seed_tab64_256blk")]:
+              (6, "mt_seed_lds_256blk"), (7, "mt_seed_tab64_256blk"), (8, "pass2_as_is"), (9, "pass2_nostore"),
+              (10, "pass2_noload")]:
     out = torch.zeros(256 * 64, dtype=torch.int32, device="cuda")
     cyc = torch.zeros(256, dtype=torch.int64, device="cuda")
     for _ in range(3):
         assert lib.seed_var(v, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(cyc.data_ptr()), 64) == 0
     torch.cuda.synchronize()
-    nb = 256 if v >= 6 else 64
+    nb = 256 if v in (6, 7) else 64
     sv[nm] = float(cyc[:nb].double().median().item())
     outs[nm] = out[:64 * 64].cpu().numpy()
 sv["tab_equal"] = bool((outs["mt_seed_lds"] == outs["mt_seed_tab64"]).all())
