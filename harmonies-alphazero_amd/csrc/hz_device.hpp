@@ -800,21 +800,18 @@ __device__ __forceinline__ int draw_pile(uint64_t misc, M& m, uint32_t& pile9) {
   } else {
     idx[0] = j[0]; idx[1] = j[1]; idx[2] = j[2];
   }
-  const int order[6] = {WATER, PLANT, WOOD, STONE, FIELD, BUILDING};
+  // the tile at flat index x: how many of the order's prefix counts are <= x
+  // picks the tile from the packed order (no per-tile select chain)
+  constexpr uint32_t kOrder = WATER | (PLANT << 3) | (WOOD << 6) | (STONE << 9) | (FIELD << 12) | (BUILDING << 15);
+  uint32_t e0 = (uint32_t)cnt[WATER], e1 = e0 + (uint32_t)cnt[PLANT], e2 = e1 + (uint32_t)cnt[WOOD];
+  uint32_t e3 = e2 + (uint32_t)cnt[STONE], e4 = e3 + (uint32_t)cnt[FIELD];
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    if (i >= k) break;
-    uint32_t rem = idx[i];
-    int tile = -1;
-#pragma unroll
-    for (int o = 0; o < 6; o++) {
-      int tt = order[o];
-      if (tile < 0) {
-        if (rem < (uint32_t)cnt[tt]) tile = tt;
-        else rem -= (uint32_t)cnt[tt];
-      }
-    }
-    pile9 = (pile9 & ~(7u << (3 * i))) | ((uint32_t)tile << (3 * i));
+    uint32_t x = idx[i];
+    uint32_t o = (uint32_t)(x >= e0) + (uint32_t)(x >= e1) + (uint32_t)(x >= e2) + (uint32_t)(x >= e3) +
+                 (uint32_t)(x >= e4);
+    uint32_t tile = i < k ? __builtin_amdgcn_ubfe(kOrder, 3 * o, 3) : 7u;
+    pile9 = (pile9 & ~(7u << (3 * i))) | (tile << (3 * i));
   }
   return k;
 }

@@ -445,16 +445,18 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 // per CU, every CU of the chip).  Stage k works on each board's episode k
 // calls ahead (the episode counter the previous launch left, plus k):
 //   seed  (k = 3) blocks [3 nblk, 4 nblk): the stream seeded in LDS and
-//     stored to a word-major ring slot (most rows by waves 1-3 while wave 0
-//     still seeds), rows [0, kAheadTwist) twisted on the way (every source
-//     still old: no serial chain);
-//   draw1 (k = 2) blocks [2 nblk, 3 nblk): the slot's twisted rows staged
-//     into LDS, the first kD1Draws pile draws run (a lane stops at a draw
-//     that would twist past the staged rows; the next stage redoes it), the
-//     partial script, cursors and draw count written beside the slot;
-//   draw2 (k = 1) blocks [nblk, 2 nblk): the whole slot staged, the
-//     remaining draws run, and stream (board-major), script, cursors and tag
-//     written to the play slot the next call's playing blocks replay.
+//     stored as seeded to a word-major ring slot (waves 1-3 store rows while
+//     wave 0 still seeds);
+//   draw1 (k = 2) blocks [2 nblk, 3 nblk): the rows the twist of rows
+//     [0, kAheadTwist) reads staged into LDS and twisted there (every
+//     source still old: no serial chain), the first kD1Draws pile draws run
+//     (a lane stops at a draw that would twist further; the next stage
+//     redoes it), the partial script, cursors and draw count written beside
+//     the slot;
+//   draw2 (k = 1) blocks [nblk, 2 nblk): the whole slot staged and twisted
+//     likewise, the remaining draws run, and stream (board-major), script,
+//     cursors and tag written to the play slot the next call's playing
+//     blocks replay.
 // Each ring slot carries one tag per board, episode * 4 + stage done, so a
 // stage only continues work its predecessor finished for the same
 // episode; otherwise it redoes the earlier stages itself in LDS.  A slot's
@@ -533,7 +535,7 @@ __device__ __forceinline__ int run_script(StreamDraw<LdsMT> &d, uint64_t &bag, u
   for (; i < to; i++) {
     uint32_t p9 = d(bag);
     if (StopOnTwist && d.m.tw != kAheadTwist) break;
-    if (p9 != 0x1FFu) apply_pile(bag, p9);
+    apply_pile_fast(bag, p9);  // 0x1FF: no tiles
     // entry i at bit 9 i of the 256-bit script (PlayDraw pops 9 bits at a time)
     int bit = 9 * i, wd = bit >> 6, off = bit & 63;
     uint64_t lo = (uint64_t)p9 << off;
@@ -559,6 +561,31 @@ __device__ __forceinline__ uint64_t episode_seed(uint64_t seed_base, int b, int 
   return seed_base + (uint64_t)b + ((uint64_t)e << 32);
 }
 
+// Rows [0, kAheadTwist) of the block's 64 LDS columns ([row][65]) replaced
+// by the next generation's: row i from rows i, i + 1 and i + 397, all
+// still old, so the rows are independent; in two halves, each read whole
+// into registers before any of it is written (row i + 1 may be another
+// thread's).  All threads of the block take part (two barriers per half).
+__device__ __forceinline__ void twist_lds(int tid) {
+  constexpr int H = kAheadTwist / 2, K = H / (kStageThreads / 64);  // 112 rows, 28 per thread
+  int col = tid & 63, r0 = tid >> 6;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint32_t v[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      int r = h * H + r0 + 4 * k;
+      v[k] = twist_word(hz_lds[r * kLdsStride + col], hz_lds[(r + 1) * kLdsStride + col],
+                        hz_lds[(r + 397) * kLdsStride + col]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; k++) hz_lds[(h * H + r0 + 4 * k) * kLdsStride + col] = v[k];
+    __syncthreads();
+  }
+}
+static_assert(kAheadTwist % 8 == 0 && kStageThreads == 256, "twist_lds row split");
+
 // a board's stream seeded and pre-twisted in its LDS column (cursor kMTAhead)
 __device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
   mt_seed(hz_lds + lane, kLdsStride, sd);
@@ -575,14 +602,11 @@ __device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
 // rows = 10, 18, ..., 618; published: 34, 66, ..., 610, 618.
 constexpr int kLastPub = 618;
 constexpr int kSeedChunk = (kStageThreads - 64) / 16;  // rows per pass of waves 1-3
-constexpr int kOverlapEnd = kAheadTwist + (kLastPub - kAheadTwist) / kSeedChunk * kSeedChunk;
+constexpr int kOverlapEnd = 2 + (kLastPub - 2) / kSeedChunk * kSeedChunk;
 struct SeedProgress {
   int *flag;
   __device__ __forceinline__ void operator()(int rows) const {
-#ifndef HZ_SEED_PUB_MASK
-#define HZ_SEED_PUB_MASK 31
-#endif
-    if ((rows & HZ_SEED_PUB_MASK) == 2 || rows == kLastPub) {
+    if ((rows & 31) == 2 || rows == kLastPub) {
       asm volatile("" ::: "memory");
       __hip_atomic_store(flag, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -612,24 +636,15 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   if (tid == 0) s_rows = 0;
   __syncthreads();
   // Stores: four boards of a row per thread (one 16-B LDS read, one 16-B
-  // store; a wave covers four rows).  Rows [kAheadTwist, 624) stay as
-  // seeded; rows [0, kAheadTwist) become the next generation's, twisted on
-  // the way: row i from rows i, i + 1 (<= 224) and i + 397 (<= 620), all
-  // still old, so the rows are independent and row i is ready as soon as
-  // pass 2 has made row i + 397.  Waves 1-3 store, chunk by chunk as wave 0
-  // publishes its progress, plain rows [r0, r0 + 12) and twisted rows
-  // [r0 - 397, r0 - 385) (those >= 2); after the barrier all four waves
-  // store what is left (the last rows and twisted rows 0, 1, which need
-  // row 1, final last).  Columns past n hold whatever LDS held; the next
-  // stages never read them.
+  // store; a wave covers four rows), the stream as seeded (the draw stages
+  // twist rows [0, kAheadTwist) after staging them, twist_lds).  Waves 1-3
+  // store rows [2, kOverlapEnd) chunk by chunk as wave 0 publishes its pass-2
+  // progress; after the barrier all four waves store the rest (the last
+  // rows and rows 0, 1, final last).  Columns past n hold whatever LDS held;
+  // the next stages never read them.
   int c4 = (tid & 15) * 4;
   uint32_t *out = rs.mt + (size_t)blk * kBlock + c4;
   auto row4 = [&](int r) { return *reinterpret_cast<const uint4 *>(rows + r * kSeedStride + c4); };
-  auto twisted4 = [&](int r) {
-    uint4 c = row4(r), c1 = row4(r + 1), f = row4(r + 397);
-    return uint4{twist_word(c.x, c1.x, f.x), twist_word(c.y, c1.y, f.y), twist_word(c.z, c1.z, f.z),
-                 twist_word(c.w, c1.w, f.w)};
-  };
   if (tid < 64) {
     if (act) {
       mt_seed_tab<kSeedStride>(rows + lane, tab, episode_seed(seed_base, b, e), SeedProgress{&s_rows});
@@ -638,7 +653,7 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   } else {
     int done = 0;
 #pragma unroll 1
-    for (int r0 = kAheadTwist; r0 < kOverlapEnd; r0 += kSeedChunk) {
+    for (int r0 = 2; r0 < kOverlapEnd; r0 += kSeedChunk) {
       // wave 0 publishes every row up to kLastPub; the bound only guards
       // against a hang should that ever change
       for (int spin = 0; done < r0 + kSeedChunk && spin < (1 << 22); spin++) {
@@ -647,10 +662,6 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
       }
       int r = r0 + ((tid - 64) >> 4);
       *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
-#ifndef HZ_SEED_NO_PROG_TWIST
-      int t = r - 397;
-      if (t >= 2) *reinterpret_cast<uint4 *>(out + (size_t)t * nrow) = twisted4(t);
-#endif
     }
 #ifdef HZ_DIAG_ROLES_ONLY
     if (tid < 128 && act) HZ_PHASE(11, t0, b);
@@ -660,17 +671,9 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
 #ifdef HZ_DIAG_ROLES_ONLY
   if (tid < 64 && act) HZ_PHASE(12, t0, b);
 #endif
-#ifndef HZ_SEED_NO_PROG_TWIST
-  constexpr int kTwistDone = kOverlapEnd - 397;  // twisted rows [2, kTwistDone) are stored
-#else
-  constexpr int kTwistDone = 2;
-#endif
-#pragma unroll 1
-  for (int r = kOverlapEnd + (tid >> 4); r < kMT; r += kStageThreads / 16)
-    *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
-  for (int i = tid >> 4; i < 2 + (kAheadTwist - kTwistDone); i += kStageThreads / 16) {
-    int t = i < 2 ? i : kTwistDone + i - 2;
-    *reinterpret_cast<uint4 *>(out + (size_t)t * nrow) = twisted4(t);
+  {  // rows [kOverlapEnd, 624) and 0, 1: 12 rows, one per 16-thread group
+    int i = tid >> 4, r = i < kMT - kOverlapEnd ? kOverlapEnd + i : i - (kMT - kOverlapEnd);
+    if (r < 2 || r >= kOverlapEnd) *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
   }
   if (tid < 64 && act) {
     rs.tag[b] = e * 4 + 1;
@@ -691,27 +694,33 @@ __device__ __forceinline__ void draw1_stage(int blk, Ring r1, size_t nrow, const
   int e = act ? ep_final[b] + 2 : 0;
   bool seeded = act && r1.tag[b] == e * 4 + 1;
   uint64_t smask = __ballot(seeded), fmask = __ballot(act && !seeded);  // the same in every wave
-  if (smask) stage_rows(r1.mt, nrow, b0, 0, kAheadTwist, tid);
+  // the rows the twist of rows [0, kAheadTwist) reads: [0, 225), [397, 621)
+  if (smask) {
+    stage_rows(r1.mt, nrow, b0, 0, kAheadTwist + 1, tid);
+    stage_rows(r1.mt, nrow, b0, 397, 397 + kAheadTwist, tid);
+  }
+  // boards the seed stage missed: seeded here, their stream (as seeded,
+  // like the seed stage's) to the slot
+  if (tid < 64 && act && !seeded) mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e));
   __syncthreads();
+  if (fmask) unstage_rows(r1.mt, nrow, b0, tid, fmask);
+  twist_lds(tid);
   if (tid < 64 && act) {
     HZ_PHASE(2, t0, b);
-    if (!seeded) seed_in_lds(lane, episode_seed(seed_base, b, e));
     StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
     int32_t *cur = r1.cur + b;
     cur[0] = kMTAhead;
     int k = draws < kD1Draws ? draws : kD1Draws;
-    // a seeded lane holds only the twisted rows: it stops before a twist
-    int k1 = seeded ? run_script<true>(d, bag, q, cur, nrow, 0, k) : run_script<false>(d, bag, q, cur, nrow, 0, k);
+    // only the twisted rows are live: a lane stops before a draw that would
+    // twist further (draw2, holding the whole stream, redoes it), so the
+    // slot's stream stays as seeded and every cursor's tw is kAheadTwist
+    int k1 = run_script<true>(d, bag, q, cur, nrow, 0, k);
 #pragma unroll
     for (int w = 0; w < 3; w++) r1.pile[(size_t)w * nrow + b] = q[w];
     r1.k1[b] = k1;
     r1.tag[b] = e * 4 + 2;
     HZ_PHASE(3, t0, b);
-  }
-  if (fmask) {  // boards seeded here: their whole stream to the slot
-    __syncthreads();
-    unstage_rows(r1.mt, nrow, b0, tid, fmask);
   }
 }
 
@@ -735,6 +744,7 @@ __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint3
   uint64_t okmask = __ballot(ok);
   if (okmask) stage_rows(r2.mt, nrow, b0, 0, kMT, tid);
   __syncthreads();
+  twist_lds(tid);  // the slot holds the stream as seeded; draw1's cursors say 224 rows twisted
   if (tid < 64 && act) HZ_PHASE(4, t0, b);
   if (tid >= 64 && act) {  // waves 1-3, while wave 0 draws: the episode's rule hashes
     uint64_t rk = rule_key(episode_seed(seed_base, b, e));

@@ -124,13 +124,14 @@ int hz_rollout(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *tra
                int32_t *steps_done);
 /* hz_reset (all boards) fused with hz_rollout in one launch: the chance
  * streams are seeded and consumed in LDS and written to HBM once.  With
- * chance-ahead on (the default), extra blocks of the same launch prepare,
- * concurrently with the play, every board's next episode: its stream seeded
- * and its first piles drawn (a game's draws do not depend on its moves);
- * the next call replays those piles instead of seeding and drawing
- * (identical results; a board whose episode counter was moved by anything
- * else seeds in place, a game needing more piles continues on the prepared
- * stream). */
+ * chance-ahead on (the default), the other blocks of the same launch run,
+ * concurrently with the play, a three-stage pipeline over every board's
+ * next episodes (a game's chance draws and the benchmark rule's hashes do
+ * not depend on its moves): the stream seeded three calls ahead, its piles
+ * drawn two and one calls ahead, with the rule hashes; a call replays the
+ * prepared piles instead of seeding and drawing (identical results; a board
+ * whose episode counter was moved by anything else seeds in place, a game
+ * needing more piles continues on the prepared stream). */
 int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state,
             uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done,
             int32_t *steps_done);

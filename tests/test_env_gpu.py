@@ -188,6 +188,18 @@ def test_play_seed_ahead_pipeline(Env, ahead, draws):
         _check_episode(env, base, ep, steps)
 
 
+def test_play_pipeline_partial_block(Env):
+    """hz_play's pipeline with a board count that leaves a partial block
+    (1000 = 15 x 64 + 40): ring slots padded to whole blocks, play slots
+    unpadded; six consecutive calls (the last three fully prepared), every
+    game bit-exact."""
+    n, base = 1000, 777
+    env = Env(n, seed_base=base, device=DEV)
+    for ep in range(6):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+
+
 def test_play_after_auto_reset_mispredicts_safely(Env):
     """hz_play with auto_reset moves episode counters by a board-dependent
     amount, so the concurrent seed-ahead guesses wrong for some boards: the
