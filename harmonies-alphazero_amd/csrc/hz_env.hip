@@ -447,9 +447,9 @@ __device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const u
 //   seed  (k = 3) blocks [3 nblk, 4 nblk): the stream seeded in LDS and
 //     stored as seeded to a word-major ring slot (waves 1-3 store rows while
 //     wave 0 still seeds);
-//   draw1 (k = 2) blocks [2 nblk, 3 nblk): the rows the twist of rows
-//     [0, kAheadTwist) reads staged into LDS and twisted there (every
-//     source still old: no serial chain), the first kD1Draws pile draws run
+//   draw1 (k = 2) blocks [2 nblk, 3 nblk): rows [0, kAheadTwist) staged
+//     into LDS twisted on the way in (every source still old: no serial
+//     chain), the first kD1Draws pile draws run
 //     (a lane stops at a draw that would twist further; the next stage
 //     redoes it), the partial script, cursors and draw count written beside
 //     the slot;
@@ -561,30 +561,39 @@ __device__ __forceinline__ uint64_t episode_seed(uint64_t seed_base, int b, int 
   return seed_base + (uint64_t)b + ((uint64_t)e << 32);
 }
 
-// Rows [0, kAheadTwist) of the block's 64 LDS columns ([row][65]) replaced
-// by the next generation's: row i from rows i, i + 1 and i + 397, all
-// still old, so the rows are independent; in two halves, each read whole
-// into registers before any of it is written (row i + 1 may be another
-// thread's).  All threads of the block take part (two barriers per half).
-__device__ __forceinline__ void twist_lds(int tid) {
-  constexpr int H = kAheadTwist / 2, K = H / (kStageThreads / 64);  // 112 rows, 28 per thread
-  int col = tid & 63, r0 = tid >> 6;
+// Rows [0, kAheadTwist) of the block's 64 boards from a slot holding the
+// streams as seeded, word-major HBM -> LDS [row][65], written as the next
+// generation's: row i from rows i, i + 1 and i + 397 of the slot (all still
+// old), read straight from HBM (16 B per load, 12 in flight per thread), so
+// the twist needs no LDS round trip and no barrier.
+__device__ __forceinline__ void stage_rows_twisted(const uint32_t *__restrict__ slot, size_t nrow, int b0, int tid) {
+  constexpr int U = 4;
+  constexpr int total = kAheadTwist * 16;
+  for (int q0 = 0; q0 < total; q0 += kStageThreads * U) {
+    uint4 c[U], c1[U], f[U];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    uint32_t v[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      int r = h * H + r0 + 4 * k;
-      v[k] = twist_word(hz_lds[r * kLdsStride + col], hz_lds[(r + 1) * kLdsStride + col],
-                        hz_lds[(r + 397) * kLdsStride + col]);
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      q = q < total ? q : total - 1;
+      const uint32_t *p = slot + b0 + (q & 15) * 4;
+      int r = q >> 4;
+      c[u] = *reinterpret_cast<const uint4 *>(p + (size_t)r * nrow);
+      c1[u] = *reinterpret_cast<const uint4 *>(p + (size_t)(r + 1) * nrow);
+      f[u] = *reinterpret_cast<const uint4 *>(p + (size_t)(r + 397) * nrow);
     }
-    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < K; k++) hz_lds[(h * H + r0 + 4 * k) * kLdsStride + col] = v[k];
-    __syncthreads();
+    for (int u = 0; u < U; u++) {
+      int q = q0 + u * kStageThreads + tid;
+      if (q < total) {
+        uint32_t *d = hz_lds + (q >> 4) * kLdsStride + (q & 15) * 4;
+        d[0] = twist_word(c[u].x, c1[u].x, f[u].x);
+        d[1] = twist_word(c[u].y, c1[u].y, f[u].y);
+        d[2] = twist_word(c[u].z, c1[u].z, f[u].z);
+        d[3] = twist_word(c[u].w, c1[u].w, f[u].w);
+      }
+    }
   }
 }
-static_assert(kAheadTwist % 8 == 0 && kStageThreads == 256, "twist_lds row split");
 
 // a board's stream seeded and pre-twisted in its LDS column (cursor kMTAhead)
 __device__ __forceinline__ void seed_in_lds(int lane, uint64_t sd) {
@@ -637,7 +646,7 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
   __syncthreads();
   // Stores: four boards of a row per thread (one 16-B LDS read, one 16-B
   // store; a wave covers four rows), the stream as seeded (the draw stages
-  // twist rows [0, kAheadTwist) after staging them, twist_lds).  Waves 1-3
+  // twist rows [0, kAheadTwist) as they stage them, stage_rows_twisted).  Waves 1-3
   // store rows [2, kOverlapEnd) chunk by chunk as wave 0 publishes its pass-2
   // progress; after the barrier all four waves store the rest (the last
   // rows and rows 0, 1, final last).  Columns past n hold whatever LDS held;
@@ -694,19 +703,22 @@ __device__ __forceinline__ void draw1_stage(int blk, Ring r1, size_t nrow, const
   int e = act ? ep_final[b] + 2 : 0;
   bool seeded = act && r1.tag[b] == e * 4 + 1;
   uint64_t smask = __ballot(seeded), fmask = __ballot(act && !seeded);  // the same in every wave
-  // the rows the twist of rows [0, kAheadTwist) reads: [0, 225), [397, 621)
-  if (smask) {
-    stage_rows(r1.mt, nrow, b0, 0, kAheadTwist + 1, tid);
-    stage_rows(r1.mt, nrow, b0, 397, 397 + kAheadTwist, tid);
-  }
+  // rows [0, kAheadTwist), twisted on the way in
+  if (smask) stage_rows_twisted(r1.mt, nrow, b0, tid);
   // boards the seed stage missed: seeded here, their stream (as seeded,
-  // like the seed stage's) to the slot
+  // like the seed stage's) to the slot, then twisted in place
   if (tid < 64 && act && !seeded) mt_seed(hz_lds + lane, kLdsStride, episode_seed(seed_base, b, e));
   __syncthreads();
-  if (fmask) unstage_rows(r1.mt, nrow, b0, tid, fmask);
-  twist_lds(tid);
+  if (fmask) {
+    unstage_rows(r1.mt, nrow, b0, tid, fmask);
+    __syncthreads();
+  }
   if (tid < 64 && act) {
     HZ_PHASE(2, t0, b);
+    if (!seeded) {
+      LdsMT m(lane, kMTSeeded);
+      m.twist_ahead(kAheadTwist);
+    }
     StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
     int32_t *cur = r1.cur + b;
@@ -742,9 +754,11 @@ __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint3
   int e = act ? ep_final[b] + 1 : 0;
   bool ok = act && r2.tag[b] == e * 4 + 2;
   uint64_t okmask = __ballot(ok);
-  if (okmask) stage_rows(r2.mt, nrow, b0, 0, kMT, tid);
+  if (okmask) {  // the slot holds the stream as seeded; draw1's cursors say 224 rows twisted
+    stage_rows_twisted(r2.mt, nrow, b0, tid);
+    stage_rows(r2.mt, nrow, b0, kAheadTwist, kMT, tid);
+  }
   __syncthreads();
-  twist_lds(tid);  // the slot holds the stream as seeded; draw1's cursors say 224 rows twisted
   if (tid < 64 && act) HZ_PHASE(4, t0, b);
   if (tid >= 64 && act) {  // waves 1-3, while wave 0 draws: the episode's rule hashes
     uint64_t rk = rule_key(episode_seed(seed_base, b, e));
