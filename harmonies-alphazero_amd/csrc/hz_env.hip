@@ -33,7 +33,7 @@ struct hz_env {
   int32_t *ahead_tag[2];     // [n] episode each slot holds (-1: none)
   uint64_t *ahead_pile[2];   // [kAheadWords][n] prepared pile scripts
   int32_t *ahead_cur[2];     // [kAheadDraws + 1][n] stream cursor after each scripted draw
-  uint32_t *ahead_rule[2];   // [kRulePlies][n] rule hashes (top 32 bits) per ply
+  uint32_t *ahead_rule[2];   // [kRulePlies][nrow] rule hashes (top 32 bits) per ply
   int32_t *ep_final[2];      // [n] episode counter after the k_rollout that read the slot
   size_t nrow;               // n rounded up to 64: row stride of the ring slots
   uint32_t *ring_mt[3];      // [624][nrow] word-major streams, three calls / two calls ahead
@@ -763,7 +763,7 @@ __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint3
   if (tid >= 64 && act) {  // waves 1-3, while wave 0 draws: the episode's rule hashes
     uint64_t rk = rule_key(episode_seed(seed_base, b, e));
 #pragma unroll 1
-    for (int j = (tid >> 6) - 1; j < kRulePlies; j += 3) rule[(size_t)j * n + b] = rule_h32(rk, j);
+    for (int j = (tid >> 6) - 1; j < kRulePlies; j += 3) rule[(size_t)j * nrow + b] = rule_h32(rk, j);
   }
   if (tid < 64 && act) {
     uint64_t bag = initial_bag(), q[kAheadWords] = {};
@@ -884,13 +884,25 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   // the episode's rule hashes into rows [0, kRulePlies) of each seeded
   // lane's LDS column (a seeded lane replays its script and never keeps its
   // stream in LDS), all four waves, issued with the tag loads
+  // (16-B loads: four boards of a row per thread; an unseeded lane's column
+  // is overwritten by its seeding after the barrier)
   if (reset_first && ahead_rule) {
-    uint32_t hv[kRulePlies / 4];
+    constexpr int K = kRulePlies * 16 / kStageThreads;
+    static_assert(kRulePlies * 16 % kStageThreads == 0, "hash rows per pass");
+    uint4 hv[K];
 #pragma unroll
-    for (int j = 0; j < kRulePlies / 4; j++) hv[j] = act ? ahead_rule[(size_t)(4 * j + (tid >> 6)) * n + b] : 0u;
-    if (seeded) {
+    for (int k = 0; k < K; k++) {
+      int q = k * kStageThreads + tid;
+      hv[k] = *reinterpret_cast<const uint4 *>(ahead_rule + (size_t)(q >> 4) * nrow + b0 + (q & 15) * 4);
+    }
 #pragma unroll
-      for (int j = 0; j < kRulePlies / 4; j++) hz_lds[(4 * j + (tid >> 6)) * kLdsStride + lane] = hv[j];
+    for (int k = 0; k < K; k++) {
+      int q = k * kStageThreads + tid;
+      uint32_t *d = hz_lds + (q >> 4) * kLdsStride + (q & 15) * 4;
+      d[0] = hv[k].x;
+      d[1] = hv[k].y;
+      d[2] = hv[k].z;
+      d[3] = hv[k].w;
     }
   }
   if (!reset_first) stage_mt(g, nb, tid, actmask, true);
@@ -1199,7 +1211,8 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
          hipMalloc(&e->ahead_tag[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMalloc(&e->ahead_pile[k], n * kAheadWords * sizeof(uint64_t)) == hipSuccess &&
          hipMalloc(&e->ahead_cur[k], n * (kAheadDraws + 1) * sizeof(int32_t)) == hipSuccess &&
-         hipMalloc(&e->ahead_rule[k], n * kRulePlies * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc(&e->ahead_rule[k], (n + kBlock - 1) / kBlock * kBlock * kRulePlies * sizeof(uint32_t)) ==
+             hipSuccess &&
          hipMalloc(&e->ep_final[k], n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ahead_tag[k], 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
