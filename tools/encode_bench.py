@@ -29,3 +29,17 @@ torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / R
 res.update({"ms": ms, "GBps": M * 5488 / (ms * 1e-3) / 1e9, "frac_of_8TBps": M * 5488 / (ms * 1e-3) / 8e12})
 print(json.dumps(res))
+# the store ceiling for the same bytes: torch's fill kernel and a memset
+buf = torch.empty(M * 5488 // 4, dtype=torch.float32, device=dev)
+for name, fn in (("fill", lambda: buf.fill_(1.0)), ("zero", lambda: buf.zero_())):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(R):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms2 = e0.elapsed_time(e1) / R
+    res[f"{name}_GBps"] = buf.numel() * 4 / (ms2 * 1e-3) / 1e9
+print(json.dumps(res))
