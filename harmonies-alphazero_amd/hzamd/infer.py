@@ -10,14 +10,33 @@ BatchNorm into the preceding conv's weights and bias once,
     W' = W * g / sqrt(var + eps),   b' = (b - mean) * g / sqrt(var + eps) + beta,
 
 keeps activations NHWC (channels_last: MIOpen's implicit-GEMM NHWC conv runs
-at ~106 TFLOP/s fp32 here, NCHW Winograd at ~82) and applies bias / residual
-add / ReLU in place.  Arithmetic stays fp32; the results differ from the
-unfolded graph only by fp32 rounding (tests/test_infer_gpu.py states the
-tolerance).  Rebuild (or call refresh()) after the weights change.
+at ~132 TFLOP/s fp32 here, NCHW Winograd at ~82) and runs each 3x3 conv
+without bias, followed by one HIP pass (`hz_bias_act`, csrc/hz_net.hip) that
+adds the bias, the residual and applies the ReLU in place (PyTorch would make
+three passes over the activation: bias add, add_, relu_).  Arithmetic stays
+fp32; the results differ from the unfolded graph only by fp32 rounding
+(tests/test_infer_gpu.py states the tolerance).  Rebuild (or call refresh())
+after the weights change.
 """
 import torch
 import torch.nn.functional as F
 from torch import nn
+
+from ._native import NativeError, lib
+
+
+def _bias_act(x, b, res=None):
+    """x = relu(x + b[c] (+ res)) in place over an NHWC activation."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)):
+        raise NativeError("hz_bias_act needs a CUDA fp32 channels_last activation")
+    if res is not None and (res.shape != x.shape or res.stride() != x.stride()):
+        raise NativeError("hz_bias_act: residual layout differs from the activation")
+    ch = x.shape[1]
+    rc = lib().hz_bias_act(x.data_ptr(), b.data_ptr(), res.data_ptr() if res is not None else None,
+                           x.numel() // ch, ch, torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_bias_act failed ({rc})")
+    return x
 
 
 def _fold(conv, bn):
@@ -31,11 +50,16 @@ def _fold(conv, bn):
 class FoldedNet(nn.Module):
     """Eval-mode HarmoniesNet (or the reference AlphaZeroModel: same module
     names) with BatchNorm folded into the convs; forward(board, glob) ->
-    (logits [B,143], value [B,1]) like the source network."""
+    (logits [B,143], value [B,1]) like the source network.
 
-    def __init__(self, net):
+    `epilogue(x, b, res=None)` is the bias [+ skip] + ReLU pass; the default
+    is the HIP kernel (CUDA fp32 activations only; no CPU path).  Tests pass
+    a plain-torch restatement to check the folding algebra on the CPU."""
+
+    def __init__(self, net, epilogue=None):
         super().__init__()
         self.src = net
+        self.epilogue = epilogue or _bias_act
         self.refresh()
 
     @torch.no_grad()
@@ -52,11 +76,12 @@ class FoldedNet(nn.Module):
     @torch.no_grad()
     def forward(self, board, glob):
         x = board.contiguous(memory_format=torch.channels_last)
+        ep = self.epilogue
         w, b = self.stem
-        x = F.conv2d(x, w, b, padding=1).relu_()
+        x = ep(F.conv2d(x, w, None, padding=1), b)
         for (w1, b1), (w2, b2) in self.blocks:
-            y = F.conv2d(x, w1, b1, padding=1).relu_()
-            x = F.conv2d(y, w2, b2, padding=1).add_(x).relu_()
+            y = ep(F.conv2d(x, w1, None, padding=1), b1)
+            x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
         w, b = self.pconv
         p = F.conv2d(x, w, b).relu_().flatten(1)               # NCHW order, as model.py flattens
         logits = F.linear(torch.cat((p, glob), 1), *self.pfc)

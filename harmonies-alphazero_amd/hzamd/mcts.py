@@ -143,8 +143,10 @@ class BatchedPredictor:
     @torch.no_grad()
     def __call__(self, board, glob):
         self.model.eval()
-        net = self.fast if self.fast is not None else self.model
-        if self.dtype is not None and self.dtype != torch.float32:
+        low = self.dtype is not None and self.dtype != torch.float32
+        # the folded net's HIP epilogue is fp32-only; autocast runs the source net
+        net = self.fast if self.fast is not None and not low else self.model
+        if low:
             with torch.autocast(device_type="cuda", dtype=self.dtype):
                 logits, value = net(board, glob)
         else:

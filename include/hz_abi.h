@@ -183,6 +183,13 @@ int hz_mcts_stats(hz_mcts *mcts, int32_t *counts);
 /* host pointers to the device arrays leaf[n] / leaf_gidx[n] (debugging) */
 int hz_mcts_leaf_ptrs(hz_mcts *mcts, int32_t **leaf, int32_t **leaf_gidx);
 
+/* ---- leaf-eval epilogue (hzamd/infer.py) ---------------------------------- */
+/* x[rows][ch] = relu((x + bias[c]) + res) in place (res may be NULL): the
+ * eval-mode BatchNorm (folded into the conv) -> [+ skip] -> ReLU tail of
+ * model.py:376-393 (ResidualBlock.forward) and model.py:325-330 (stem) over an
+ * NHWC activation.  ch % 4 == 0, pointers 16-byte aligned. */
+int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int32_t ch, void *stream);
+
 /* ---- build info ---------------------------------------------------------- */
 const char *hz_version(void);
 

@@ -1,10 +1,20 @@
-"""FoldedNet (BatchNorm folded into the convs, NHWC) computes the eval-mode
+"""FoldedNet (BatchNorm folded into the convs, NHWC; its HIP epilogue
+restated in torch here) computes the eval-mode
 reference network up to fp32 rounding: max |diff| <= 1e-4 on logits and
 values (non-trivial BatchNorm statistics, default 128x8 architecture)."""
 import torch
 
 from hzamd.infer import FoldedNet
 from hzamd.net import TINY, HarmoniesNet
+
+
+def torch_epilogue(x, b, res=None):
+    """Plain-torch restatement of hz_bias_act (the HIP epilogue FoldedNet
+    uses on the GPU): relu((x + b[c]) + res)."""
+    x = x + b.view(1, -1, 1, 1)
+    if res is not None:
+        x = x + res
+    return x.relu()
 
 
 def _randomise_bn(net, g):
@@ -26,7 +36,7 @@ def _check(cfg, B):
     glob = torch.rand(B, 42, generator=g)
     with torch.no_grad():
         l0, v0 = net(board, glob)
-        l1, v1 = FoldedNet(net)(board, glob)
+        l1, v1 = FoldedNet(net, torch_epilogue)(board, glob)
     assert l1.shape == l0.shape and v1.shape == v0.shape
     assert (l1 - l0).abs().max().item() <= 1e-4
     assert (v1 - v0).abs().max().item() <= 1e-4
@@ -43,7 +53,7 @@ def test_folded_matches_eval_tiny():
 def test_refresh_tracks_weight_updates():
     torch.manual_seed(1)
     net = HarmoniesNet(TINY).eval()
-    f = FoldedNet(net)
+    f = FoldedNet(net, torch_epilogue)
     with torch.no_grad():
         net.conv.weight.mul_(1.5)
     f.refresh()

@@ -29,3 +29,30 @@ def test_folded_gpu_matches_cpu_reference():
     p, v = BatchedPredictor(gnet)(board.cuda(), glob.cuda())
     assert (p.cpu() - torch.softmax(l0, 1)).abs().max().item() <= 2e-3
     assert (v.cpu() - v0.reshape(-1)).abs().max().item() <= 2e-3
+
+
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("batch", [1, 3, 4096])
+def test_bias_act_equals_torch_passes(batch, res):
+    """hz_bias_act == the three torch passes it replaces (bias add, add_,
+    relu_) exactly: same fp32 operations in the same order."""
+    from hzamd.infer import _bias_act
+    g = torch.Generator(device="cuda").manual_seed(batch)
+    x = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(128, device="cuda", generator=g)
+    r = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last) if res else None
+    want = x + b.view(1, -1, 1, 1)
+    if res:
+        want.add_(r)
+    want.relu_()
+    got = _bias_act(x.clone(memory_format=torch.channels_last), b, r)
+    assert torch.equal(got, want)
+
+
+def test_bias_act_rejects_nchw():
+    from hzamd._native import NativeError
+    from hzamd.infer import _bias_act
+    x = torch.randn(2, 128, 5, 7, device="cuda")
+    with pytest.raises(NativeError):
+        _bias_act(x, torch.zeros(128, device="cuda"))
