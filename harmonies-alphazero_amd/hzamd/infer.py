@@ -25,6 +25,29 @@ from torch import nn
 from ._native import NativeError, lib
 
 
+def pack_conv3x3(w):
+    """[co][ci][3][3] -> [kh*3+kw][ci/8][co][ci%8], the layout hz_conv3x3_bias_act
+    reads (one 16-byte B fragment per lane)."""
+    co, ci = w.shape[0], w.shape[1]
+    return w.permute(2, 3, 1, 0).reshape(9, ci // 8, 8, co).permute(0, 1, 3, 2).contiguous()
+
+
+def _conv3x3_act(x, wpack, b, res=None):
+    """relu((conv3x3(x) + b) + res) for a 128-channel NHWC activation, one HIP launch."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_conv3x3_bias_act needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    if res is not None and (res.shape != x.shape or res.stride() != x.stride()):
+        raise NativeError("hz_conv3x3_bias_act: residual layout differs from the activation")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    rc = lib().hz_conv3x3_bias_act(x.data_ptr(), wpack.data_ptr(), b.data_ptr(),
+                                   res.data_ptr() if res is not None else None, out.data_ptr(), x.shape[0],
+                                   torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_conv3x3_bias_act failed ({rc})")
+    return out
+
+
 def _bias_act(x, b, res=None):
     """x = relu(x + b[c] (+ res)) in place over an NHWC activation."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)):
@@ -56,10 +79,11 @@ class FoldedNet(nn.Module):
     is the HIP kernel (CUDA fp32 activations only; no CPU path).  Tests pass
     a plain-torch restatement to check the folding algebra on the CPU."""
 
-    def __init__(self, net, epilogue=None):
+    def __init__(self, net, epilogue=None, native_conv=True):
         super().__init__()
         self.src = net
         self.epilogue = epilogue or _bias_act
+        self.native_conv = native_conv and epilogue is None
         self.refresh()
 
     @torch.no_grad()
@@ -67,6 +91,11 @@ class FoldedNet(nn.Module):
         n = self.src
         self.stem = _fold(n.conv, n.bn)
         self.blocks = [(_fold(b.conv1, b.bn1), _fold(b.conv2, b.bn2)) for b in n.residual_blocks]
+        # the tower's 128-channel convs run as one fused HIP kernel each
+        # (conv + bias + skip + ReLU); other widths use MIOpen + hz_bias_act
+        self.packed = None
+        if self.native_conv and self.blocks and self.blocks[0][0][0].shape[:2] == (128, 128):
+            self.packed = [(pack_conv3x3(w1), pack_conv3x3(w2)) for (w1, _), (w2, _) in self.blocks]
         self.pconv = _fold(n.policy_conv, n.policy_bn)
         self.vconv = _fold(n.value_conv, n.value_bn)
         self.pfc = (n.policy_fc.weight.detach(), n.policy_fc.bias.detach())
@@ -79,9 +108,14 @@ class FoldedNet(nn.Module):
         ep = self.epilogue
         w, b = self.stem
         x = ep(F.conv2d(x, w, None, padding=1), b)
-        for (w1, b1), (w2, b2) in self.blocks:
-            y = ep(F.conv2d(x, w1, None, padding=1), b1)
-            x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
+        if self.packed is not None:
+            for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
+                y = _conv3x3_act(x, p1, b1)
+                x = _conv3x3_act(y, p2, b2, x)
+        else:
+            for (w1, b1), (w2, b2) in self.blocks:
+                y = ep(F.conv2d(x, w1, None, padding=1), b1)
+                x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
         w, b = self.pconv
         p = F.conv2d(x, w, b).relu_().flatten(1)               # NCHW order, as model.py flattens
         logits = F.linear(torch.cat((p, glob), 1), *self.pfc)

@@ -56,3 +56,46 @@ def test_bias_act_rejects_nchw():
     x = torch.randn(2, 128, 5, 7, device="cuda")
     with pytest.raises(NativeError):
         _bias_act(x, torch.zeros(128, device="cuda"))
+
+
+def _conv_ref(x, w, b, res):
+    y = torch.nn.functional.conv2d(x.double(), w.double(), None, padding=1) + b.double().view(1, -1, 1, 1)
+    if res is not None:
+        y = y + res.double()
+    return y.relu()
+
+
+@pytest.mark.parametrize("batch", [1, 13, 64])
+@pytest.mark.parametrize("res", [False, True])
+def test_conv3x3_exact_on_integer_data(batch, res):
+    """Small-integer inputs and weights: every product and partial sum is
+    exact in fp32, so hz_conv3x3_bias_act must equal the fp64 conv exactly
+    (catches any operand-layout, tap or channel-order mistake; asymmetric
+    weights so a transposed tap or swapped co/ci shows)."""
+    from hzamd.infer import _conv3x3_act, pack_conv3x3
+    g = torch.Generator().manual_seed(batch * 2 + res)
+    x = torch.randint(-3, 4, (batch, 128, 5, 7), generator=g).float()
+    w = torch.randint(-2, 3, (128, 128, 3, 3), generator=g).float()
+    b = torch.randint(-50, 50, (128,), generator=g).float()
+    r = torch.randint(-20, 20, (batch, 128, 5, 7), generator=g).float() if res else None
+    want = _conv_ref(x, w, b, r).float()
+    cl = torch.channels_last
+    got = _conv3x3_act(x.cuda().contiguous(memory_format=cl), pack_conv3x3(w).cuda(), b.cuda(),
+                       r.cuda().contiguous(memory_format=cl) if res else None)
+    assert torch.equal(got.cpu(), want)
+
+
+@pytest.mark.parametrize("batch", [8, 4096])
+def test_conv3x3_matches_miopen_float(batch):
+    """Real-valued data at the leaf-eval batch: within fp32 rounding of
+    MIOpen's conv + the torch epilogue (|diff| <= 1e-4 on O(1) outputs)."""
+    from hzamd.infer import _conv3x3_act, pack_conv3x3
+    g = torch.Generator(device="cuda").manual_seed(batch)
+    cl = torch.channels_last
+    x = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
+    w = (torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.05).contiguous(memory_format=cl)
+    b = torch.randn(128, device="cuda", generator=g) * 0.1
+    r = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=cl)
+    want = (torch.nn.functional.conv2d(x, w, b, padding=1) + r).relu()
+    got = _conv3x3_act(x, pack_conv3x3(w), b, r)
+    assert (got - want).abs().max().item() <= 1e-4
