@@ -249,6 +249,156 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
+// 8-wave form on v_mfma_f32_16x16x4_f32: the 280 rows as 18 blocks of 16
+// (the last 8 rows repeat row 279), wave w = (row half rh = w >> 2, output
+// channels 32 (w & 3) .. +32): 9 row blocks x 2 column blocks x 4 registers
+// = 72 accumulators, so two waves share each SIMD and cover each other's
+// LDS and memory waits.  A step is 16 channels of one tap: lane (r = l & 15,
+// kg = l >> 4) reads channels 16 gs + 4 kg .. +3 of its row with one 16-B
+// LDS read and MFMA j takes channel 16 gs + 4 kg + j (B alike, weights
+// packed [tap][ci/16][co][ci%16]).
+constexpr int kStage8 = (kRows * 8 + 511) / 512;  // float4 per thread per chunk (5)
+
+__global__ void __launch_bounds__(512, 1)
+    k_conv3x3_w8(const float *__restrict__ x, const float4 *__restrict__ wp, const float *__restrict__ bias,
+                 const float *__restrict__ res, float *__restrict__ out, int32_t batch) {
+  extern __shared__ float4 lds4[];
+  float *lds = (float *)lds4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
+  const int s0 = blockIdx.x * kCS;
+  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+
+  for (int i = t; i < 2 * kCS * 63; i += 512) {
+    int pc = i % 63, ph = pc / 9, pw = pc - 9 * ph;
+    if (ph == 0 || ph == 6 || pw == 0 || pw == 8) {
+      float4 *p = (float4 *)(lds + (size_t)i * kLdsRow);
+#pragma unroll
+      for (int k = 0; k < kLdsRow / 4; k++) p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+
+  f32x4 stg[kStage8];
+  int gsrc[kStage8], ldst[kStage8];
+#pragma unroll
+  for (int it = 0; it < kStage8; it++) {
+    int f = it * 512 + t;
+    f = f < kRows * 8 ? f : kRows * 8 - 1;
+    int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
+    gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
+    ldst[it] = (s * 63 + (ch + 1) * 9 + cw + 1) * kLdsRow + 4 * part;
+  }
+#define HZ_STAGE_LOAD8(q)                                                                 \
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
+  _Pragma("unroll") for (int it = 0; it < kStage8; it++)                                  \
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q)));
+#define HZ_STAGE_STORE8(buf)                                                              \
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
+  _Pragma("unroll") for (int it = 0; it < kStage8; it++) *(f32x4 *)(lds + (buf) * kBuf + ldst[it]) = stg[it];
+
+  int abase[kRB];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    int r = (rh * kRB + rb) * 16 + (lane & 15);
+    r = r < kRows ? r : kRows - 1;
+    int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
+    abase[rb] = (s * 63 + ch * 9 + cw) * kLdsRow + 4 * kg;
+  }
+
+  f32x4 acc[kRB][2];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
+
+  const int co0 = 32 * (w & 3) + (lane & 15);
+  // B fragment of step L = (q * 9 + tap) * 2 + gs, column block cb:
+  // wp[((tap * 8 + 2 q + gs) * 128 + co0 + 16 cb) * 4 + kg]
+  const float4 *wl = wp + co0 * 4 + kg;
+  auto bload = [&](int L, int cb) -> float4 {
+    int q2 = L / 18, r = L - 18 * q2, t2 = r >> 1, g2 = r & 1;
+    return wl[(t2 * 8 + 2 * q2 + g2) * 512 + 64 * cb];
+  };
+
+  HZ_STAGE_LOAD8(0)
+  HZ_STAGE_STORE8(0)
+  __syncthreads();
+
+  float4 b[2][2];
+  b[0][0] = bload(0, 0);
+  b[0][1] = bload(0, 1);
+  float4 acur[kRB];
+
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const float *lb = lds + (q & 1) * kBuf;
+#pragma unroll
+    for (int rb = 0; rb < kRB; rb++) acur[rb] = *(const float4 *)(lb + abase[rb]);
+    if (q < 3) { HZ_STAGE_LOAD8(q + 1) }
+    for (int tap = 0; tap < 9; tap++) {
+      const int toff = ((tap / 3) * 9 + tap % 3) * kLdsRow;
+      const int tn = tap < 8 ? tap + 1 : 8;
+      const int toffn = ((tn / 3) * 9 + tn % 3) * kLdsRow;
+      const int L0 = (q * 9 + tap) * 2;
+#pragma unroll
+      for (int gs = 0; gs < 2; gs++) {
+        const int Ln = L0 + gs + 1 < 72 ? L0 + gs + 1 : 71;
+        b[(gs + 1) & 1][0] = bload(Ln, 0);
+        b[(gs + 1) & 1][1] = bload(Ln, 1);
+        float4 a[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) a[rb] = acur[rb];
+        const int noff = gs == 0 ? toff + 16 : toffn;
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) acur[rb] = *(const float4 *)(lb + abase[rb] + noff);
+        const float4 b0 = b[gs][0], b1 = b[gs][1];
+#define HZ_MF(c)                                                                              \
+  _Pragma("unroll") for (int rb = 0; rb < kRB; rb++) {                                        \
+    acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb].c, b0.c, acc[rb][0], 0, 0, 0);    \
+    acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb].c, b1.c, acc[rb][1], 0, 0, 0);    \
+  }
+        HZ_MF(x)
+        HZ_MF(y)
+        HZ_MF(z)
+        HZ_MF(w)
+#undef HZ_MF
+      }
+    }
+    if (q < 3) {
+      HZ_STAGE_STORE8((q + 1) & 1)
+      __syncthreads();
+    }
+  }
+
+  // epilogue: C/D row = 4 kg + reg, column = lane & 15
+  const float bc0 = bias[co0], bc1 = bias[co0 + 16];
+  float *ob = out + (size_t)s0 * 35 * 128 + co0;
+  const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co0 : nullptr;
+  const int nrow = ns * 35;
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+    float rv[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const bool ok = rbase + j < nrow;
+      rv[0][j] = rsb && ok ? rsb[(rbase + j) * 128] : 0.f;
+      rv[1][j] = rsb && ok ? rsb[(rbase + j) * 128 + 16] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (rbase + j < nrow) {
+        float v0 = acc[rb][0][j] + bc0, v1 = acc[rb][1][j] + bc1;
+        if (rsb) {
+          v0 = v0 + rv[0][j];
+          v1 = v1 + rv[1][j];
+        }
+        ob[(rbase + j) * 128] = v0 > 0.f ? v0 : 0.f;
+        ob[(rbase + j) * 128 + 16] = v1 > 0.f ? v1 : 0.f;
+      }
+    }
+  }
+}
+#undef HZ_STAGE_LOAD8
+#undef HZ_STAGE_STORE8
+
 #undef HZ_STAGE_LOAD
 #undef HZ_STAGE_STORE
 }  // namespace
@@ -261,12 +411,12 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
   static bool init = false;
   const size_t lds = 2 * (size_t)kBuf * sizeof(float);
   if (!init) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+    if (hipFuncSetAttribute((const void *)k_conv3x3_w8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return 1;
     init = true;
   }
-  hipLaunchKernelGGL(k_conv3x3, dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(k_conv3x3_w8, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, x,
                      (const float4 *)wpack, bias, res, out, batch);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

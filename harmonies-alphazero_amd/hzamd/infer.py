@@ -26,10 +26,10 @@ from ._native import NativeError, lib
 
 
 def pack_conv3x3(w):
-    """[co][ci][3][3] -> [kh*3+kw][ci/8][co][ci%8], the layout hz_conv3x3_bias_act
+    """[co][ci][3][3] -> [kh*3+kw][ci/16][co][ci%16], the layout hz_conv3x3_bias_act
     reads (one 16-byte B fragment per lane)."""
     co, ci = w.shape[0], w.shape[1]
-    return w.permute(2, 3, 1, 0).reshape(9, ci // 8, 8, co).permute(0, 1, 3, 2).contiguous()
+    return w.permute(2, 3, 1, 0).reshape(9, ci // 16, 16, co).permute(0, 1, 3, 2).contiguous()
 
 
 def _conv3x3_act(x, wpack, b, res=None):

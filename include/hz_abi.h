@@ -194,7 +194,7 @@ int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int
  * 128 -> 128 channel convs (model.py:362-371, kernel 3, padding 1) on the
  * 5x7 board: x, res, out NHWC [batch][5][7][128] (res may be NULL; out must
  * not alias x or res), wpack = w[co][ci][kh][kw] repacked as
- * [kh*3+kw][ci/8][co][ci%8] (hzamd/infer.py:pack_conv3x3).  f32 MFMA, exact
+ * [kh*3+kw][ci/16][co][ci%16] (hzamd/infer.py:pack_conv3x3).  f32 MFMA, exact
  * fp32 products and sums (summation order differs from MIOpen's). */
 int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res, float *out,
                         int32_t batch, void *stream);
