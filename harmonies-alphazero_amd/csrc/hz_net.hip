@@ -63,200 +63,32 @@ extern "C" int hz_bias_act(float *x, const float *bias, const float *res, int64_
 // ---- 3x3 conv (128 -> 128 channels, 5x7 board, pad 1) with the epilogue ----
 //
 // The residual tower's convs (model.py:376-393) as an implicit GEMM on the
-// f32 MFMA (v_mfma_f32_32x32x2_f32: exact fp32 fma chains):
+// f32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32 fma chains):
 //     out[(s, cell), co] = sum_{tap, ci} x[s, cell + tap, ci] * w[co, ci, tap]
-// One workgroup = 8 states = 280 rows (9 row blocks of 32, the last 8 rows
-// repeat row 279 and are not stored); wave w owns output channels
-// 32w..32w+31, so every wave holds 9 accumulator tiles (144 registers).
-// The input is staged through LDS 32 channels at a time on a zero-halo
-// [8][7 x 9][36] grid (pad 4: conflict-free 16-B reads), double-buffered,
-// the next chunk's global loads in flight while the current one is
-// consumed.  Weights are prepacked [tap][ci/8][co][8] so a lane's B
-// fragment for 4 k-steps is one 16-B load, one tap ahead of its use.  K
-// order inside a group of 8 channels: MFMA j takes channel 8g + j in lanes
-// 0-31 (k = 0) and 8g + 4 + j in lanes 32-63 (k = 1), for A and B alike.
+// One 512-thread workgroup = 8 states = 280 rows as 18 blocks of 16 (the
+// last 8 rows repeat row 279 and are not stored).  Wave w = (row half
+// rh = w >> 2, output channels 32 (w & 3) .. +32): 9 row blocks x 2 column
+// blocks x 4 registers = 72 accumulators, so two waves share each SIMD and
+// cover each other's LDS and memory waits.  The input is staged through LDS
+// 32 channels at a time on a zero-halo [8][7 x 9][36] grid, double-buffered,
+// the next chunk's global loads in flight while the current one is consumed.
+// A step is 16 channels of one tap: lane (r = l & 15, kg = l >> 4) reads
+// channels 16 gs + 4 kg .. +3 of its row with one 16-B LDS read, and MFMA j
+// takes channel 16 gs + 4 kg + j (B alike: weights prepacked
+// [tap][ci/16][co][ci%16], one 16-B fragment per lane, loaded a step ahead).
 // Epilogue: out = relu((acc + bias[co]) + res), as hz_bias_act.
+// (The 4-wave 32x32x2 form with 144 accumulators per wave measured the same
+// 336 us; PMC: MFMA pipes busy 81 % at 2.42 GHz, profiles/r01.)
 namespace {
 
 constexpr int kCS = 8;             // states per workgroup
 constexpr int kRows = kCS * 35;    // 280 output rows
-constexpr int kRB = 9;             // row blocks of 32
+constexpr int kRB = 9;             // row blocks of 16 per wave (two row halves)
 constexpr int kLdsRow = 36;        // floats per padded cell (32 channels + 4)
 constexpr int kBuf = kCS * 63 * kLdsRow;  // floats per staging buffer
-constexpr int kStage = kRows * 8 / 256 + 1;  // float4 per thread per chunk (2240 / 256 -> 9)
 
-using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
-__global__ void __launch_bounds__(256, 1)
-    k_conv3x3(const float *__restrict__ x, const float4 *__restrict__ wp, const float *__restrict__ bias,
-              const float *__restrict__ res, float *__restrict__ out, int32_t batch) {
-  extern __shared__ float4 lds4[];
-  float *lds = (float *)lds4;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, h = lane >> 5;
-  const int s0 = blockIdx.x * kCS;
-  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
-
-  // zero both buffers' halo cells (the interior is overwritten by staging)
-  for (int i = t; i < 2 * kCS * 63; i += 256) {
-    int pc = i % 63, ph = pc / 9, pw = pc - 9 * ph;
-    if (ph == 0 || ph == 6 || pw == 0 || pw == 8) {
-      float4 *p = (float4 *)(lds + (size_t)i * kLdsRow);
-#pragma unroll
-      for (int k = 0; k < kLdsRow / 4; k++) p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-
-  // staging map: float4 f = it * 256 + t -> (state-cell sc, channel quad part)
-  f32x4 stg[kStage];
-  int gsrc[kStage], ldst[kStage];
-#pragma unroll
-  for (int it = 0; it < kStage; it++) {
-    int f = it * 256 + t;
-    f = f < kRows * 8 ? f : kRows * 8 - 1;  // threads past the end repeat the last quad
-    int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
-    gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
-    ldst[it] = (s * 63 + (ch + 1) * 9 + cw + 1) * kLdsRow + 4 * part;
-  }
-  // Staging loads are inline asm: the compiler would sink plain loads past
-  // the tap loop to their LDS stores (and wait on them there), and makes
-  // volatile ones wait one by one.  The waits are ours: vmcnt(0) before the
-  // loads (the weight fragments in flight were issued steps earlier, so
-  // nothing the compiler tracks is older than the staging loads and its own
-  // vmcnt counts stay exact) and vmcnt(0) before the stores.
-#define HZ_STAGE_LOAD(q)                                                                  \
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
-  _Pragma("unroll") for (int it = 0; it < kStage; it++)                                   \
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q)));
-#define HZ_STAGE_STORE(buf)                                                               \
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
-  _Pragma("unroll") for (int it = 0; it < kStage; it++) *(f32x4 *)(lds + (buf) * kBuf + ldst[it]) = stg[it];
-
-  // A row bases (floats), tap (-1,-1) folded in so tap offsets are >= 0
-  int abase[kRB];
-#pragma unroll
-  for (int rb = 0; rb < kRB; rb++) {
-    int r = rb * 32 + (lane & 31);
-    r = r < kRows ? r : kRows - 1;
-    int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
-    abase[rb] = (s * 63 + ch * 9 + cw) * kLdsRow + 4 * h;  // padded (ch+1-1, cw+1-1)
-  }
-
-  f32x16 acc[kRB];
-#pragma unroll
-  for (int rb = 0; rb < kRB; rb++) acc[rb] = (f32x16){};
-
-  const int co = 32 * w + (lane & 31);
-  const float4 *wl = wp + co * 2 + h;  // + ((tap * 16 + c8) * 128) * 2 float4s
-
-  HZ_STAGE_LOAD(0)
-  HZ_STAGE_STORE(0)
-  __syncthreads();
-
-  // B fragments ring: step L = (q * 9 + tap) * 4 + g uses b[g]; the
-  // fragment for step L + 2 is loaded at step L into b[(g + 2) & 3], whose
-  // previous value was last read at step L - 2 (no register copies, so no
-  // wait on a load in flight)
-  auto bload = [&](int L) -> float4 {
-    int q2 = L / 36, r = L - 36 * q2, t2 = r >> 2, g2 = r & 3;
-    return wl[(t2 * 16 + 4 * q2 + g2) * 256];
-  };
-  float4 acur[kRB];
-  float4 b[4];
-  b[0] = bload(0);
-  b[1] = bload(1);
-
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const float *lb = lds + (q & 1) * kBuf;
-#pragma unroll
-    for (int rb = 0; rb < kRB; rb++) acur[rb] = *(const float4 *)(lb + abase[rb]);  // tap 0, step 0
-    // next chunk's input, in flight for the whole chunk
-    if (q < 3) { HZ_STAGE_LOAD(q + 1) }
-    for (int tap = 0; tap < 9; tap++) {
-      const int toff = ((tap / 3) * 9 + tap % 3) * kLdsRow;
-      const int L0 = (q * 9 + tap) * 4;
-      // LDS offset of the next tap (its step 0 is prefetched during step 3)
-      const int tn = tap < 8 ? tap + 1 : 8;
-      const int toffn = ((tn / 3) * 9 + tn % 3) * kLdsRow;
-#pragma unroll
-      for (int g = 0; g < 4; g++) {
-        b[(g + 2) & 3] = bload(L0 + g + 2 < 144 ? L0 + g + 2 : 143);  // unconditional: no select copies
-        float4 a[kRB];
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) a[rb] = acur[rb];
-        // A fragments of the next step, read while this step's MFMAs run
-        const int noff = g < 3 ? toff + 8 * (g + 1) : toffn;
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) acur[rb] = *(const float4 *)(lb + abase[rb] + noff);
-        const float4 bg = b[g];
-        // 9 independent accumulators between dependent MFMAs
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].x, bg.x, acc[rb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].y, bg.y, acc[rb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].z, bg.z, acc[rb], 0, 0, 0);
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rb].w, bg.w, acc[rb], 0, 0, 0);
-      }
-    }
-    if (q < 3) {
-      HZ_STAGE_STORE((q + 1) & 1)
-      __syncthreads();
-    }
-  }
-
-  // epilogue: C/D row = (reg & 3) + 8 * (reg >> 2) + 4 * h, column = lane & 31.
-  // Row block 8 holds rows 256-287: registers 12-15 (rows 280-287) are the
-  // repeated padding rows.  A full workgroup stores unguarded, with each
-  // tile's 16 residual loads issued together.
-  const float bc = bias[co];
-  float *ob = out + (size_t)s0 * 35 * 128 + co;
-  const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co : nullptr;
-  if (ns == kCS) {
-#pragma unroll
-    for (int rb = 0; rb < kRB; rb++) {
-      float rv[16];
-#pragma unroll
-      for (int reg = 0; reg < 16; reg++) {
-        int r = rb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        rv[reg] = (rsb && (rb < 8 || reg < 12)) ? rsb[r * 128] : 0.f;
-      }
-#pragma unroll
-      for (int reg = 0; reg < 16; reg++) {
-        int r = rb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (rb < 8 || reg < 12) {
-          float v = acc[rb][reg] + bc;
-          if (rsb) v = v + rv[reg];
-          ob[r * 128] = v > 0.f ? v : 0.f;
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int rb = 0; rb < kRB; rb++) {
-#pragma unroll
-      for (int reg = 0; reg < 16; reg++) {
-        int r = rb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (r < ns * 35) {
-          float v = acc[rb][reg] + bc;
-          if (rsb) v = v + rsb[r * 128];
-          ob[r * 128] = v > 0.f ? v : 0.f;
-        }
-      }
-    }
-  }
-}
-
-// 8-wave form on v_mfma_f32_16x16x4_f32: the 280 rows as 18 blocks of 16
-// (the last 8 rows repeat row 279), wave w = (row half rh = w >> 2, output
-// channels 32 (w & 3) .. +32): 9 row blocks x 2 column blocks x 4 registers
-// = 72 accumulators, so two waves share each SIMD and cover each other's
-// LDS and memory waits.  A step is 16 channels of one tap: lane (r = l & 15,
-// kg = l >> 4) reads channels 16 gs + 4 kg .. +3 of its row with one 16-B
-// LDS read and MFMA j takes channel 16 gs + 4 kg + j (B alike, weights
-// packed [tap][ci/16][co][ci%16]).
 constexpr int kStage8 = (kRows * 8 + 511) / 512;  // float4 per thread per chunk (5)
 
 __global__ void __launch_bounds__(512, 1)
@@ -399,8 +231,6 @@ __global__ void __launch_bounds__(512, 1)
 #undef HZ_STAGE_LOAD8
 #undef HZ_STAGE_STORE8
 
-#undef HZ_STAGE_LOAD
-#undef HZ_STAGE_STORE
 }  // namespace
 
 extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res,
