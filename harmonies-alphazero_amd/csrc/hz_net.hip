@@ -91,6 +91,16 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int kStage8 = (kRows * 8 + 511) / 512;  // float4 per thread per chunk (5)
 
+#ifdef HZ_NET_DIAG
+// diagnostic build only (tools/conv_phases.py): per-workgroup phase stamps of
+// waves 0 and 4, written to this buffer alone
+__device__ uint64_t g_conv_stamps[1024][2][10];
+#define HZ_STAMP(k)                                                                   \
+  if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][k] = __builtin_amdgcn_s_memtime();
+#else
+#define HZ_STAMP(k)
+#endif
+
 __global__ void __launch_bounds__(512, 1)
     k_conv3x3_w8(const float *__restrict__ x, const float4 *__restrict__ wp, const float *__restrict__ bias,
                  const float *__restrict__ res, float *__restrict__ out, int32_t batch) {
@@ -99,6 +109,10 @@ __global__ void __launch_bounds__(512, 1)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
   const int s0 = blockIdx.x * kCS;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+  HZ_STAMP(0)
+#ifdef HZ_NET_DIAG
+  if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][8] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   for (int i = t; i < 2 * kCS * 63; i += 512) {
     int pc = i % 63, ph = pc / 9, pw = pc - 9 * ph;
@@ -149,9 +163,11 @@ __global__ void __launch_bounds__(512, 1)
     return wl[(t2 * 8 + 2 * q2 + g2) * 512 + 64 * cb];
   };
 
+  HZ_STAMP(1)
   HZ_STAGE_LOAD8(0)
   HZ_STAGE_STORE8(0)
   __syncthreads();
+  HZ_STAMP(2)
 
   float4 b[2][2];
   b[0][0] = bload(0, 0);
@@ -197,6 +213,7 @@ __global__ void __launch_bounds__(512, 1)
       HZ_STAGE_STORE8((q + 1) & 1)
       __syncthreads();
     }
+    HZ_STAMP(3 + q)
   }
 
   // epilogue: C/D row = 4 kg + reg, column = lane & 15
@@ -204,31 +221,42 @@ __global__ void __launch_bounds__(512, 1)
   float *ob = out + (size_t)s0 * 35 * 128 + co0;
   const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co0 : nullptr;
   const int nrow = ns * 35;
+  // all 72 residual values requested at once (the A/B/staging registers are
+  // dead here): one memory round trip instead of one per row block
+  float rv[kRB][2][4];
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
     const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
-    float rv[2][4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const bool ok = rbase + j < nrow;
-      rv[0][j] = rsb && ok ? rsb[(rbase + j) * 128] : 0.f;
-      rv[1][j] = rsb && ok ? rsb[(rbase + j) * 128 + 16] : 0.f;
+      rv[rb][0][j] = rsb && ok ? rsb[(rbase + j) * 128] : 0.f;
+      rv[rb][1][j] = rsb && ok ? rsb[(rbase + j) * 128 + 16] : 0.f;
     }
+  }
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (rbase + j < nrow) {
         float v0 = acc[rb][0][j] + bc0, v1 = acc[rb][1][j] + bc1;
         if (rsb) {
-          v0 = v0 + rv[0][j];
-          v1 = v1 + rv[1][j];
+          v0 = v0 + rv[rb][0][j];
+          v1 = v1 + rv[rb][1][j];
         }
         ob[(rbase + j) * 128] = v0 > 0.f ? v0 : 0.f;
         ob[(rbase + j) * 128 + 16] = v1 > 0.f ? v1 : 0.f;
       }
     }
   }
+  HZ_STAMP(7)
+#ifdef HZ_NET_DIAG
+  if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][9] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 #undef HZ_STAGE_LOAD8
+#undef HZ_STAMP
 #undef HZ_STAGE_STORE8
 
 }  // namespace
@@ -250,3 +278,10 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
                      (const float4 *)wpack, bias, res, out, batch);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+#ifdef HZ_NET_DIAG
+extern "C" int hz_net_diag_stamps(uint64_t *host) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), sizeof(g_conv_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
