@@ -11,6 +11,8 @@
 //     x = relu((x + bias[c]) + res)
 // HBM-bound: 8 B (12 B with res) per element.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <cstdint>
 
 #include "../../include/hz_abi.h"
@@ -266,13 +268,16 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
   if (!x || !wpack || !bias || !out || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)wpack | (uintptr_t)out | (uintptr_t)res) & 15) return -1;
   if (batch == 0) return 0;
-  static bool init = false;
+  // the 145 KB dynamic-LDS opt-in, once per device
+  static std::atomic<uint64_t> init_mask{0};
   const size_t lds = 2 * (size_t)kBuf * sizeof(float);
-  if (!init) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
     if (hipFuncSetAttribute((const void *)k_conv3x3_w8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
       return 1;
-    init = true;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
   hipLaunchKernelGGL(k_conv3x3_w8, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, x,
                      (const float4 *)wpack, bias, res, out, batch);
