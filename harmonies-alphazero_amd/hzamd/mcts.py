@@ -16,6 +16,7 @@ from . import _native as nat
 from .env import ACTION_SIZE
 
 MAX_CHILDREN = 69
+COMPACT_BUCKET = 256  # leaf batches of active boards are rounded up to this
 
 
 class BatchedMCTS:
@@ -83,16 +84,39 @@ class BatchedMCTS:
         return self.counts
 
     # -- one full search per board -------------------------------------------
-    def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None):
+    def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None,
+               compact=True):
         """get_best_action_and_pi's simulation loop (MCTS.py:288-352) for every
-        active board; returns root visit counts int32 [n, 143]."""
+        active board; returns root visit counts int32 [n, 143].
+
+        With `compact` and some boards inactive (games already over), only the
+        active boards' leaves go to the evaluator: rows gathered, the batch
+        rounded up to a multiple of COMPACT_BUCKET (repeats of the first
+        active row; at most n / COMPACT_BUCKET distinct shapes), results
+        scattered back.  Inactive boards take no part in expand/backup, so
+        their rows were never read; a row-wise evaluator gives every active
+        board the same priors and value either way."""
         if active is not None:
             active = active.to(device=self.device, dtype=torch.uint8).contiguous()
         self.begin(active)
+        rows = None
+        if compact and active is not None:
+            k = int(active.sum())  # one host sync per search (the ply loop syncs anyway)
+            if 0 < k < self.n:
+                rows = torch.nonzero(active, as_tuple=False).flatten()
+                kp = min(self.n, -(-k // COMPACT_BUCKET) * COMPACT_BUCKET)
+                gather = torch.cat((rows, rows[:1].expand(kp - k))) if kp > k else rows
+                pol = torch.zeros(self.n, ACTION_SIZE, dtype=torch.float32, device=self.device)
+                val = torch.zeros(self.n, dtype=torch.float32, device=self.device)
         for _ in range(self.num_simulations if sims is None else int(sims)):
             self.select(cpuct, active)
             board, glob = self.encode_leaves()
-            policy, value = evaluator(board, glob)
+            if rows is None:
+                policy, value = evaluator(board, glob)
+            else:
+                pc, vc = evaluator(board.index_select(0, gather), glob.index_select(0, gather))
+                policy = pol.index_copy_(0, rows, pc[:k].to(torch.float32))
+                value = val.index_copy_(0, rows, vc.reshape(-1)[:k].to(torch.float32))
             self.expand_backup(policy, value, noise, eps, testing)
         return self.result()
 

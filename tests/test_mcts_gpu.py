@@ -119,3 +119,36 @@ def test_mcts_exact_keys_mode():
         m = oracle.mt_from_words(mt0[b], idx0[b])
         _, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, 1.5, testing=True, exact_keys=True)
         assert (visits[b] == ov).all() and (counts[b, 0], counts[b, 1]) == (nn, ne), b
+
+
+def test_mcts_compacted_leaf_batch_matches_full_batch():
+    """Leaf batches compacted to the active boards (rounded up to the bucket,
+    padded with repeats) give every board the same search as the full batch:
+    identical visit counts and node/edge counts, stub evaluator, 30 % of the
+    boards inactive (including a partial bucket)."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, base, sims, cpuct = 700, 900, 16, 1.5
+    g = torch.Generator().manual_seed(7)
+    active = (torch.rand(n, generator=g) > 0.3).to(DEV)
+    out = []
+    for compact in (False, True):
+        env = BatchedEnv(n, seed_base=base, device=DEV)
+        env.reset()
+        for _ in range(9):
+            mask, count = env.legal_mask()
+            env.step(env.rule_actions(mask, count))
+        mcts = BatchedMCTS(env, sims)
+        calls = []
+
+        def ev(board, glob):
+            calls.append(board.shape[0])
+            return stub_evaluator(board, glob)
+        v = mcts.search(ev, cpuct, active=active, compact=compact).clone()
+        out.append((v.cpu(), mcts.stats().clone().cpu(), calls))
+    (v0, c0, calls0), (v1, c1, calls1) = out
+    assert torch.equal(v0, v1)
+    assert torch.equal(c0[:, :2], c1[:, :2])
+    k = int(active.sum())
+    assert calls0 == [n] * sims and calls1 == [min(n, -(-k // 256) * 256)] * sims
+    assert bool((v1[~active.cpu()] == 0).all())
