@@ -290,3 +290,59 @@ extern "C" int hz_net_diag_stamps(uint64_t *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), sizeof(g_conv_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
+
+// ---- policy / value heads up to the linear layers ---------------------------
+//
+// model.py:336-351 after the tower: policy = relu(BN(conv1x1(x))) (2
+// channels), value = relu(BN(conv1x1(x))) (1 channel), each flattened in
+// NCHW order and concatenated with the 42 global features.  With BN folded
+// (hzamd/infer.py), one pass over the [B][35][128] activation writes both
+// concatenated inputs of the linear layers: pcat[B][70 + 42], vcat[B][35 + 42].
+// Wave per state; lane c < 35 owns cell c (its 128 channels are 512
+// contiguous bytes); the weights hw[3][128] (policy 0, 1, value) sit in LDS.
+namespace {
+
+__global__ void __launch_bounds__(256) k_heads(const float *__restrict__ x, const float *__restrict__ hw,
+                                               const float *__restrict__ hb, const float *__restrict__ glob,
+                                               float *__restrict__ pcat, float *__restrict__ vcat, int32_t batch) {
+  __shared__ float4 w4[3][32];
+  const int t = threadIdx.x, lane = t & 63;
+  if (t < 96) w4[t >> 5][t & 31] = ((const float4 *)hw)[t];
+  __syncthreads();
+  const int b = blockIdx.x * 4 + (t >> 6);
+  if (b >= batch) return;
+  if (lane < 35) {
+    const float4 *xr = (const float4 *)(x + ((size_t)b * 35 + lane) * 128);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 32; k++) {
+      const float4 v = xr[k], a = w4[0][k], c = w4[1][k], d = w4[2][k];
+      s0 += v.x * a.x + v.y * a.y + v.z * a.z + v.w * a.w;
+      s1 += v.x * c.x + v.y * c.y + v.z * c.z + v.w * c.w;
+      s2 += v.x * d.x + v.y * d.y + v.z * d.z + v.w * d.w;
+    }
+    s0 += hb[0];
+    s1 += hb[1];
+    s2 += hb[2];
+    pcat[(size_t)b * 112 + lane] = s0 > 0.f ? s0 : 0.f;
+    pcat[(size_t)b * 112 + 35 + lane] = s1 > 0.f ? s1 : 0.f;
+    vcat[(size_t)b * 77 + lane] = s2 > 0.f ? s2 : 0.f;
+  }
+  if (lane < 42) {
+    const float g = glob[(size_t)b * 42 + lane];
+    pcat[(size_t)b * 112 + 70 + lane] = g;
+    vcat[(size_t)b * 77 + 35 + lane] = g;
+  }
+}
+
+}  // namespace
+
+extern "C" int hz_heads(const float *x, const float *hw, const float *hb, const float *glob, float *pcat,
+                        float *vcat, int32_t batch, void *stream) {
+  if (!x || !hw || !hb || !glob || !pcat || !vcat || batch < 0) return -1;
+  if (((uintptr_t)x | (uintptr_t)hw) & 15) return -1;
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(k_heads, dim3((batch + 3) / 4), dim3(256), 0, (hipStream_t)stream, x, hw, hb, glob, pcat,
+                     vcat, batch);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -48,6 +48,23 @@ def _conv3x3_act(x, wpack, b, res=None):
     return out
 
 
+def _heads(x, glob, hw, hb):
+    """(relu(policy conv1x1) flattened NCHW || glob, relu(value conv1x1) || glob)
+    for the default heads (2 + 1 filters on the 5x7 board), one HIP launch."""
+    B = x.shape[0]
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_heads needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    glob = glob.to(torch.float32).contiguous()
+    pcat = torch.empty(B, 112, dtype=torch.float32, device=x.device)
+    vcat = torch.empty(B, 77, dtype=torch.float32, device=x.device)
+    rc = lib().hz_heads(x.data_ptr(), hw.data_ptr(), hb.data_ptr(), glob.data_ptr(), pcat.data_ptr(),
+                        vcat.data_ptr(), B, torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_heads failed ({rc})")
+    return pcat, vcat
+
+
 def _bias_act(x, b, res=None):
     """x = relu(x + b[c] (+ res)) in place over an NHWC activation."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)):
@@ -101,6 +118,12 @@ class FoldedNet(nn.Module):
         self.pfc = (n.policy_fc.weight.detach(), n.policy_fc.bias.detach())
         self.vfc1 = (n.value_fc1.weight.detach(), n.value_fc1.bias.detach())
         self.vfc2 = (n.value_fc2.weight.detach(), n.value_fc2.bias.detach())
+        # both heads' 1x1 convs + ReLU + flatten + concat with glob: one HIP pass
+        self.heads = None
+        if (self.native_conv and self.pconv[0].shape == (2, 128, 1, 1) and self.vconv[0].shape == (1, 128, 1, 1)
+                and n.policy_fc.in_features == 112 and n.value_fc1.in_features == 77):
+            self.heads = (torch.cat((self.pconv[0].reshape(2, 128), self.vconv[0].reshape(1, 128))).contiguous(),
+                          torch.cat((self.pconv[1], self.vconv[1])).contiguous())
 
     @torch.no_grad()
     def forward(self, board, glob):
@@ -116,6 +139,11 @@ class FoldedNet(nn.Module):
             for (w1, b1), (w2, b2) in self.blocks:
                 y = ep(F.conv2d(x, w1, None, padding=1), b1)
                 x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
+        if self.heads is not None:
+            pcat, vcat = _heads(x, glob, *self.heads)
+            logits = F.linear(pcat, *self.pfc)
+            v = F.linear(vcat, *self.vfc1).relu_()
+            return logits, torch.tanh(F.linear(v, *self.vfc2))
         w, b = self.pconv
         p = F.conv2d(x, w, b).relu_().flatten(1)               # NCHW order, as model.py flattens
         logits = F.linear(torch.cat((p, glob), 1), *self.pfc)

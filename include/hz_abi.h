@@ -199,6 +199,13 @@ int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int
 int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res, float *out,
                         int32_t batch, void *stream);
 
+/* The heads of model.py:336-351 up to their linear layers, BN folded:
+ * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)
+ * || glob[b] (42); vcat[b] = relu(hw[2] . x[b][cell] + hb[2]) (35) || glob[b].
+ * x NHWC [batch][5][7][128] (16-byte aligned), hw [3][128], hb [3]. */
+int hz_heads(const float *x, const float *hw, const float *hb, const float *glob, float *pcat, float *vcat,
+             int32_t batch, void *stream);
+
 /* ---- build info ---------------------------------------------------------- */
 const char *hz_version(void);
 

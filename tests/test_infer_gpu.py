@@ -99,3 +99,23 @@ def test_conv3x3_matches_miopen_float(batch):
     want = (torch.nn.functional.conv2d(x, w, b, padding=1) + r).relu()
     got = _conv3x3_act(x, pack_conv3x3(w), b, r)
     assert (got - want).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("batch", [1, 5, 4096])
+def test_heads_match_torch(batch):
+    """hz_heads == conv1x1 + bias + ReLU, NCHW flatten, concat with glob for
+    both heads (model.py:336-351), within fp32 summation-order rounding."""
+    from hzamd.infer import _heads
+    g = torch.Generator(device="cuda").manual_seed(batch)
+    cl = torch.channels_last
+    x = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
+    glob = torch.rand(batch, 42, device="cuda", generator=g)
+    hw = torch.randn(3, 128, device="cuda", generator=g) * 0.1
+    hb = torch.randn(3, device="cuda", generator=g) * 0.1
+    p = torch.nn.functional.conv2d(x, hw[:2].reshape(2, 128, 1, 1), hb[:2]).relu().flatten(1)
+    v = torch.nn.functional.conv2d(x, hw[2:].reshape(1, 128, 1, 1), hb[2:]).relu().flatten(1)
+    pcat, vcat = _heads(x, glob, hw.contiguous(), hb.contiguous())
+    assert pcat.shape == (batch, 112) and vcat.shape == (batch, 77)
+    assert (pcat[:, :70] - p).abs().max().item() <= 1e-5
+    assert (vcat[:, :35] - v).abs().max().item() <= 1e-5
+    assert torch.equal(pcat[:, 70:], glob) and torch.equal(vcat[:, 35:], glob)
