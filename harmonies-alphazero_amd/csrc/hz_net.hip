@@ -346,3 +346,119 @@ extern "C" int hz_heads(const float *x, const float *hw, const float *hb, const 
                      vcat, batch);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// ---- the stem: 3x3 conv 38 -> 128 channels + bias + ReLU (model.py:328-330) -
+//
+// Same tiling as k_conv3x3_w8 (8 states per workgroup, wave = row half x 32
+// output channels, 9 x 2 tiles of v_mfma_f32_16x16x4_f32), but the input is
+// the encoder's NCHW board [B][38][5][7] read directly (no layout copy),
+// staged once per workgroup into a zero-halo LDS grid with the channels
+// padded to 48 (three 16-channel steps per tap; the weights are packed with
+// zero rows for channels 38-47).
+namespace {
+
+constexpr int kStemC = 38, kStemCP = 48;
+constexpr int kStemRow = kStemCP + 4;  // floats per padded cell
+constexpr int kStemLds = kCS * 63 * kStemRow;
+
+__global__ void __launch_bounds__(512, 1)
+    k_stem3x3(const float *__restrict__ board, const float4 *__restrict__ wp, const float *__restrict__ bias,
+              float *__restrict__ out, int32_t batch) {
+  extern __shared__ float4 lds4[];
+  float *lds = (float *)lds4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
+  const int s0 = blockIdx.x * kCS;
+  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+
+  // whole grid zeroed first (halo and channels 38-47), then the interior
+  for (int i = t; i < kStemLds / 4; i += 512) lds4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  for (int i = t; i < kCS * kStemC * 35; i += 512) {
+    int s = i / (kStemC * 35), r = i - s * (kStemC * 35), c = r / 35, cell = r - 35 * c;
+    int ch = cell / 7, cw = cell - 7 * ch;
+    int sg = s < ns ? s0 + s : s0 + ns - 1;
+    lds[(s * 63 + (ch + 1) * 9 + cw + 1) * kStemRow + c] = board[(size_t)sg * (kStemC * 35) + r];
+  }
+  __syncthreads();
+
+  int abase[kRB];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    int r = (rh * kRB + rb) * 16 + (lane & 15);
+    r = r < kRows ? r : kRows - 1;
+    int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
+    abase[rb] = (s * 63 + ch * 9 + cw) * kStemRow + 4 * kg;
+  }
+  f32x4 acc[kRB][2];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
+
+  const int co0 = 32 * (w & 3) + (lane & 15);
+  // B fragment of step L = tap * 3 + gs: wp[((tap * 3 + gs) * 128 + co0 + 16 cb) * 4 + kg]
+  const float4 *wl = wp + co0 * 4 + kg;
+  // one slot per channel step (static registers), loaded a step ahead
+  float4 b[3][2];
+  b[0][0] = wl[0];
+  b[0][1] = wl[64];
+  for (int tap = 0; tap < 9; tap++) {
+    const int toff = ((tap / 3) * 9 + tap % 3) * kStemRow;
+#pragma unroll
+    for (int gs = 0; gs < 3; gs++) {
+      const int L = tap * 3 + gs, Ln = L + 1 < 27 ? L + 1 : 26;
+      b[(gs + 1) % 3][0] = wl[Ln * 512];
+      b[(gs + 1) % 3][1] = wl[Ln * 512 + 64];
+      float4 a[kRB];
+#pragma unroll
+      for (int rb = 0; rb < kRB; rb++) a[rb] = *(const float4 *)(lds + abase[rb] + toff + 16 * gs);
+      const float4 b0 = b[gs][0], b1 = b[gs][1];
+#define HZ_MF(c)                                                                              \
+  _Pragma("unroll") for (int rb = 0; rb < kRB; rb++) {                                        \
+    acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb].c, b0.c, acc[rb][0], 0, 0, 0);    \
+    acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rb].c, b1.c, acc[rb][1], 0, 0, 0);    \
+  }
+      HZ_MF(x)
+      HZ_MF(y)
+      HZ_MF(z)
+      HZ_MF(w)
+#undef HZ_MF
+    }
+  }
+
+  const float bc0 = bias[co0], bc1 = bias[co0 + 16];
+  float *ob = out + (size_t)s0 * 35 * 128 + co0;
+  const int nrow = ns * 35;
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (rbase + j < nrow) {
+        float v0 = acc[rb][0][j] + bc0, v1 = acc[rb][1][j] + bc1;
+        ob[(rbase + j) * 128] = v0 > 0.f ? v0 : 0.f;
+        ob[(rbase + j) * 128 + 16] = v1 > 0.f ? v1 : 0.f;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bias, float *out,
+                                   int32_t batch, void *stream) {
+  if (!board || !wpack || !bias || !out || batch < 0) return -1;
+  if (((uintptr_t)wpack | (uintptr_t)out) & 15) return -1;
+  if (batch == 0) return 0;
+  static std::atomic<uint64_t> init_mask{0};
+  const size_t lds = (size_t)kStemLds * sizeof(float);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_stem3x3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL(k_stem3x3, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, board,
+                     (const float4 *)wpack, bias, out, batch);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -48,6 +48,28 @@ def _conv3x3_act(x, wpack, b, res=None):
     return out
 
 
+def pack_stem(w):
+    """Stem weights [128][38][3][3] with the input channels zero-padded to 48,
+    packed like pack_conv3x3 (hz_stem3x3_bias_act's layout)."""
+    w48 = torch.zeros(w.shape[0], 48, 3, 3, dtype=w.dtype, device=w.device)
+    w48[:, :w.shape[1]] = w
+    return pack_conv3x3(w48)
+
+
+def _stem_act(board, wpack, b):
+    """relu(conv3x3(board) + b) from the encoder's NCHW board, NHWC out, one HIP launch."""
+    if not (board.is_cuda and board.dtype == torch.float32 and board.shape[1:] == (38, 5, 7)):
+        raise NativeError("hz_stem3x3_bias_act needs a CUDA fp32 [B,38,5,7] board")
+    board = board.contiguous()
+    out = torch.empty(board.shape[0], 128, 5, 7, dtype=torch.float32, device=board.device,
+                      memory_format=torch.channels_last)
+    rc = lib().hz_stem3x3_bias_act(board.data_ptr(), wpack.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                   board.shape[0], torch.cuda.current_stream(board.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_stem3x3_bias_act failed ({rc})")
+    return out
+
+
 def _heads(x, glob, hw, hb):
     """(relu(policy conv1x1) flattened NCHW || glob, relu(value conv1x1) || glob)
     for the default heads (2 + 1 filters on the 5x7 board), one HIP launch."""
@@ -110,6 +132,9 @@ class FoldedNet(nn.Module):
         self.blocks = [(_fold(b.conv1, b.bn1), _fold(b.conv2, b.bn2)) for b in n.residual_blocks]
         # the tower's 128-channel convs run as one fused HIP kernel each
         # (conv + bias + skip + ReLU); other widths use MIOpen + hz_bias_act
+        self.stem_packed = None
+        if self.native_conv and self.stem[0].shape == (128, 38, 3, 3):
+            self.stem_packed = pack_stem(self.stem[0])
         self.packed = None
         if self.native_conv and self.blocks and self.blocks[0][0][0].shape[:2] == (128, 128):
             self.packed = [(pack_conv3x3(w1), pack_conv3x3(w2)) for (w1, _), (w2, _) in self.blocks]
@@ -127,10 +152,12 @@ class FoldedNet(nn.Module):
 
     @torch.no_grad()
     def forward(self, board, glob):
-        x = board.contiguous(memory_format=torch.channels_last)
         ep = self.epilogue
         w, b = self.stem
-        x = ep(F.conv2d(x, w, None, padding=1), b)
+        if self.stem_packed is not None:
+            x = _stem_act(board, self.stem_packed, b)  # reads the NCHW board directly
+        else:
+            x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
         if self.packed is not None:
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
                 y = _conv3x3_act(x, p1, b1)

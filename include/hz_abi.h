@@ -199,6 +199,13 @@ int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int
 int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res, float *out,
                         int32_t batch, void *stream);
 
+/* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
+ * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the
+ * encoder writes it, out NHWC [batch][5][7][128], wpack = w with the input
+ * channels zero-padded to 48, packed as for hz_conv3x3_bias_act. */
+int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bias, float *out, int32_t batch,
+                        void *stream);
+
 /* The heads of model.py:336-351 up to their linear layers, BN folded:
  * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)
  * || glob[b] (42); vcat[b] = relu(hw[2] . x[b][cell] + hb[2]) (35) || glob[b].

@@ -119,3 +119,18 @@ def test_heads_match_torch(batch):
     assert (pcat[:, :70] - p).abs().max().item() <= 1e-5
     assert (vcat[:, :35] - v).abs().max().item() <= 1e-5
     assert torch.equal(pcat[:, 70:], glob) and torch.equal(vcat[:, 35:], glob)
+
+
+@pytest.mark.parametrize("batch", [1, 13, 64])
+def test_stem_exact_on_integer_data(batch):
+    """hz_stem3x3_bias_act on small-integer data equals the fp64 conv exactly
+    (NCHW board in, NHWC out; channel padding 38 -> 48 must contribute 0)."""
+    from hzamd.infer import _stem_act, pack_stem
+    g = torch.Generator().manual_seed(100 + batch)
+    board = torch.randint(-3, 4, (batch, 38, 5, 7), generator=g).float()
+    w = torch.randint(-2, 3, (128, 38, 3, 3), generator=g).float()
+    b = torch.randint(-50, 50, (128,), generator=g).float()
+    want = _conv_ref(board, w, b, None).float()
+    got = _stem_act(board.cuda(), pack_stem(w).cuda(), b.cuda())
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got.cpu(), want)
