@@ -1,4 +1,4 @@
-"""FoldedNet on the GPU (MIOpen NHWC convs) against the unfolded eval-mode
+"""FoldedNet on the GPU (HIP stem / tower / heads kernels) against the unfolded eval-mode
 network run on the CPU in fp32: max |diff| <= 2e-3 on logits and values at
 batch 512 with non-trivial BatchNorm statistics (different conv algorithms
 and summation orders on the two devices)."""
@@ -23,7 +23,10 @@ def test_folded_gpu_matches_cpu_reference():
     with torch.no_grad():
         l0, v0 = net(board, glob)
     gnet = net.to("cuda")
-    l1, v1 = FoldedNet(gnet)(board.cuda(), glob.cuda())
+    fnet = FoldedNet(gnet)
+    # the default net must take the native kernels, not the MIOpen fallback
+    assert fnet.stem_packed is not None and fnet.packed is not None and fnet.heads is not None
+    l1, v1 = fnet(board.cuda(), glob.cuda())
     assert (l1.cpu() - l0).abs().max().item() <= 2e-3
     assert (v1.cpu() - v0).abs().max().item() <= 2e-3
     p, v = BatchedPredictor(gnet)(board.cuda(), glob.cuda())
