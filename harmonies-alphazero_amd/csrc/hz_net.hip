@@ -360,6 +360,8 @@ namespace {
 constexpr int kStemC = 38, kStemCP = 48;
 constexpr int kStemRow = kStemCP + 4;  // floats per padded cell
 constexpr int kStemLds = kCS * 63 * kStemRow;
+constexpr int kStemN = kCS * kStemC * 35;        // board floats per workgroup
+constexpr int kStemIt = (kStemN + 511) / 512;    // per thread (21)
 
 __global__ void __launch_bounds__(512, 1)
     k_stem3x3(const float *__restrict__ board, const float4 *__restrict__ wp, const float *__restrict__ bias,
@@ -370,14 +372,29 @@ __global__ void __launch_bounds__(512, 1)
   const int s0 = blockIdx.x * kCS;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
 
-  // whole grid zeroed first (halo and channels 38-47), then the interior
+  // all of this thread's board loads are issued first (coalesced along the
+  // NCHW board), the grid is zeroed (halo and channels 38-47) while they are
+  // in flight, then the interior is written
+  float v[kStemIt];
+#pragma unroll
+  for (int k = 0; k < kStemIt; k++) {
+    const int i = t + 512 * k;
+    if (i < kStemN) {
+      const int s = i / (kStemC * 35);
+      const int sg = s < ns ? s0 + s : s0 + ns - 1;
+      v[k] = board[(size_t)sg * (kStemC * 35) + (i - s * (kStemC * 35))];
+    }
+  }
   for (int i = t; i < kStemLds / 4; i += 512) lds4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  for (int i = t; i < kCS * kStemC * 35; i += 512) {
-    int s = i / (kStemC * 35), r = i - s * (kStemC * 35), c = r / 35, cell = r - 35 * c;
-    int ch = cell / 7, cw = cell - 7 * ch;
-    int sg = s < ns ? s0 + s : s0 + ns - 1;
-    lds[(s * 63 + (ch + 1) * 9 + cw + 1) * kStemRow + c] = board[(size_t)sg * (kStemC * 35) + r];
+#pragma unroll
+  for (int k = 0; k < kStemIt; k++) {
+    const int i = t + 512 * k;
+    if (i < kStemN) {
+      int s = i / (kStemC * 35), r = i - s * (kStemC * 35), c = r / 35, cell = r - 35 * c;
+      int ch = cell / 7, cw = cell - 7 * ch;
+      lds[(s * 63 + (ch + 1) * 9 + cw + 1) * kStemRow + c] = v[k];
+    }
   }
   __syncthreads();
 
