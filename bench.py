@@ -1,13 +1,26 @@
 """Benchmark: BASELINE config 2 — 4096 concurrent boards per GPU, pure env
-step / legal_actions / score HIP kernels, bit-exact vs the CPU engine.
+step / legal_actions / score HIP kernels, bit-exact vs the CPU engine — with
+config 3 (and, at N > 1, config 4's exchange) measured in the same run.
 
-One bench step = one batched pass of the env hot path over 4096 boards, a
-single hz_play launch: HarmoniesGameState() on every board (CPython-exact
-seeding and opening draws), then play to the end of every game (legal mask ->
-build-defined splitmix rule pick -> apply_move, incl. chance draws and final
-scoring).
+Headline (config 2): one bench step = `--launches-per-step` (256) batched
+passes of the env hot path over 4096 boards, each a single hz_play launch:
+HarmoniesGameState() on every board (CPython-exact seeding and opening
+draws), then play to the end of every game (legal mask -> build-defined
+splitmix rule pick -> apply_move, incl. chance draws and final scoring).
+The final states of the first and the last timed launch are compared with
+the C oracle board by board.
 Boards are seeded by their global id (rank * 4096 + b), so N GPUs run N
 independent shards (weak scaling, no data-path collective).
+
+`selfplay` sub-object (config 3, profile_self_play.py's loop batched): 4096
+boards x 200 MCTS simulations per move with the default 128-filter x
+8-block network in fp32, 2 warm-up + 3 timed moves; at N > 1 the timed
+moves' (s, pi, player) records are all-gathered over RCCL (config 4's
+exchange) and timed separately.
+
+Other configs: --config 3 (self-play moves only, or --full-game), --config 4
+(whole self-play iterations + the all-gather into every rank's replay
+buffer), --config 5 (the full training loop).
 
 Prints one JSON line (rank 0).  Usage:
   python bench.py [--gpus N] [--steps K] [--warmup W] [--boards 4096]
@@ -35,14 +48,21 @@ BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 PIPELINE_DEPTH = 4         # hz_play launches until every board replays a fully prepared episode
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
+CLOCK_GHZ = 2.4            # MI355X peak engine clock (cycle figures of the issue-bound view)
+MT_SEED_STEPS = 1246       # init_by_array's two 623-step passes: the seeding chain per reset
+MT_STEP_FLOOR_CYCLES = 17  # tools/alu_chain.py: the bare MT recurrence per step
+MEAN_SELFPLAY_PLIES = 62.4  # mean game length
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--boards", type=int, default=4096)
+    ap.add_argument("--launches-per-step", type=int, default=256,
+                    help="config 2: hz_play launches (4096-board batches) per bench step")
     ap.add_argument("--seed-base", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -51,12 +71,28 @@ def parse():
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
-                    help="2: env kernels (default, the headline); 3: MCTS self-play moves with the network; "
-                         "5: whole training iterations (self-play -> buffer -> training -> arena)")
-    ap.add_argument("--iterations", type=int, default=2, help="config 5: training iterations timed")
-    ap.add_argument("--eval-games", type=int, default=32, help="config 5: arena games per evaluation")
-    ap.add_argument("--sims", type=int, default=200, help="config 3: MCTS simulations per move")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
+                         "moves with the network; 4: whole self-play iterations + the RCCL all-gather into "
+                         "every rank's replay buffer; 5: whole training iterations "
+                         "(self-play -> buffer -> training -> arena)")
+    ap.add_argument("--no-selfplay", action="store_true", help="config 2: skip the selfplay sub-object")
+    ap.add_argument("--sp-boards", type=int, default=4096, help="selfplay sub-object: boards per GPU")
+    ap.add_argument("--sp-sims", type=int, default=200, help="selfplay sub-object: simulations per move")
+    ap.add_argument("--sp-warmup", type=int, default=2, help="selfplay sub-object: untimed moves")
+    ap.add_argument("--sp-moves", type=int, default=3, help="selfplay sub-object: timed moves")
+    ap.add_argument("--sp-cpu-seconds", type=float, default=8.0,
+                    help="selfplay sub-object: C-twin MCTS baseline sample (host cores)")
+    ap.add_argument("--iterations", type=int, default=5,
+                    help="config 5: training iterations timed (one evaluation cycle at eval-every 5); "
+                         "config 4: self-play iterations timed")
+    ap.add_argument("--eval-games", type=int, default=30, help="config 5: arena games per evaluation (config.py:92)")
+    ap.add_argument("--eval-every", type=int, default=5, help="config 5: eval_frequency (config.py:94)")
+    ap.add_argument("--eval-sims", type=int, default=200, help="config 5: mcts_config_eval sims (config.py:68)")
+    ap.add_argument("--sims", type=int, default=None,
+                    help="MCTS simulations per move (config 3/4: 200; config 5: 400 = mcts_config_default)")
+    ap.add_argument("--records-out", default=None,
+                    help="config 4: write this rank's replay buffer and own records (torch.save) for tests")
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     ap.add_argument("--full-game", action="store_true",
                     help="config 3: time one complete game on every board (games/s measured, not estimated)")
@@ -108,35 +144,38 @@ def cpu_baseline(boards, seconds):
 def bench_loop(args, dev, rank, world):
     """BASELINE config 5: the reference's main.py loop (trainer.Trainer) on
     the batched engine, one step = one training iteration: `boards` games per
-    rank of self-play with the best model (MCTS `sims` per move, self-play
-    noise), RCCL all-gather of the records into every rank's replay buffer,
-    rank-0 training (reference training config: Adam, batch 64, 2 epochs over
-    the buffer, buffer 50,000), weight broadcast, checkpoint, buffer file, and
-    every iteration an arena of `eval_games` games between candidate and best
-    (mcts_config_eval with `sims` simulations).  Reports games/hour."""
+    rank of self-play with the best model (mcts_config_default: 400 sims per
+    move, self-play noise), RCCL all-gather of the records into every rank's
+    replay buffer, rank-0 training (reference training config: Adam, batch
+    64, 2 epochs over the buffer, buffer 50,000), weight broadcast,
+    checkpoint, buffer file, and every `eval_every` (5) iterations an arena
+    of `eval_games` (30) games between candidate and best
+    (mcts_config_eval, 200 sims), sharded over the ranks.  Reports
+    games/hour over `iterations` (default 5 = one evaluation cycle)."""
     import tempfile
     from hzamd.manager import ModelManager
     from hzamd.net import DEFAULT
     from hzamd.trainer import Trainer
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = True
+    sims = args.sims or 400
     model_cfg = dict(DEFAULT, board_size=(5, 7))
     train_cfg = {"device": str(dev), "optimizer_type": "Adam", "learning_rate": 0.001, "weight_decay": 0.0001,
                  "value_loss_weight": 1.0, "policy_loss_weight": 1.0, "batch_size": 64, "momentum": 0.9,
                  "use_scheduler": True, "scheduler_type": "StepLR", "scheduler_step_size": 30,
                  "scheduler_gamma": 0.5, "force_lr_reset_on_load": False, "new_forced_lr": 0.000125}
-    mcts_cfg = {"num_simulations": args.sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+    mcts_cfg = {"num_simulations": sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
                 "fpu_value": 0.25, "turns_until_tau0": 15, "action_size": 143, "testing": False}
     tmp = tempfile.mkdtemp(prefix=f"hz_loop_r{rank}_")
     sp_cfg = {"num_iterations": args.iterations + 1, "num_games_per_iter": args.boards, "epochs_per_iter": 2,
               "replay_buffer_size": 50000, "checkpoint_folder": os.path.join(tmp, "ck"),
               "replay_buffer_folder": os.path.join(tmp, "buf"), "replay_buffer_filename": "replay_buffer.pkl",
-              "eval_frequency": 1, "eval_episodes": args.eval_games, "eval_win_rate_threshold": 0.51,
+              "eval_frequency": args.eval_every, "eval_episodes": args.eval_games, "eval_win_rate_threshold": 0.51,
               "best_model_filename": "best_model.pth.tar"}
     mm = ModelManager(model_cfg, train_cfg)
-    tr = Trainer(mm, mcts_cfg, sp_cfg, train_cfg, eval_mcts_config={"num_simulations": args.sims},
+    tr = Trainer(mm, mcts_cfg, sp_cfg, train_cfg, eval_mcts_config={"num_simulations": args.eval_sims},
                  seed_base=args.seed_base, log=lambda *_: None)
-    # warm-up iteration (kernels, MIOpen algorithm search), then the timed ones
+    # warm-up iteration (kernels, allocator), then the timed ones
     tr.iteration = 0
     tr.execute_self_play_phase(tr.best_model_manager)
     tr.execute_training_phase()
@@ -145,7 +184,7 @@ def bench_loop(args, dev, rank, world):
         dist.barrier()
     t0 = time.perf_counter()
     phases = {"self_play": 0.0, "training": 0.0, "evaluation": 0.0}
-    games = 0
+    games, evals = 0, 0
     for it in range(1, args.iterations + 1):
         tr.iteration = it
         a = time.perf_counter()
@@ -159,13 +198,17 @@ def bench_loop(args, dev, rank, world):
         tr.save_buffer()
         torch.cuda.synchronize(dev)
         c = time.perf_counter()
-        tr.evaluate_model()
+        if it % args.eval_every == 0:
+            tr.evaluate_model()
+            evals += 1
         torch.cuda.synchronize(dev)
         d = time.perf_counter()
         phases["self_play"] += b - a
         phases["training"] += c - b
         phases["evaluation"] += d - c
         games += sp["games"]
+        print(f"[config5] iteration {it}: self-play {b - a:.1f}s training {c - b:.1f}s eval {d - c:.1f}s",
+              file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -173,16 +216,65 @@ def bench_loop(args, dev, rank, world):
     if world > 1:
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     if rank == 0:
+        ref = (sims == 400 and args.eval_sims == 200 and args.eval_games == 30 and args.eval_every == 5)
         print(json.dumps({
             "metric": "full loop self-play games/hour (self-play -> buffer -> training -> arena)",
             "value": games / elapsed * 3600.0, "unit": "games/hour", "n_gpus": world, "steps": args.iterations,
             "warmup": 1, "ms_per_step": elapsed * 1000.0 / args.iterations, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic: random-init network, seeded games",
-            "config": {"workload": f"config5: {args.boards} games/rank/iteration, {args.sims} sims/move, "
-                                   f"arena {args.eval_games} games every iteration, default 128fx8 net",
-                       "boards_per_gpu": args.boards, "sims": args.sims, "parallelism": f"shard{world}"},
-            "phase_seconds": phases, "games": games,
+            "config": {"workload": f"config5: {args.boards} games/rank/iteration, {sims} sims/move, arena "
+                                   f"{args.eval_games} games x {args.eval_sims} sims every {args.eval_every} "
+                                   f"iterations, default 128fx8 net"
+                                   + ("" if ref else " (deviates from config.py:53-99)"),
+                       "boards_per_gpu": args.boards, "sims": sims, "eval_sims": args.eval_sims,
+                       "eval_games": args.eval_games, "eval_frequency": args.eval_every,
+                       "reference_config": ref, "parallelism": f"shard{world}"},
+            "phase_seconds": phases, "games": games, "evaluations": evals,
         }))
+
+
+class TimedEvaluator:
+    """Wraps the leaf evaluator: HIP events around every call (the current
+    stream, where the network's kernels run) and the rows it computed."""
+
+    device_rows = True
+
+    def __init__(self, pred, dev):
+        self.pred = pred
+        self.events = []
+        self.rows = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def __call__(self, board, glob, rows=None, count=None):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = self.pred(board, glob, rows, count)
+        b.record()
+        self.events.append((a, b))
+        self.rows += count if count is not None else board.shape[0]
+        return out
+
+    def reset(self):
+        torch.cuda.synchronize()
+        self.events.clear()
+        self.rows.zero_()
+
+    def ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+def _selfplay_setup(args, dev, rank, sims, n):
+    from hzamd.mcts import BatchedPredictor
+    from hzamd.net import HarmoniesNet
+    from hzamd.selfplay import SelfPlay
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = True
+    net = HarmoniesNet().to(dev).eval()
+    dtype = torch.bfloat16 if args.nn_dtype == "bf16" else None
+    ev = TimedEvaluator(BatchedPredictor(net, dtype=dtype), dev)
+    cfg = {"num_simulations": sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+           "turns_until_tau0": 15, "testing": False}
+    sp = SelfPlay(n, ev, cfg, seed_base=args.seed_base + rank * n, device=dev)
+    return sp, ev
 
 
 def bench_selfplay(args, dev, rank, world):
@@ -190,35 +282,15 @@ def bench_selfplay(args, dev, rank, world):
     the default 128-filter x 8-block network (random init, torch.manual_seed(0),
     BatchedPredictor = ModelManager.predict batched).  One step = one move of
     every board (full search + choice + env step)."""
-    from hzamd.mcts import BatchedPredictor
-    from hzamd.net import HarmoniesNet, flops_per_eval
-    from hzamd.selfplay import SelfPlay
-    torch.manual_seed(0)
-    torch.backends.cudnn.benchmark = True
-    net = HarmoniesNet().to(dev).eval()
-    dtype = torch.bfloat16 if args.nn_dtype == "bf16" else None
-    pred = BatchedPredictor(net, dtype=dtype)
-    nn_ev = []
-
-    def evaluator(board, glob):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        out = pred(board, glob)
-        b.record()
-        nn_ev.append((a, b))
-        return out
-
-    n = args.boards
-    cfg = {"num_simulations": args.sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
-           "turns_until_tau0": 15, "testing": False}
-    sp = SelfPlay(n, evaluator, cfg, seed_base=args.seed_base + rank * n, device=dev)
+    from hzamd.net import flops_per_eval
+    n, sims = args.boards, args.sims or 200
+    sp, ev = _selfplay_setup(args, dev, rank, sims, n)
     if args.full_game:
-        return bench_selfplay_games(args, sp, nn_ev, dev, rank, world)
+        return bench_selfplay_games(args, sp, ev, dev, rank, world, sims)
     sp.env.reset()
     for w in range(args.warmup):
         sp.move(w)
-    torch.cuda.synchronize(dev)
-    nn_ev.clear()
+    ev.reset()
     edges = 0
     if world > 1:
         dist.barrier()
@@ -231,31 +303,32 @@ def bench_selfplay(args, dev, rank, world):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    nn_ms = sum(a.elapsed_time(b) for a, b in nn_ev)
-    sims_done = n * args.sims * args.steps
+    nn_ms = ev.ms()
+    rows = int(ev.rows.item())
+    sims_done = n * sims * args.steps
     if world > 1:
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     sims_all = sims_done * world
     per_move = elapsed / args.steps
-    avg_plies = 62.4  # mean game length
     fl = flops_per_eval()
     if rank == 0:
         print(json.dumps({
-            "metric": "self-play MCTS simulations/sec (= NN leaf evals/s) @4096 boards x 200 sims",
+            "metric": "self-play MCTS simulations/sec @4096 boards x 200 sims",
             "value": sims_all / elapsed, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": per_move * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
-            "config": {"workload": f"config3: {n} boards x {args.sims} sims/move, default 128fx8 net",
-                       "boards_per_gpu": n, "sims": args.sims, "parallelism": f"shard{world}"},
-            "games_per_s_est": world * n / (per_move * avg_plies),
+            "config": {"workload": f"config3: {n} boards x {sims} sims/move, default 128fx8 net",
+                       "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
+            "games_per_s_est": world * n / (per_move * MEAN_SELFPLAY_PLIES),
             "env_steps_per_s": (edges + n * args.steps) * world / elapsed,
-            "nn_ms_per_move": nn_ms / args.steps, "tree_ms_per_move": per_move * 1e3 - nn_ms / args.steps,
-            "nn_tflops": fl * n * args.sims * args.steps / (nn_ms * 1e-3) / 1e12,
-            "note": "games/s estimated from ms per move x mean game length 62.4 plies",
+            "nn_rows_evaluated": rows, "nn_ms_per_move": nn_ms / args.steps,
+            "tree_ms_per_move": per_move * 1e3 - nn_ms / args.steps,
+            "nn_tflops": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
+            "note": f"games/s estimated from ms per move x mean game length {MEAN_SELFPLAY_PLIES} plies",
         }))
 
 
-def bench_selfplay_games(args, sp, nn_ev, dev, rank, world):
+def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
     """Config 3, measured end to end: after `warmup` moves of a throw-away
     game, every board plays one whole self-play game (search + choice + env
     step per ply, records kept on the device as SelfPlay.play does); games/s
@@ -265,14 +338,11 @@ def bench_selfplay_games(args, sp, nn_ev, dev, rank, world):
     sp.env.reset()
     for w in range(args.warmup):
         sp.move(w)
-    torch.cuda.synchronize(dev)
-    nn_ev.clear()
-    plies = [0]
+    ev.reset()
     orig_move = sp.move
 
     def move(ply, done=None):  # progress on stderr (a long run must not look hung)
         out = orig_move(ply, done)
-        plies[0] = ply + 1
         if ply % 8 == 0:
             print(f"[config3 full game] ply {ply}", file=sys.stderr, flush=True)
         return out
@@ -286,8 +356,9 @@ def bench_selfplay_games(args, sp, nn_ev, dev, rank, world):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     sp.move = orig_move
-    evals = int(rec["valid"].sum().item()) * args.sims
-    nn_ms = sum(a.elapsed_time(b) for a, b in nn_ev)
+    moves = int(rec["valid"].sum().item())
+    nn_ms = ev.ms()
+    rows = int(ev.rows.item())
     if world > 1:
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     if rank == 0:
@@ -296,12 +367,224 @@ def bench_selfplay_games(args, sp, nn_ev, dev, rank, world):
             "value": world * n / elapsed, "unit": "games/s", "n_gpus": world, "steps": 1, "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
-            "config": {"workload": f"config3: {n} boards x {args.sims} sims/move, one whole game per board",
-                       "boards_per_gpu": n, "sims": args.sims, "parallelism": f"shard{world}"},
-            "plies": rec["plies"], "moves": int(rec["valid"].sum().item()),
-            "sims_per_s": world * evals / elapsed, "nn_s": nn_ms * 1e-3,
-            "nn_tflops": flops_per_eval() * n * args.sims * len(nn_ev) / args.sims / (nn_ms * 1e-3) / 1e12
-            if nn_ms else None,
+            "config": {"workload": f"config3: {n} boards x {sims} sims/move, one whole game per board",
+                       "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
+            "plies": rec["plies"], "moves": moves, "sims_per_s": world * moves * sims / elapsed,
+            "nn_rows_evaluated": rows, "nn_rows_skipped": moves * sims - rows, "nn_s": nn_ms * 1e-3,
+            "nn_tflops": flops_per_eval() * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
+        }))
+
+
+def selfplay_probe(args, dev, rank, world):
+    """The `selfplay` sub-object of the default line: config 3 per move
+    (profile_self_play.py:17-77's loop, batched) and, at N > 1, config 4's
+    RCCL all-gather of the timed moves' records.  Returns a dict on rank 0."""
+    from hzamd import distributed as hd
+    from hzamd.net import flops_per_eval
+    n, sims = args.sp_boards, args.sp_sims
+    sp, ev = _selfplay_setup(args, dev, rank, sims, n)
+    sp.env.reset()
+    for w in range(args.sp_warmup):
+        sp.move(w)
+    torch.cuda.synchronize(dev)
+    # root states + streams of the first timed move: the CPU twin's sample
+    cpu_roots = sp.env.export_state(with_mt=True) if rank == 0 and world == 1 else None
+    sp.keep_noise = True
+    sp.noise_log.clear()
+    ev.reset()
+    recs = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.sp_moves):
+        recs.append(sp.move(args.sp_warmup + k))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    nn_ms = ev.ms()
+    rows = int(ev.rows.item())
+    board_moves = int(sum(int(a.sum().item()) for _, _, a in recs))
+    sims_done = board_moves * sims
+    exchange = None
+    if world > 1:
+        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
+        sims_all, rows_all = (int(x) for x in all_reduce([sims_done, rows], dist.ReduceOp.SUM))
+        # config 4's exchange on the records of the timed moves (z pending:
+        # the games are not over; the bytes and the collective are the same)
+        st = torch.cat([s.t()[a] for s, _, a in recs])
+        vis = torch.cat([v[a] for _, v, a in recs])
+        player = ((st[:, 5] >> 41) & 1).to(torch.int8)
+        packed = hd.pack_records(st, vis, torch.zeros(st.shape[0], dtype=torch.int8, device=dev), player)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        x0 = time.perf_counter()
+        gathered = hd.all_gather_records(packed)
+        torch.cuda.synchronize(dev)
+        xdt = time.perf_counter() - x0
+        xdt = all_reduce([xdt], dist.ReduceOp.MAX)[0]
+        nbytes = gathered.numel() * 8
+        exchange = {"collective": "all_gather (counts) + all_gather_into_tensor (records)",
+                    "records": int(gathered.shape[0]), "bytes_per_rank_received": nbytes,
+                    "ms": xdt * 1e3, "GBps": nbytes / xdt / 1e9,
+                    "records_per_move_per_rank": int(packed.shape[0]) / args.sp_moves,
+                    "est_ms_per_iteration": xdt * 1e3 / args.sp_moves * MEAN_SELFPLAY_PLIES,
+                    "note": "records of the timed moves (336 B each); a self-play iteration exchanges "
+                            "~62 plies' worth once"}
+    else:
+        sims_all, rows_all = sims_done, rows
+    per_move = elapsed / args.sp_moves
+    fl = flops_per_eval()
+    nn_tf = fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None
+    out = None
+    if rank == 0:
+        out = {"workload": f"config3: {n} boards/GPU x {sims} sims/move, default 128fx8 net, fp32 "
+                           f"({args.sp_warmup} warm-up + {args.sp_moves} timed moves from the game start)",
+               "sims_per_s": sims_all / elapsed, "nn_evals_per_s": rows_all / elapsed,
+               "games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
+               "games_per_s_basis": f"ms per move x mean game length {MEAN_SELFPLAY_PLIES} plies; "
+                                    "complete games: bench.py --config 3 --full-game",
+               "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
+               "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
+               "nn_rows_evaluated": rows, "sims": sims_done,
+               "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": nn_tf / FP32_MFMA_PEAK_TFLOPS if nn_tf else None,
+                               "flop_per_eval": fl, "basis": "whole leaf-eval forward (HIP events around "
+                                                             "each call) incl. the linear layers"},
+               "exchange": exchange, "dtype": "fp32", "n_gpus": world}
+        if cpu_roots is not None and args.sp_cpu_seconds > 0:
+            out["cpu_baseline"] = selfplay_cpu_baseline(cpu_roots, sp.noise_log[0][0], sims, args.sp_cpu_seconds)
+    sp.mcts.close()
+    sp.env.close()
+    return out
+
+
+def selfplay_cpu_baseline(roots, noise, sims, seconds):
+    """The C twin's MCTS (oracle/hz_oracle.c or_mcts_search, the reference's
+    get_best_action_and_pi restated) on the box's host cores: the first timed
+    move's root states and streams, same sims / cpuct / noise, the stub
+    evaluator in place of the network (tree work only), boards spread over
+    threads (ctypes releases the GIL); plus the reference network's batch-1
+    CPU forward (ModelManager.predict's shape) timed separately."""
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    import oracle
+    from hzamd.net import HarmoniesNet
+    from hzamd.state import unpack_ref
+    st, mt, idx = (t.cpu().numpy() for t in roots)
+    mt = mt.view(np.uint32)
+    nz = noise.cpu().numpy()
+    nthreads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    nb = st.shape[1]
+
+    def one(b):
+        m = oracle.mt_from_words(mt[b], idx[b])
+        ref = unpack_ref(st[:, b])
+        if oracle.is_game_over(ref):
+            return 0
+        oracle.mcts_search(ref, m, sims, 2.0, eps=0.25, testing=False, tau0=15, ply=0, noise=nz[b])
+        return sims
+
+    done, b0 = 0, 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(nthreads) as pool:
+        while time.perf_counter() - t0 < seconds and b0 < nb:
+            chunk = list(range(b0, min(nb, b0 + 4 * nthreads)))
+            done += sum(pool.map(one, chunk))
+            b0 += len(chunk)
+    dt = time.perf_counter() - t0
+    # one search on one thread, for the per-core figure
+    t1 = time.perf_counter()
+    k1, s1 = 0, 0
+    while time.perf_counter() - t1 < min(2.0, seconds / 4):
+        s1 += one(k1 % nb)
+        k1 += 1
+    dt1 = time.perf_counter() - t1
+    net = HarmoniesNet().eval()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(nthreads)
+    with torch.no_grad():
+        b, g = torch.zeros(1, 38, 5, 7), torch.zeros(1, 42)
+        for _ in range(5):
+            net(b, g)
+        t2 = time.perf_counter()
+        for _ in range(40):
+            net(b, g)
+        nn_s = (time.perf_counter() - t2) / 40
+    torch.set_num_threads(prev)
+    tree_1 = s1 / dt1
+    return {"value": done / dt, "unit": "sims/s", "cores": nthreads, "kind": "port",
+            "value_1core": tree_1, "nn_cpu_ms_per_eval": nn_s * 1e3,
+            "est_sims_per_s_one_process": 1.0 / (1.0 / tree_1 + nn_s),
+            "sample": f"{b0} boards' first timed move searched ({done} sims, {sims} per board) in {dt:.1f}s by the "
+                      f"C twin's or_mcts_search on {nthreads} threads with the stub evaluator (tree work only); "
+                      f"1 thread: {k1} searches in {dt1:.1f}s; the reference net's batch-1 CPU forward "
+                      f"({nthreads} intra-op threads) timed separately; est_sims_per_s_one_process = one "
+                      f"reference-shaped process (one tree, one predict per leaf)"}
+
+
+def bench_exchange(args, dev, rank, world):
+    """BASELINE config 4: every rank plays `iterations` self-play iterations
+    (SelfPlay.iteration: one whole game on each of its 4096 boards, seeded by
+    global board id) and all-gathers the packed (s, pi, z) records over RCCL
+    into every rank's device replay buffer (trainer.py:104-127's Pool
+    fan-out + replay_buffer.extend).  Self-play and the exchange are timed
+    separately; value = games of all ranks / total time."""
+    from hzamd import distributed as hd
+    n, sims = args.boards, args.sims or 200
+    sp, ev = _selfplay_setup(args, dev, rank, sims, n)
+    buf = hd.ReplayBuffer(max(50000, 2 * n * 80 * world), dev)
+    # warm-up: a few moves (kernels, allocator) and one exchange
+    sp.env.reset()
+    for w in range(min(2, args.warmup)):
+        sp.move(w)
+    if world > 1:
+        hd.all_gather_records(torch.zeros(1, hd.RECORD_WORDS, dtype=torch.int64, device=dev))
+    torch.cuda.synchronize(dev)
+    own = []
+    t_play = t_x = 0.0
+    games = examples = 0
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for it in range(args.iterations):
+        tm = {}
+        gathered, _ = sp.iteration(buf, timings=tm)
+        t_play += tm["play_s"]
+        t_x += tm["exchange_s"]
+        games += n * world
+        examples += int(gathered.shape[0])
+        own.append(tm["own_records"])
+        print(f"[config4] iteration {it}: self-play {tm['play_s']:.1f}s exchange {tm['exchange_s'] * 1e3:.1f} ms "
+              f"({int(gathered.shape[0])} records)", file=sys.stderr, flush=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed, t_play, t_x = all_reduce([elapsed, t_play, t_x], dist.ReduceOp.MAX)
+    if args.records_out:
+        torch.save({"buffer": buf.records().cpu(), "own": torch.cat(own).cpu(),
+                    "own_counts": torch.tensor([o.shape[0] for o in own]), "rank": rank, "world": world},
+                   f"{args.records_out}.rank{rank}.pt")
+    nbytes = examples * hd.RECORD_WORDS * 8
+    if rank == 0:
+        print(json.dumps({
+            "metric": "self-play games/sec @4096 boards/GPU x 200 MCTS sims + RCCL all-gather of (s, pi, z)",
+            "value": games / elapsed, "unit": "games/s", "n_gpus": world, "steps": args.iterations,
+            "warmup": 1, "ms_per_step": elapsed * 1e3 / args.iterations, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.nn_dtype,
+            "data": "synthetic: random-init network, seeded games",
+            "config": {"workload": f"config4: {n} boards/GPU x {sims} sims/move, whole games, records "
+                                   f"all-gathered into every rank's replay buffer",
+                       "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
+            "self_play_s": t_play, "exchange": {"ms": t_x * 1e3, "records": examples,
+                                                "bytes_per_rank_received": nbytes,
+                                                "GBps": nbytes / t_x / 1e9 if t_x > 0 and world > 1 else None,
+                                                "collective": "all_gather (counts) + all_gather_into_tensor"
+                                                if world > 1 else "none (one rank)"},
+            "examples_per_iteration": examples / args.iterations,
         }))
 
 
@@ -330,21 +613,23 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    if args.config == 3:
-        bench_selfplay(args, dev, rank, world)
+    if args.config in (3, 4):
+        (bench_selfplay if args.config == 3 else bench_exchange)(args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return
 
     from hzamd.env import BatchedEnv
+    from hzamd.state import unpack_ref
 
-    n = args.boards
+    n, L = args.boards, args.launches_per_step
     env = BatchedEnv(n, seed_base=args.seed_base + rank * n, device=dev)
     games = torch.zeros(n, dtype=torch.int32, device=dev)
     steps = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    launches = [0]  # hz_play launches so far: launch k plays every board's episode k
 
-    def one_step(ev=None, g=games, s=steps):
+    def one_launch(ev=None, g=games, s=steps):
         # hz_play: HarmoniesGameState() on every board fused with rule-driven
         # play to the end of the game, one launch
         if ev:
@@ -352,44 +637,52 @@ def main():
         env.rollout(MAX_PLIES, games_done=g, steps_done=s, reset=True)
         if ev:
             ev[1].record(stream)
+        launches[0] += 1
 
     # first batch (episode 0: board b seeded seed_base + rank*n + b) doubles as
-    # the parity guard: its env-step count must equal the C oracle's
-    one_step()
+    # a parity guard: its env-step count must equal the C oracle's
+    one_launch()
     torch.cuda.synchronize(dev)
     first_steps = int(steps.sum().item())
     # the chance-ahead pipeline (seed -> draw1 -> draw2 -> play) is primed
-    # after three launches; fewer warm-up steps than that get extra untimed
-    # priming launches, reported as pipeline_prime
-    prime = max(0, PIPELINE_DEPTH - args.warmup)
-    for _ in range(max(0, args.warmup - 1) + prime):
-        one_step()
+    # after three launches; warm-up is at least that many
+    prime = max(0, PIPELINE_DEPTH - args.warmup * L)
+    for _ in range(max(0, args.warmup * L - 1) + prime):
+        one_launch()
     torch.cuda.synchronize(dev)
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    # per-step counters of the timed launches (each step plays a new episode)
-    games_t = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
-    steps_t = torch.zeros(args.steps, n, dtype=torch.int32, device=dev)
+    # per-launch counters of the timed launches (each launch plays a new episode)
+    T = args.steps * L
+    games_t = torch.zeros(T, n, dtype=torch.int32, device=dev)
+    steps_t = torch.zeros(T, n, dtype=torch.int32, device=dev)
+    first_ep = launches[0]
+    first_state = torch.empty(6, n, dtype=torch.int64, device=dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(None, games_t[i], steps_t[i])
+    for i in range(T):
+        one_launch(None, games_t[i], steps_t[i])
+        if i == 0:  # the first timed batch's final states, for the oracle check (a 196 KB copy)
+            first_state.copy_(env.export_state())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    last_ep = launches[0] - 1
+    last_state = env.export_state()
     # the dominant kernel's average launch duration, from HIP events around
     # each launch on its stream, in a separate loop of the same launches (the
     # event markers would otherwise sit between the timed launches)
-    for i in range(args.steps):
-        one_step(evs[i], games, steps)
+    K = min(T, 512)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for i in range(K):
+        one_launch(evs[i], games, steps)
     torch.cuda.synchronize(dev)
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / K
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
+    longest = int(steps_t.max())
     if world > 1:
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
         c = all_reduce([timed_steps, timed_games], dist.ReduceOp.SUM)
@@ -402,7 +695,7 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # roofline of the dominant kernel (hz_play = k_rollout with reset), per launch
-    alg_bytes = (timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET) / args.steps
+    alg_bytes = (timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET) / T
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -410,22 +703,45 @@ def main():
             traffic = json.load(open(args.traffic_json)).get("k_rollout_bytes_per_launch")
         except Exception:
             traffic = None
+    cycles = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
+    issue = {"kernel_cycles": cycles, "longest_game_plies": longest,
+             "cycles_per_ply_longest_game": cycles / max(1, longest),
+             "cycles_per_mt_seed_step": cycles / MT_SEED_STEPS, "mt_step_floor_cycles": MT_STEP_FLOOR_CYCLES,
+             "note": f"a launch is the longest serial per-lane chain of its roles (one board's whole game, or a "
+                     f"stream's {MT_SEED_STEPS}-step seeding) at {CLOCK_GHZ} GHz; the bare MT recurrence costs "
+                     f"{MT_STEP_FLOOR_CYCLES} cycles/step (tools/alu_chain.py), DESIGN.md §3"}
 
     # the same workload with chance-ahead off (every launch seeds and draws
     # in-kernel), for comparison; not the headline number
     off_steps, off_elapsed = 0, float("nan")
     if not args.no_off_compare:
-        off_steps, off_elapsed = off_compare(env, one_step, games, args, dev, world)
+        off_steps, off_elapsed = off_compare(env, one_launch, games, args, dev, world)
 
     api = None
     if args.api_mode and rank == 0:
         api = api_mode(env, dev, stream)
     enc = encoder_roofline(dev, n, args.seed_base) if rank == 0 else None
 
+    parity = None
     if rank == 0:
         import oracle  # test infrastructure: parity guard + cpu_baseline only
         ref_total = oracle.play_rule_games(n, args.seed_base, nthreads=8)[0]
         assert ref_total == first_steps, (ref_total, first_steps)
+        checked = []
+        for ep, stt in ((first_ep, first_state), (last_ep, last_state)):
+            got = stt.cpu().numpy()
+            _, finals, _, _ = oracle.play_rule_games(n, args.seed_base, nthreads=8, episode=ep)
+            bad = [b for b in range(n) if not (unpack_ref(got[:, b]) == finals[b]).all()]
+            assert not bad, f"episode {ep}: boards {bad[:8]} differ from the C oracle"
+            checked.append(ep)
+        parity = (f"first batch: {first_steps} env steps == C oracle ({ref_total}); final states of the first and "
+                  f"last timed batches (episodes {checked[0]}, {checked[1]}): {n}/{n} boards bit-exact vs C oracle")
+    sp = None
+    if not args.no_selfplay:
+        env.close()
+        sp = selfplay_probe(args, dev, rank, world)
+
+    if rank == 0:
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(n, args.cpu_seconds)
         out = {
             "metric": "self-play env-steps/sec + games/sec @4096 boards, 1/2/4/8 GPUs; bit-exact vs CPU",
@@ -441,14 +757,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic: CPython-seeded games, seeds = global board id, build-defined splitmix rule policy",
-            "config": {"workload": "config2: 4096 concurrent boards/GPU, reset + rule-driven play to game end "
-                                   "(legal mask, step, chance draws, final scoring), one hz_play launch",
-                       "boards_per_gpu": n, "env_steps_per_step": timed_steps / args.steps,
+            "config": {"workload": f"config2: 4096 concurrent boards/GPU, reset + rule-driven play to game end "
+                                   f"(legal mask, step, chance draws, final scoring); one step = {L} hz_play "
+                                   f"launches of 4096 boards",
+                       "boards_per_gpu": n, "launches_per_step": L, "env_steps_per_step": timed_steps / args.steps,
                        "games_per_step": timed_games / args.steps, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "kernel_ms": kern_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "kernel": "k_rollout", "kernel_ms": kern_ms, "kernel_ms_launches": K,
+                         "alg_bytes_per_launch": alg_bytes, "issue_bound": issue},
             "chance_ahead": {"on": True, "note": "each hz_play also prepares every board's next three episodes "
                                                  "as a pipeline on the other CUs (stream seeding, pile draws and "
                                                  "rule hashes, none of which depends on moves); steady state: one "
@@ -458,12 +775,14 @@ def main():
                              "ms_per_step_off": (off_elapsed * 1000.0 / args.steps) if off_steps else None},
             "encoder_roofline": enc,
             "cpu_baseline": cpu,
-            "parity": f"first batch: {first_steps} env steps == C oracle ({ref_total})",
+            "parity": parity,
+            "selfplay": sp,
         }
         if api:
             out["api_path"] = api
         print(json.dumps(out))
-    env.close()
+    if args.no_selfplay:
+        env.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -495,19 +814,20 @@ def encoder_roofline(dev, n, seed_base):
             "bytes_per_state": BYTES_PER_ENCODE}
 
 
-def off_compare(env, one_step, games, args, dev, world):
+def off_compare(env, one_launch, games, args, dev, world):
     """Time the same workload with chance-ahead off (every launch seeds and
     draws in-kernel); returns (env steps of all ranks, max elapsed)."""
     env.set_seed_ahead(False)
     for _ in range(2):
-        one_step()
+        one_launch()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    steps_o = torch.zeros(args.steps, env.n, dtype=torch.int32, device=dev)
+    T = args.steps * args.launches_per_step
+    steps_o = torch.zeros(T, env.n, dtype=torch.int32, device=dev)
     t1 = time.perf_counter()
-    for i in range(args.steps):
-        one_step(None, games, steps_o[i])
+    for i in range(T):
+        one_launch(None, games, steps_o[i])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -59,10 +59,11 @@ constexpr uint64_t kCodeSetLo = code_sets(0, 4), kCodeSetMid = code_sets(4, 4), 
 
 __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
                                                       long item_stride, const int32_t *__restrict__ idx, int m,
-                                                      float *__restrict__ board) {
+                                                      const int32_t *__restrict__ mcount, float *__restrict__ board) {
   __shared__ uint64_t smask[kEncWaves][76];
   __shared__ float sval[kEncWaves][76];
   int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (mcount) m = *mcount < m ? *mcount : m;  // device-side item count (compacted leaf batches)
   long j0 = 2 * ((long)blockIdx.x * kEncWaves + w);
   bool live = j0 < m;
 #pragma unroll
@@ -146,8 +147,9 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
 
 __global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict__ st, long word_stride,
                                                      long item_stride, const int32_t *__restrict__ idx, int m,
-                                                     float *__restrict__ glob) {
+                                                     const int32_t *__restrict__ mcount, float *__restrict__ glob) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mcount) m = *mcount < m ? *mcount : m;
   if (i >= m * 42) return;
   int j = i / 42, f = i - j * 42;
   long b = idx ? (long)idx[j] : (long)j;
@@ -174,16 +176,18 @@ __global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict_
   glob[i] = val;
 }
 
+// mcount (device pointer, may be NULL): only items [0, min(m, *mcount)) are
+// written; the grid is sized for m.
 inline void launch_encode(const uint64_t *st, long word_stride, long item_stride, const int32_t *idx, int m,
-                          float *board, float *glob, hipStream_t stream) {
+                          float *board, float *glob, hipStream_t stream, const int32_t *mcount = nullptr) {
   if (board) {
     long pairs = ((long)m + 1) / 2;
     hipLaunchKernelGGL(k_encode_board, dim3((unsigned)((pairs + kEncWaves - 1) / kEncWaves)), dim3(256), 0, stream,
-                       st, word_stride, item_stride, idx, m, board);
+                       st, word_stride, item_stride, idx, m, mcount, board);
   }
   if (glob) {
     hipLaunchKernelGGL(k_encode_glob, dim3((unsigned)((m * 42 + 255) / 256)), dim3(256), 0, stream, st,
-                       word_stride, item_stride, idx, m, glob);
+                       word_stride, item_stride, idx, m, mcount, glob);
   }
 }
 

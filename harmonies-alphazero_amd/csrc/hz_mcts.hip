@@ -48,6 +48,8 @@ struct hz_mcts {
   int32_t *depth;        // [n]
   int32_t *leaf;         // [n]  leaf node of the current simulation, -1 = inactive
   int32_t *leaf_gidx;    // [n]  b*max_nodes + leaf for the encoder, -1 = no eval
+  int32_t *slot;         // [n]  row of board b in the gathered leaf batch, -1 = not evaluated
+  int32_t *gidx_c;       // [n]  leaf_gidx of the gathered rows, in board order
 };
 
 namespace {
@@ -190,6 +192,44 @@ __global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__re
   }
 }
 
+// ------------------------------------------------------------ gather leaves
+// The boards whose selected leaf needs the network (active, not terminal:
+// MCTS.py:297-341 never calls predict on a terminal leaf), in board order:
+// rows[j] = board of gathered row j, slot[b] = j (or -1), count[0] = rows.
+// One workgroup; thread t owns boards [t*per, (t+1)*per) (contiguous, so the
+// exclusive scan of the per-thread counts keeps board order).
+constexpr int kGatherThreads = 1024;
+__global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *__restrict__ rows,
+                                                           int32_t *__restrict__ count) {
+  __shared__ int32_t part[kGatherThreads];
+  const int t = threadIdx.x;
+  const int per = (m.n + kGatherThreads - 1) / kGatherThreads;
+  const int b0 = t * per < m.n ? t * per : m.n, b1 = b0 + per < m.n ? b0 + per : m.n;
+  int c = 0;
+  for (int b = b0; b < b1; b++) c += m.leaf_gidx[b] >= 0;
+  part[t] = c;
+  __syncthreads();
+  for (int o = 1; o < kGatherThreads; o <<= 1) {
+    int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int j = part[t] - c;
+  for (int b = b0; b < b1; b++) {
+    int g = m.leaf_gidx[b];
+    if (g >= 0) {
+      m.slot[b] = j;
+      m.gidx_c[j] = g;
+      if (rows) rows[j] = b;
+      j++;
+    } else {
+      m.slot[b] = -1;
+    }
+  }
+  if (t == kGatherThreads - 1) count[0] = part[t];
+}
+
 // ---------------------------------------------------------- expand + backup
 struct ExpandLds {
   uint32_t mt[kMT];
@@ -208,7 +248,8 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
                                                          const float *__restrict__ policy,
                                                          const float *__restrict__ value,
                                                          const double *__restrict__ noise, double eps,
-                                                         float one_minus_eps, int testing) {
+                                                         float one_minus_eps, int testing,
+                                                         const int32_t *__restrict__ row_of) {
   __shared__ ExpandLds L;
   int b = blockIdx.x;
   int lane = threadIdx.x;
@@ -218,6 +259,9 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
   size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
   State ls = load_node(m.node_state + (nb + leaf) * 6);
   int leaf_player = player_of(ls.misc);
+  // policy/value row of this board: its own (per-board batch) or its row in
+  // the gathered batch (hz_mcts_gather_leaves)
+  const size_t row = row_of ? (size_t)row_of[b] : (size_t)b;
   double v;
   if (game_done(ls.misc)) {
     // MCTS.py:333-341: outcome from the leaf player's perspective
@@ -225,7 +269,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
     double outcome = wc == 1 ? 1.0 : wc == 2 ? -1.0 : 0.0;
     v = (wc == 3) ? 0.0 : (leaf_player == 0 ? outcome : -outcome);
   } else {
-    v = (double)value[b];
+    v = (double)value[row];
     uint64_t mk[3];
     int nl = legal_mask(ls, mk);
     bool noisy = leaf == 0 && !testing && noise;
@@ -352,7 +396,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
           }
           if (f != 2) {
             int a = kth_action(mk, c);
-            float p = policy[(size_t)b * kActions + a];
+            float p = policy[row * kActions + a];
             if (noisy) p = __double2float_rn(__dadd_rn((double)__fmul_rn(one_minus_eps, p),
                                                        __dmul_rn(eps, noise[(size_t)b * kMaxChildren + c])));
             int e = base_e + (L.flag[c] >> 4);
@@ -428,7 +472,8 @@ hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, 
             alloc(&m->node_ne, N) && alloc(&m->edge_action, E) && alloc(&m->edge_child, E) &&
             alloc(&m->edge_n, E) && alloc(&m->edge_w, E) && alloc(&m->edge_p, E) && alloc(&m->edge_player, E) &&
             alloc(&m->ht, n * m->hcap) && alloc(&m->counts, n * 4) && alloc(&m->path, n * max_depth) &&
-            alloc(&m->depth, n) && alloc(&m->leaf, n) && alloc(&m->leaf_gidx, n);
+            alloc(&m->depth, n) && alloc(&m->leaf, n) && alloc(&m->leaf_gidx, n) && alloc(&m->slot, n) &&
+            alloc(&m->gidx_c, n);
   if (ok) {
     ok = hipMemset(m->ht, 0, n * m->hcap * sizeof(uint64_t)) == hipSuccess &&
          hipMemset(m->counts, 0, n * 4 * sizeof(int32_t)) == hipSuccess &&
@@ -447,7 +492,7 @@ void hz_mcts_destroy(hz_mcts *m) {
   if (!m) return;
   void *ptrs[] = {m->node_state, m->node_hash, m->node_e0,   m->node_ne, m->edge_action, m->edge_child,
                   m->edge_n,     m->edge_w,    m->edge_p,    m->edge_player, m->ht, m->counts,
-                  m->path,       m->depth,     m->leaf,      m->leaf_gidx};
+                  m->path,       m->depth,     m->leaf,      m->leaf_gidx, m->slot, m->gidx_c};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   free(m);
@@ -478,13 +523,30 @@ int hz_mcts_encode_leaves(hz_mcts *m, float *board, float *glob) {
   return launch_err();
 }
 
-int hz_mcts_expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
-                          double eps, int32_t testing) {
+int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, int32_t *count) {
+  if (!m || !count || (!board && !glob)) return -1;
+  hipLaunchKernelGGL(k_gather, dim3(1), dim3(kGatherThreads), 0, m->stream, *m, rows, count);
+  launch_encode(m->node_state, 1, 6, m->gidx_c, m->n, board, glob, m->stream, count);
+  return launch_err();
+}
+
+static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
+                         double eps, int32_t testing, const int32_t *slot) {
   if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
   float ome = (float)(1.0 - eps);
   hipLaunchKernelGGL(k_expand_backup, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing);
+                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
   return launch_err();
+}
+
+int hz_mcts_expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
+                          double eps, int32_t testing) {
+  return expand_backup(m, env, policy, value, noise, eps, testing, nullptr);
+}
+
+int hz_mcts_expand_backup_gathered(hz_mcts *m, hz_env *env, const float *policy, const float *value,
+                                   const double *noise, double eps, int32_t testing) {
+  return m ? expand_backup(m, env, policy, value, noise, eps, testing, m->slot) : -1;
 }
 
 int hz_mcts_result(hz_mcts *m, int32_t *visits) {

@@ -105,11 +105,14 @@ __device__ uint64_t g_conv_stamps[1024][2][10];
 
 __global__ void __launch_bounds__(512, 1)
     k_conv3x3_w8(const float *__restrict__ x, const float4 *__restrict__ wp, const float *__restrict__ bias,
-                 const float *__restrict__ res, float *__restrict__ out, int32_t batch) {
+                 const float *__restrict__ res, float *__restrict__ out, int32_t batch,
+                 const int32_t *__restrict__ live) {
   extern __shared__ float4 lds4[];
   float *lds = (float *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
   const int s0 = blockIdx.x * kCS;
+  if (live) batch = *live < batch ? *live : batch;  // rows past the live count are not computed
+  if (s0 >= batch) return;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
   HZ_STAMP(0)
 #ifdef HZ_NET_DIAG
@@ -264,7 +267,7 @@ __global__ void __launch_bounds__(512, 1)
 }  // namespace
 
 extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res,
-                                   float *out, int32_t batch, void *stream) {
+                                   float *out, int32_t batch, const int32_t *live, void *stream) {
   if (!x || !wpack || !bias || !out || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)wpack | (uintptr_t)out | (uintptr_t)res) & 15) return -1;
   if (batch == 0) return 0;
@@ -280,7 +283,7 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
   hipLaunchKernelGGL(k_conv3x3_w8, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, x,
-                     (const float4 *)wpack, bias, res, out, batch);
+                     (const float4 *)wpack, bias, res, out, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -304,9 +307,12 @@ namespace {
 
 __global__ void __launch_bounds__(256) k_heads(const float *__restrict__ x, const float *__restrict__ hw,
                                                const float *__restrict__ hb, const float *__restrict__ glob,
-                                               float *__restrict__ pcat, float *__restrict__ vcat, int32_t batch) {
+                                               float *__restrict__ pcat, float *__restrict__ vcat, int32_t batch,
+                                               const int32_t *__restrict__ live) {
   __shared__ float4 w4[3][32];
   const int t = threadIdx.x, lane = t & 63;
+  if (live) batch = *live < batch ? *live : batch;
+  if (blockIdx.x * 4 >= batch) return;
   if (t < 96) w4[t >> 5][t & 31] = ((const float4 *)hw)[t];
   __syncthreads();
   const int b = blockIdx.x * 4 + (t >> 6);
@@ -338,12 +344,12 @@ __global__ void __launch_bounds__(256) k_heads(const float *__restrict__ x, cons
 }  // namespace
 
 extern "C" int hz_heads(const float *x, const float *hw, const float *hb, const float *glob, float *pcat,
-                        float *vcat, int32_t batch, void *stream) {
+                        float *vcat, int32_t batch, const int32_t *live, void *stream) {
   if (!x || !hw || !hb || !glob || !pcat || !vcat || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)hw) & 15) return -1;
   if (batch == 0) return 0;
   hipLaunchKernelGGL(k_heads, dim3((batch + 3) / 4), dim3(256), 0, (hipStream_t)stream, x, hw, hb, glob, pcat,
-                     vcat, batch);
+                     vcat, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -365,11 +371,13 @@ constexpr int kStemIt = (kStemN + 511) / 512;    // per thread (21)
 
 __global__ void __launch_bounds__(512, 1)
     k_stem3x3(const float *__restrict__ board, const float4 *__restrict__ wp, const float *__restrict__ bias,
-              float *__restrict__ out, int32_t batch) {
+              float *__restrict__ out, int32_t batch, const int32_t *__restrict__ live) {
   extern __shared__ float4 lds4[];
   float *lds = (float *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
   const int s0 = blockIdx.x * kCS;
+  if (live) batch = *live < batch ? *live : batch;
+  if (s0 >= batch) return;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
 
   // all of this thread's board loads are issued first (coalesced along the
@@ -461,7 +469,7 @@ __global__ void __launch_bounds__(512, 1)
 }  // namespace
 
 extern "C" int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bias, float *out,
-                                   int32_t batch, void *stream) {
+                                   int32_t batch, const int32_t *live, void *stream) {
   if (!board || !wpack || !bias || !out || batch < 0) return -1;
   if (((uintptr_t)wpack | (uintptr_t)out) & 15) return -1;
   if (batch == 0) return 0;
@@ -476,6 +484,6 @@ extern "C" int hz_stem3x3_bias_act(const float *board, const float *wpack, const
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
   hipLaunchKernelGGL(k_stem3x3, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, board,
-                     (const float4 *)wpack, bias, out, batch);
+                     (const float4 *)wpack, bias, out, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -49,13 +49,15 @@ _SIGS = {
     "hz_mcts_select": ([_vp, _vp, _c.c_float], _c.c_int),
     "hz_mcts_encode_leaves": ([_vp, _vp, _vp], _c.c_int),
     "hz_mcts_expand_backup": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
+    "hz_mcts_gather_leaves": ([_vp, _vp, _vp, _vp, _vp], _c.c_int),
+    "hz_mcts_expand_backup_gathered": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
     "hz_mcts_result": ([_vp, _vp], _c.c_int),
     "hz_mcts_stats": ([_vp, _vp], _c.c_int),
     "hz_mcts_leaf_ptrs": ([_vp, _vp, _vp], _c.c_int),
     "hz_bias_act": ([_vp, _vp, _vp, _c.c_int64, _c.c_int32, _vp], _c.c_int),
-    "hz_conv3x3_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp], _c.c_int),
-    "hz_heads": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp], _c.c_int),
-    "hz_stem3x3_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp], _c.c_int),
+    "hz_conv3x3_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_heads": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_stem3x3_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_version": ([], _c.c_char_p),
 }
 

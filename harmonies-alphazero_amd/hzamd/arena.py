@@ -54,23 +54,33 @@ class MctsAgent:
         return self._search(env, mask, self.evaluator)
 
 
-def _routed(eval_a, eval_b, a_rows):
-    """One leaf batch, each row evaluated by its board's searching agent."""
-    ia = torch.nonzero(a_rows).flatten()
-    ib = torch.nonzero(~a_rows).flatten()
+class _Routed:
+    """One leaf batch, each row evaluated by its board's searching agent.
+    BatchedMCTS gathers the leaves that need the network (device_rows):
+    row j belongs to board rows[j], so the agent is picked by rows[j], never
+    by the row's position."""
 
-    def evaluator(board, glob):
+    device_rows = True
+
+    def __init__(self, eval_a, eval_b, a_rows):
+        self.eval_a, self.eval_b, self.a_rows = eval_a, eval_b, a_rows
+
+    def __call__(self, board, glob, rows=None, count=None):
+        if rows is not None:
+            k = int(count.item())
+            board, glob = board[:k], glob[:k]
+            a = self.a_rows.index_select(0, rows[:k].to(torch.int64))
+        else:
+            a = self.a_rows
         n = board.shape[0]
         policy = torch.zeros(n, 143, dtype=torch.float32, device=board.device)
         value = torch.zeros(n, dtype=torch.float32, device=board.device)
-        for idx, ev in ((ia, eval_a), (ib, eval_b)):
+        for idx, ev in ((torch.nonzero(a).flatten(), self.eval_a), (torch.nonzero(~a).flatten(), self.eval_b)):
             if idx.numel():
                 p, v = ev(board.index_select(0, idx), glob.index_select(0, idx))
                 policy.index_copy_(0, idx, p.to(torch.float32))
                 value.index_copy_(0, idx, v.reshape(-1).to(torch.float32))
         return policy, value
-
-    return evaluator
 
 
 def summarize(outcome_a):
@@ -85,14 +95,14 @@ def summarize(outcome_a):
             "win_rate": 0.5 if decisive == 0 else wins / decisive}
 
 
-def play_games(agent_a, agent_b, n_games, seed_base=0, device="cuda", max_plies=200, env=None):
-    """Play n_games (board g seeded seed_base + g); A plays P0 in even games.
-    Returns (outcome from A's perspective int64 [n], final state words [6, n],
-    plies played)."""
-    env = env or BatchedEnv(n_games, seed_base=seed_base, device=device)
+def play_games(agent_a, agent_b, n_games, seed_base=0, device="cuda", max_plies=200, env=None, first_game=0):
+    """Play games first_game .. first_game + n_games - 1 (game g seeded
+    seed_base + g); A plays P0 in even games.  Returns (outcome from A's
+    perspective int64 [n], final state words [6, n], plies played)."""
+    env = env or BatchedEnv(n_games, seed_base=seed_base + first_game, device=device)
     env.reset()
     n, d = env.n, env.device
-    a_is_p0 = (torch.arange(n, device=d) % 2) == 0
+    a_is_p0 = ((torch.arange(n, device=d) + first_game) % 2) == 0
     shared = (isinstance(agent_a, MctsAgent) and isinstance(agent_b, MctsAgent)
               and agent_a.cfg == agent_b.cfg and agent_a.exact_keys == agent_b.exact_keys)
     ply = 0
@@ -105,7 +115,7 @@ def play_games(agent_a, agent_b, n_games, seed_base=0, device="cuda", max_plies=
         a_turn = ((to_move == 0) == a_is_p0) & ~done
         b_turn = ~a_turn & ~done
         if shared:
-            act = agent_a._search(env, ~done, _routed(agent_a.evaluator, agent_b.evaluator, a_turn))
+            act = agent_a._search(env, ~done, _Routed(agent_a.evaluator, agent_b.evaluator, a_turn))
         else:
             act = torch.full((n,), -1, dtype=torch.int64, device=d)
             for agent, mask in ((agent_a, a_turn), (agent_b, b_turn)):
@@ -124,14 +134,43 @@ def play_games(agent_a, agent_b, n_games, seed_base=0, device="cuda", max_plies=
     return outcome_a, final, ply
 
 
+def shard(n_games, rank, world):
+    """Games [first, first + count) of rank `rank` when n_games are split
+    over `world` ranks as evenly as possible (the first n % world ranks get
+    one more)."""
+    q, r = divmod(int(n_games), int(world))
+    count = q + (1 if rank < r else 0)
+    return rank * q + min(rank, r), count
+
+
 def evaluate_model(candidate_evaluator, best_evaluator, n_games=30, threshold=0.51, mcts_config=None,
-                   seed_base=0, device="cuda"):
+                   seed_base=0, device="cuda", group=None):
     """Trainer.evaluate_model (trainer.py:293-375) batched: returns the
     summary from the candidate's perspective plus `passed` (win_rate >
-    threshold, i.e. the candidate becomes the best model)."""
-    cand = MctsAgent(candidate_evaluator, mcts_config)
-    best = MctsAgent(best_evaluator, mcts_config)
-    outcome, _, _ = play_games(cand, best, n_games, seed_base=seed_base, device=device)
-    s = summarize(outcome)
+    threshold, i.e. the candidate becomes the best model).
+
+    With torch.distributed initialised the n_games are sharded over the
+    ranks (game g is the same game at any world size: seed seed_base + g,
+    candidate P0 in even g) and the win/loss/draw counts are all-reduced, so
+    every rank returns the same summary and promotion decision."""
+    import torch.distributed as dist
+    from . import distributed as hd
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    first, count = shard(n_games, rank, world)
+    counts = torch.zeros(3, dtype=torch.int64)
+    if count:
+        cand = MctsAgent(candidate_evaluator, mcts_config)
+        best = MctsAgent(best_evaluator, mcts_config)
+        outcome, _, _ = play_games(cand, best, count, seed_base=seed_base, device=device, first_game=first)
+        o = outcome.cpu()
+        counts = torch.tensor([int((o == 1).sum()), int((o == -1).sum()), int((o == 0).sum())])
+    if world > 1:
+        t = counts.to(hd.collective_device(group))
+        dist.all_reduce(t, group=group)
+        counts = t.cpu()
+    wins, losses, draws = (int(c) for c in counts)
+    decisive = wins + losses
+    s = {"wins": wins, "losses": losses, "draws": draws, "win_rate": 0.5 if decisive == 0 else wins / decisive}
     s["passed"] = s["win_rate"] > threshold
     return s

@@ -41,6 +41,14 @@ def unpack_records(rec):
     return states, visits, z, player
 
 
+def collective_device(group=None):
+    """Where a small control tensor must live for a collective: the CPU under
+    gloo, the current GPU under RCCL ("nccl")."""
+    if dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
 def pi_of(visits):
     v = visits.to(torch.float64)
     t = v.sum(1, keepdim=True)
@@ -49,23 +57,27 @@ def pi_of(visits):
 
 def all_gather_records(rec, group=None):
     """Variable-length all-gather: counts first (int64), then one padded
-    all_gather_into_tensor of the packed records; rank order preserved."""
+    all_gather_into_tensor of the packed records; rank order preserved.
+    Under RCCL the records move GPU to GPU over xGMI; under gloo (CPU
+    rehearsals, which cannot all-gather device tensors) they are staged
+    through host memory."""
     world = dist.get_world_size(group)
     dev = rec.device
-    cnt = torch.tensor([rec.shape[0]], dtype=torch.int64, device=dev)
+    cdev = collective_device(group)
+    src = rec.to(cdev)
+    cnt = torch.tensor([src.shape[0]], dtype=torch.int64, device=cdev)
     counts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt, group=group)
     counts = [int(c.item()) for c in counts]
     mx = max(counts)
-    pad = torch.zeros(mx, RECORD_WORDS, dtype=torch.int64, device=dev)
-    pad[:rec.shape[0]] = rec
-    out = torch.empty(world * mx, RECORD_WORDS, dtype=torch.int64, device=dev)
-    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+    pad = torch.zeros(mx, RECORD_WORDS, dtype=torch.int64, device=cdev)
+    pad[:src.shape[0]] = src
+    out = torch.empty(world * mx, RECORD_WORDS, dtype=torch.int64, device=cdev)
+    if cdev.type == "cuda" and hasattr(dist, "all_gather_into_tensor"):
         dist.all_gather_into_tensor(out, pad, group=group)
     else:
-        parts = list(out.split(mx))
-        dist.all_gather(parts, pad, group=group)
-    return torch.cat([out[r * mx: r * mx + counts[r]] for r in range(world)])
+        dist.all_gather(list(out.split(mx)), pad, group=group)
+    return torch.cat([out[r * mx: r * mx + counts[r]] for r in range(world)]).to(dev)
 
 
 def broadcast_weights(model, src=0, group=None):

@@ -32,7 +32,16 @@ def pack_conv3x3(w):
     return w.permute(2, 3, 1, 0).reshape(9, ci // 16, 16, co).permute(0, 1, 3, 2).contiguous()
 
 
-def _conv3x3_act(x, wpack, b, res=None):
+def _live_ptr(live):
+    """Device int32 scalar bounding the rows the HIP kernels compute (None = all)."""
+    if live is None:
+        return None
+    if not (live.is_cuda and live.dtype == torch.int32):
+        raise NativeError("live row count must be a CUDA int32 tensor")
+    return live.data_ptr()
+
+
+def _conv3x3_act(x, wpack, b, res=None, live=None):
     """relu((conv3x3(x) + b) + res) for a 128-channel NHWC activation, one HIP launch."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
             and x.shape[1:] == (128, 5, 7)):
@@ -42,7 +51,7 @@ def _conv3x3_act(x, wpack, b, res=None):
     out = torch.empty_like(x, memory_format=torch.channels_last)
     rc = lib().hz_conv3x3_bias_act(x.data_ptr(), wpack.data_ptr(), b.data_ptr(),
                                    res.data_ptr() if res is not None else None, out.data_ptr(), x.shape[0],
-                                   torch.cuda.current_stream(x.device).cuda_stream)
+                                   _live_ptr(live), torch.cuda.current_stream(x.device).cuda_stream)
     if rc != 0:
         raise NativeError(f"hz_conv3x3_bias_act failed ({rc})")
     return out
@@ -56,7 +65,7 @@ def pack_stem(w):
     return pack_conv3x3(w48)
 
 
-def _stem_act(board, wpack, b):
+def _stem_act(board, wpack, b, live=None):
     """relu(conv3x3(board) + b) from the encoder's NCHW board, NHWC out, one HIP launch."""
     if not (board.is_cuda and board.dtype == torch.float32 and board.shape[1:] == (38, 5, 7)):
         raise NativeError("hz_stem3x3_bias_act needs a CUDA fp32 [B,38,5,7] board")
@@ -64,13 +73,13 @@ def _stem_act(board, wpack, b):
     out = torch.empty(board.shape[0], 128, 5, 7, dtype=torch.float32, device=board.device,
                       memory_format=torch.channels_last)
     rc = lib().hz_stem3x3_bias_act(board.data_ptr(), wpack.data_ptr(), b.data_ptr(), out.data_ptr(),
-                                   board.shape[0], torch.cuda.current_stream(board.device).cuda_stream)
+                                   board.shape[0], _live_ptr(live), torch.cuda.current_stream(board.device).cuda_stream)
     if rc != 0:
         raise NativeError(f"hz_stem3x3_bias_act failed ({rc})")
     return out
 
 
-def _heads(x, glob, hw, hb):
+def _heads(x, glob, hw, hb, live=None):
     """(relu(policy conv1x1) flattened NCHW || glob, relu(value conv1x1) || glob)
     for the default heads (2 + 1 filters on the 5x7 board), one HIP launch."""
     B = x.shape[0]
@@ -81,7 +90,7 @@ def _heads(x, glob, hw, hb):
     pcat = torch.empty(B, 112, dtype=torch.float32, device=x.device)
     vcat = torch.empty(B, 77, dtype=torch.float32, device=x.device)
     rc = lib().hz_heads(x.data_ptr(), hw.data_ptr(), hb.data_ptr(), glob.data_ptr(), pcat.data_ptr(),
-                        vcat.data_ptr(), B, torch.cuda.current_stream(x.device).cuda_stream)
+                        vcat.data_ptr(), B, _live_ptr(live), torch.cuda.current_stream(x.device).cuda_stream)
     if rc != 0:
         raise NativeError(f"hz_heads failed ({rc})")
     return pcat, vcat
@@ -140,9 +149,11 @@ class FoldedNet(nn.Module):
             self.packed = [(pack_conv3x3(w1), pack_conv3x3(w2)) for (w1, _), (w2, _) in self.blocks]
         self.pconv = _fold(n.policy_conv, n.policy_bn)
         self.vconv = _fold(n.value_conv, n.value_bn)
-        self.pfc = (n.policy_fc.weight.detach(), n.policy_fc.bias.detach())
-        self.vfc1 = (n.value_fc1.weight.detach(), n.value_fc1.bias.detach())
-        self.vfc2 = (n.value_fc2.weight.detach(), n.value_fc2.bias.detach())
+        # snapshots like the folded convs: an optimizer step on the source
+        # net changes nothing here until refresh()
+        self.pfc = (n.policy_fc.weight.detach().clone(), n.policy_fc.bias.detach().clone())
+        self.vfc1 = (n.value_fc1.weight.detach().clone(), n.value_fc1.bias.detach().clone())
+        self.vfc2 = (n.value_fc2.weight.detach().clone(), n.value_fc2.bias.detach().clone())
         # both heads' 1x1 convs + ReLU + flatten + concat with glob: one HIP pass
         self.heads = None
         if (self.native_conv and self.pconv[0].shape == (2, 128, 1, 1) and self.vconv[0].shape == (1, 128, 1, 1)
@@ -151,23 +162,27 @@ class FoldedNet(nn.Module):
                           torch.cat((self.pconv[1], self.vconv[1])).contiguous())
 
     @torch.no_grad()
-    def forward(self, board, glob):
+    def forward(self, board, glob, live=None):
+        """live (CUDA int32 [1], optional): only rows < live[0] are needed;
+        the HIP kernels skip the others (their outputs are unspecified)."""
         ep = self.epilogue
         w, b = self.stem
+        if self.stem_packed is None or self.packed is None:
+            live = None
         if self.stem_packed is not None:
-            x = _stem_act(board, self.stem_packed, b)  # reads the NCHW board directly
+            x = _stem_act(board, self.stem_packed, b, live)  # reads the NCHW board directly
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
         if self.packed is not None:
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
-                y = _conv3x3_act(x, p1, b1)
-                x = _conv3x3_act(y, p2, b2, x)
+                y = _conv3x3_act(x, p1, b1, None, live)
+                x = _conv3x3_act(y, p2, b2, x, live)
         else:
             for (w1, b1), (w2, b2) in self.blocks:
                 y = ep(F.conv2d(x, w1, None, padding=1), b1)
                 x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
         if self.heads is not None:
-            pcat, vcat = _heads(x, glob, *self.heads)
+            pcat, vcat = _heads(x, glob, *self.heads, live=live)
             logits = F.linear(pcat, *self.pfc)
             v = F.linear(vcat, *self.vfc1).relu_()
             return logits, torch.tanh(F.linear(v, *self.vfc2))

@@ -2,13 +2,22 @@
 in lock-step so that every simulation's leaf evaluations form one PyTorch
 batch (the reference evaluates one leaf at a time: MCTS.py:291-352).
 
-    select (HIP) -> encode leaves (HIP) -> evaluator(board, glob) (PyTorch)
-    -> expand + backup (HIP)
+    select (HIP) -> gather + encode the leaves that need the network (HIP)
+    -> evaluator(board, glob) (PyTorch) -> expand + backup (HIP)
 
-The evaluator is any callable (board f32[n,38,5,7], glob f32[n,42]) ->
-(policy f32[n,143] probabilities, value f32[n]) on the same device, e.g.
+Like the reference, which calls predict only for non-terminal leaves
+(MCTS.py:297-341), each simulation's batch holds only the active boards
+whose selected leaf is not terminal, gathered in board order on the device.
+
+The evaluator is any callable (board f32[k,38,5,7], glob f32[k,42]) ->
+(policy f32[k,143] probabilities, value f32[k]) on the same device, e.g.
 `BatchedPredictor(model)` wrapping model.py's AlphaZeroModel the way
 ModelManager.predict does (softmax over all 143 logits, model.py:81-110).
+An evaluator with `device_rows = True` is instead called as
+evaluator(board, glob, rows, count) on the full [n]-row buffers, of which
+the first count[0] (a device int32) are live and rows[j] is row j's board:
+no host round trip per simulation (BatchedPredictor's HIP kernels take
+count as their live-row bound).
 """
 import torch
 
@@ -16,7 +25,6 @@ from . import _native as nat
 from .env import ACTION_SIZE
 
 MAX_CHILDREN = 69
-COMPACT_BUCKET = 256  # leaf batches of active boards are rounded up to this
 
 
 class BatchedMCTS:
@@ -36,6 +44,11 @@ class BatchedMCTS:
         self.glob = torch.zeros(self.n, 42, dtype=torch.float32, device=d)
         self.visits = torch.zeros(self.n, ACTION_SIZE, dtype=torch.int32, device=d)
         self.counts = torch.zeros(self.n, 4, dtype=torch.int32, device=d)
+        self.rows = torch.zeros(self.n, dtype=torch.int32, device=d)
+        self.count = torch.zeros(1, dtype=torch.int32, device=d)
+        self.eval_rows = torch.zeros(1, dtype=torch.int64, device=d)  # leaves evaluated, last search
+        self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
+        self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -66,14 +79,24 @@ class BatchedMCTS:
                   "hz_mcts_encode_leaves")
         return self.board, self.glob
 
-    def expand_backup(self, policy, value, noise=None, eps=0.25, testing=True):
+    def gather_leaves(self):
+        """The leaves that need the network, in board order: (board, glob,
+        rows, count) with rows [0, count[0]) live (hz_mcts_gather_leaves)."""
+        nat.check(nat.lib().hz_mcts_gather_leaves(self._h, nat.ptr(self.board), nat.ptr(self.glob),
+                                                  nat.ptr(self.rows), nat.ptr(self.count)),
+                  "hz_mcts_gather_leaves")
+        return self.board, self.glob, self.rows, self.count
+
+    def expand_backup(self, policy, value, noise=None, eps=0.25, testing=True, gathered=False):
+        if policy.numel() == 0:  # no leaf needed the network (never read, but not NULL)
+            policy, value = self._nil_pol, self._nil_val
         policy = policy.to(dtype=torch.float32).contiguous()
         value = value.reshape(-1).to(dtype=torch.float32).contiguous()
         if noise is not None:
             noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
-        nat.check(nat.lib().hz_mcts_expand_backup(self._h, self.env.handle, nat.ptr(policy), nat.ptr(value),
-                                                  nat.ptr(noise), float(eps), int(bool(testing))),
-                  "hz_mcts_expand_backup")
+        fn = nat.lib().hz_mcts_expand_backup_gathered if gathered else nat.lib().hz_mcts_expand_backup
+        nat.check(fn(self._h, self.env.handle, nat.ptr(policy), nat.ptr(value), nat.ptr(noise), float(eps),
+                     int(bool(testing))), "hz_mcts_expand_backup")
 
     def result(self):
         nat.check(nat.lib().hz_mcts_result(self._h, nat.ptr(self.visits)), "hz_mcts_result")
@@ -85,39 +108,38 @@ class BatchedMCTS:
 
     # -- one full search per board -------------------------------------------
     def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None,
-               compact=True):
+               gather=True):
         """get_best_action_and_pi's simulation loop (MCTS.py:288-352) for every
         active board; returns root visit counts int32 [n, 143].
 
-        With `compact` and some boards inactive (games already over), only the
-        active boards' leaves go to the evaluator: rows gathered, the batch
-        rounded up to a multiple of COMPACT_BUCKET (repeats of the first
-        active row; at most n / COMPACT_BUCKET distinct shapes), results
-        scattered back.  Inactive boards take no part in expand/backup, so
-        their rows were never read; a row-wise evaluator gives every active
-        board the same priors and value either way."""
+        gather (default): each simulation evaluates only the leaves that need
+        the network (module docstring); `eval_rows` counts them on the device.
+        gather=False evaluates one row per board (terminal leaves and inactive
+        boards included, their results unused), as before."""
         if active is not None:
             active = active.to(device=self.device, dtype=torch.uint8).contiguous()
         self.begin(active)
-        rows = None
-        if compact and active is not None:
-            k = int(active.sum())  # one host sync per search (the ply loop syncs anyway)
-            if 0 < k < self.n:
-                rows = torch.nonzero(active, as_tuple=False).flatten()
-                kp = min(self.n, -(-k // COMPACT_BUCKET) * COMPACT_BUCKET)
-                gather = torch.cat((rows, rows[:1].expand(kp - k))) if kp > k else rows
-                pol = torch.zeros(self.n, ACTION_SIZE, dtype=torch.float32, device=self.device)
-                val = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+        self.eval_rows.zero_()
+        device_rows = bool(getattr(evaluator, "device_rows", False))
         for _ in range(self.num_simulations if sims is None else int(sims)):
             self.select(cpuct, active)
-            board, glob = self.encode_leaves()
-            if rows is None:
+            if not gather:
+                board, glob = self.encode_leaves()
                 policy, value = evaluator(board, glob)
+                self.eval_rows += self.n
+                self.expand_backup(policy, value, noise, eps, testing)
+                continue
+            board, glob, rows, count = self.gather_leaves()
+            self.eval_rows += count
+            if device_rows:
+                policy, value = evaluator(board, glob, rows, count)
             else:
-                pc, vc = evaluator(board.index_select(0, gather), glob.index_select(0, gather))
-                policy = pol.index_copy_(0, rows, pc[:k].to(torch.float32))
-                value = val.index_copy_(0, rows, vc.reshape(-1)[:k].to(torch.float32))
-            self.expand_backup(policy, value, noise, eps, testing)
+                k = int(count.item())  # one host read per simulation
+                if k:
+                    policy, value = evaluator(board[:k], glob[:k])
+                else:
+                    policy, value = self._nil_pol, self._nil_val
+            self.expand_backup(policy, value, noise, eps, testing, gathered=True)
         return self.result()
 
 
@@ -147,7 +169,11 @@ def pi_from_visits(visits):
 
 class BatchedPredictor:
     """ModelManager.predict (model.py:81-110) for a whole batch: eval mode,
-    no grad, softmax over all 143 logits (illegal moves are not masked)."""
+    no grad, softmax over all 143 logits (illegal moves are not masked).
+    Called by BatchedMCTS with the device row count (device_rows): the
+    folded net's HIP kernels compute only the live rows."""
+
+    device_rows = True
 
     def __init__(self, model, dtype=None, fold=True):
         self.model = model
@@ -165,16 +191,18 @@ class BatchedPredictor:
             self.fast.refresh()
 
     @torch.no_grad()
-    def __call__(self, board, glob):
+    def __call__(self, board, glob, rows=None, count=None):
         self.model.eval()
         low = self.dtype is not None and self.dtype != torch.float32
-        # the folded net's HIP epilogue is fp32-only; autocast runs the source net
-        net = self.fast if self.fast is not None and not low else self.model
+        # the folded net's HIP kernels are fp32-only; autocast runs the source
+        # net (on every row: it has no live-row bound)
         if low:
             with torch.autocast(device_type="cuda", dtype=self.dtype):
-                logits, value = net(board, glob)
+                logits, value = self.model(board, glob)
+        elif self.fast is not None:
+            logits, value = self.fast(board, glob, live=count)
         else:
-            logits, value = net(board, glob)
+            logits, value = self.model(board, glob)
         return torch.softmax(logits.float(), dim=1), value.float().reshape(-1)
 
 

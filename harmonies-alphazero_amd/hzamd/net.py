@@ -1,10 +1,14 @@
 """Policy/value network with the reference architecture (model.py:277-394).
 
-The leaf evaluator stays stock PyTorch-ROCm: this module
-only restates the architecture so that self-play can run where the reference
-checkout is absent, with parameter names matching model.py so that
-`model_state_dict` entries of the reference's checkpoints
-(model.py:161-182) load unchanged.
+This module restates the architecture (training runs it as a plain PyTorch
+module) with parameter names matching model.py, so that `model_state_dict`
+entries of the reference's checkpoints (model.py:161-182) load unchanged.
+Leaf evaluation does not run it as is: hzamd.infer.FoldedNet folds its
+eval-mode BatchNorms and runs the stem, the 16 tower convs and the heads as
+hand-written HIP MFMA kernels (csrc/hz_net.hip); only the heads' linear
+layers stay PyTorch.  (SURVEY §2 row 5 planned a stock-PyTorch leaf
+evaluator; the network is 97 % of a 200-sim move, so it was replaced — see
+DESIGN.md §0.)
 
 Stem conv3x3 (38 -> F) + BN + ReLU; R residual blocks
 (conv-BN-ReLU-conv-BN + skip, ReLU); policy head conv1x1 (F -> 2) + BN + ReLU,

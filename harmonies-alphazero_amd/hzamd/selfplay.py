@@ -133,20 +133,34 @@ class SelfPlay:
         return {"states": states.contiguous(), "visits": visits, "pi": pi, "z": z[mask].contiguous(),
                 "player": rec["players"][mask], "board": board_id}
 
-    def iteration(self, buffer=None, group=None):
+    def iteration(self, buffer=None, group=None, timings=None):
         """One self-play phase: every board plays a game; with torch.distributed
         initialised the packed records of all ranks are all-gathered (RCCL)
-        into `buffer` (a distributed.ReplayBuffer) on every rank."""
+        into `buffer` (a distributed.ReplayBuffer) on every rank, in rank
+        order.  timings (a dict, optional) gets "play_s" and "exchange_s"
+        (device-synchronised; the exchange starts after a barrier)."""
         from . import distributed as hd
+        import time
         import torch.distributed as dist
+        t0 = time.perf_counter()
         rec = self.play()
         comp = self.compact(rec)
         packed = hd.pack_records(comp["states"], comp["visits"], comp["z"], comp["player"])
-        if dist.is_available() and dist.is_initialized():
-            packed = hd.all_gather_records(packed, group)
+        distributed = dist.is_available() and dist.is_initialized()
+        if timings is not None:
+            torch.cuda.synchronize(self.device)
+            timings["play_s"] = time.perf_counter() - t0
+            timings["own_records"] = packed
+            if distributed:
+                dist.barrier(group)
+        t1 = time.perf_counter()
+        out = hd.all_gather_records(packed, group) if distributed else packed
         if buffer is not None:
-            buffer.extend(packed)
-        return packed, rec
+            buffer.extend(out)
+        if timings is not None:
+            torch.cuda.synchronize(self.device)
+            timings["exchange_s"] = time.perf_counter() - t1
+        return out, rec
 
     def examples(self, compact):
         """The reference's replay-buffer tuples (trainer.py:529-538), on CPU."""

@@ -70,16 +70,20 @@ class Trainer:
 
     def _initialize_best_model(self):
         """trainer.py:262-290: load the best checkpoint, or save the current
-        model as the initial best."""
+        model as the initial best.  Under torch.distributed only rank 0
+        decides (does a loadable best checkpoint exist?); every rank then
+        takes the same, unconditional barrier before the others load."""
         folder = self.self_play_config["checkpoint_folder"]
         self.best_model_manager = ModelManager(copy.deepcopy(self.model_manager.model_config),
                                                copy.deepcopy(self.model_manager.training_config))
-        loaded, _ = self.best_model_manager.load_checkpoint(folder=folder, filename=self.best_model_filename)
-        if not loaded:
-            if self.rank == 0:
+        loaded = False
+        if self.rank == 0:
+            loaded, _ = self.best_model_manager.load_checkpoint(folder=folder, filename=self.best_model_filename)
+            if not loaded:
                 self.model_manager.save_checkpoint(folder=folder, filename=self.best_model_filename)
-            if _dist():
-                dist.barrier()
+        if _dist():
+            dist.barrier()  # the file rank 0 may just have written is complete
+        if self.rank != 0 or not loaded:
             self.best_model_manager.load_checkpoint(folder=folder, filename=self.best_model_filename)
 
     # -- phases --------------------------------------------------------------
@@ -113,6 +117,10 @@ class Trainer:
         return res
 
     def evaluate_model(self):
+        """trainer.py:293-375: the eval_episodes games are sharded over the
+        ranks and their counts all-reduced (hzamd.arena.evaluate_model), so
+        the promotion decision is the same on every rank; the barrier before
+        the reload is unconditional on all ranks whenever it is taken."""
         c = self.self_play_config
         res = arena.evaluate_model(BatchedPredictor(self.model_manager.model),
                                    BatchedPredictor(self.best_model_manager.model),

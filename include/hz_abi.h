@@ -168,6 +168,14 @@ int hz_mcts_select(hz_mcts *mcts, const uint8_t *active, float cpuct);
 /* create_state_tensors of every board's selected leaf into board[n][38][5][7],
  * glob[n][42]; rows of terminal leaves / inactive boards are zero */
 int hz_mcts_encode_leaves(hz_mcts *mcts, float *board, float *glob);
+/* The leaves that need the network, gathered: the active boards whose
+ * selected leaf is not terminal (MCTS.py:297-341 calls predict only for
+ * those), in ascending board order.  count[0] (device) = k; rows[j] (may be
+ * NULL, [n]) = board of row j; board[j] / glob[j] for j < k get the leaf's
+ * create_state_tensors, rows >= k are not written.  No host round trip: the
+ * leaf-eval kernels below take `count` as their live-row bound.  Pair with
+ * hz_mcts_expand_backup_gathered. */
+int hz_mcts_gather_leaves(hz_mcts *mcts, float *board, float *glob, int32_t *rows, int32_t *count);
 /* expand_leaf (MCTS.py:151-218) with policy[n][143] (probabilities, as
  * ModelManager.predict returns them, model.py:81-110), root Dirichlet mix
  * (MCTS.py:308-327) when !testing using noise[n][69] (i-th legal move), then
@@ -176,6 +184,10 @@ int hz_mcts_encode_leaves(hz_mcts *mcts, float *board, float *glob);
  * board's MT stream in child order, like the reference's apply_move calls. */
 int hz_mcts_expand_backup(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
                           const double *noise, double eps, int32_t testing);
+/* the same with policy[k][143] / value[k] in the row order of the last
+ * hz_mcts_gather_leaves (board b reads row j where rows[j] = b) */
+int hz_mcts_expand_backup_gathered(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
+                                   const double *noise, double eps, int32_t testing);
 /* root visit counts by action id: visits[n][143] (MCTS.py:355-376) */
 int hz_mcts_result(hz_mcts *mcts, int32_t *visits);
 /* per-board [nodes, edges, search generation, overflow flag] -> counts[n][4] */
@@ -183,7 +195,10 @@ int hz_mcts_stats(hz_mcts *mcts, int32_t *counts);
 /* host pointers to the device arrays leaf[n] / leaf_gidx[n] (debugging) */
 int hz_mcts_leaf_ptrs(hz_mcts *mcts, int32_t **leaf, int32_t **leaf_gidx);
 
-/* ---- leaf-eval epilogue (hzamd/infer.py) ---------------------------------- */
+/* ---- leaf-eval kernels (hzamd/infer.py) ---------------------------------- */
+/* `live` (device pointer, may be NULL) bounds the rows computed: rows
+ * >= min(batch, *live) are neither read nor written (gathered leaf batches
+ * whose size is known only on the device). */
 /* x[rows][ch] = relu((x + bias[c]) + res) in place (res may be NULL): the
  * eval-mode BatchNorm (folded into the conv) -> [+ skip] -> ReLU tail of
  * model.py:376-393 (ResidualBlock.forward) and model.py:325-330 (stem) over an
@@ -197,21 +212,21 @@ int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int
  * [kh*3+kw][ci/16][co][ci%16] (hzamd/infer.py:pack_conv3x3).  f32 MFMA, exact
  * fp32 products and sums (summation order differs from MIOpen's). */
 int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res, float *out,
-                        int32_t batch, void *stream);
+                        int32_t batch, const int32_t *live, void *stream);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the
  * encoder writes it, out NHWC [batch][5][7][128], wpack = w with the input
  * channels zero-padded to 48, packed as for hz_conv3x3_bias_act. */
 int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bias, float *out, int32_t batch,
-                        void *stream);
+                        const int32_t *live, void *stream);
 
 /* The heads of model.py:336-351 up to their linear layers, BN folded:
  * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)
  * || glob[b] (42); vcat[b] = relu(hw[2] . x[b][cell] + hb[2]) (35) || glob[b].
  * x NHWC [batch][5][7][128] (16-byte aligned), hw [3][128], hb [3]. */
 int hz_heads(const float *x, const float *hw, const float *hb, const float *glob, float *pcat, float *vcat,
-             int32_t batch, void *stream);
+             int32_t batch, const int32_t *live, void *stream);
 
 /* ---- build info ---------------------------------------------------------- */
 const char *hz_version(void);

@@ -29,7 +29,7 @@ class MT(ctypes.Structure):
 class MctsCfg(ctypes.Structure):
     _fields_ = [("sims", ctypes.c_int32), ("cpuct", ctypes.c_float), ("eps", ctypes.c_double),
                 ("testing", ctypes.c_int32), ("tau0", ctypes.c_int32), ("ply", ctypes.c_int32),
-                ("u", ctypes.c_double), ("exact_keys", ctypes.c_int32)]
+                ("u", ctypes.c_double), ("exact_keys", ctypes.c_int32), ("negate_value", ctypes.c_int32)]
 
 
 def build():
@@ -171,9 +171,10 @@ def play_rule_games(n, seed_base, nthreads=0, episode=0):
 
 
 def mcts_search(st, m, sims, cpuct, eps=0.25, testing=True, tau0=15, ply=0, u=0.0, noise=None,
-                exact_keys=False):
+                exact_keys=False, negate_value=False):
     st = np.ascontiguousarray(st, np.int16)
-    cfg = MctsCfg(sims, cpuct, eps, int(bool(testing)), tau0, ply, u, int(bool(exact_keys)))
+    cfg = MctsCfg(sims, cpuct, eps, int(bool(testing)), tau0, ply, u, int(bool(exact_keys)),
+                  int(bool(negate_value)))
     nz = np.zeros(143, np.float64) if noise is None else np.ascontiguousarray(noise, np.float64)
     visits = np.zeros(143, np.int32)
     nn = ctypes.c_int32(0)

@@ -752,6 +752,7 @@ int or_mcts_search(const int16_t *root_ref, or_mt *m, const or_mcts_cfg *cfg, co
     int leaf_player = ls->player;
     if (!st_game_over(ls)) {
       stub_eval_state(ls, pol, &value);
+      if (cfg->negate_value) value = -value;
       if (node == 0 && !cfg->testing) {                    /* MCTS.py:308-327 */
         int L = legal_of(ls, mask);
         float one_m_eps = (float)(1.0 - cfg->eps);

@@ -68,6 +68,7 @@ typedef struct {
   int32_t ply;
   double  u;            /* uniform for tau=1 sampling */
   int32_t exact_keys;   /* 0: key nodes like hash(state) (reference); 1: exact canonical */
+  int32_t negate_value; /* 1: the stub's value negated (a second, different evaluator) */
 } or_mcts_cfg;
 
 int or_mcts_search(const int16_t *root, or_mt *m, const or_mcts_cfg *cfg, const double *noise,

@@ -1,0 +1,44 @@
+"""World-N rehearsal of the training loop (hzamd.trainer.Trainer, BASELINE
+config 5) for tests/test_multirank_gpu.py: launched by torch.distributed.run
+with gloo, every rank on cuda:0 (a one-GPU box).  Each rank writes what it
+ended with: model and best-model weights, replay buffer, history."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "harmonies-alphazero_amd"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main(out, folder):
+    from hzamd.manager import ModelManager
+    from hzamd.trainer import Trainer
+    from test_manager_cpu import MODEL_CFG
+    from test_trainer_gpu import EVAL, MCTS, TRAIN
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    torch.cuda.set_device(0)
+    torch.manual_seed(100 + rank)  # ranks start from different weights: the broadcast must fix that
+    cfg = {"num_iterations": 2, "num_games_per_iter": 6, "epochs_per_iter": 1, "replay_buffer_size": 1000,
+           "checkpoint_folder": os.path.join(folder, "ck"), "replay_buffer_folder": os.path.join(folder, "buf"),
+           "replay_buffer_filename": "rb.pkl", "eval_frequency": 2, "eval_episodes": 5,
+           "eval_win_rate_threshold": 0.0, "best_model_filename": "best.pth.tar"}
+    mm = ModelManager(MODEL_CFG, TRAIN)
+    tr = Trainer(mm, MCTS, cfg, TRAIN, eval_mcts_config=EVAL, seed_base=7, log=lambda *_: None)
+    hist = tr.run_training_loop()
+    flat = lambda m: torch.cat([t.detach().reshape(-1).double().cpu() for t in m.state_dict().values()])  # noqa
+    torch.save({"model": flat(tr.model_manager.model), "best": flat(tr.best_model_manager.model),
+                "buffer": tr.replay_buffer.records().cpu(),
+                "evals": [h["evaluation"] for h in hist], "examples": [h["self_play"]["examples"] for h in hist],
+                "world": dist.get_world_size()}, f"{out}.rank{rank}.pt")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -26,7 +26,8 @@ def oracle_game(seed, a_is_p0, agent_a, agent_b):
         if kind == "greedy":
             a = oracle.greedy_move(s, m)
         else:
-            a = oracle.mcts_search(s, m, SIMS, 2.0, eps=0.0, testing=True, tau0=0, ply=ply)[0]
+            a = oracle.mcts_search(s, m, SIMS, 2.0, eps=0.0, testing=True, tau0=0, ply=ply,
+                                   negate_value=kind == "mcts_neg")[0]
         s = oracle.step(s, a, m)[1]
         ply += 1
     return s
@@ -55,7 +56,24 @@ def test_mcts_vs_greedy_tournament():
     assert s["wins"] + s["losses"] + s["draws"] == 16
 
 
+def neg_stub_evaluator(board, glob):
+    p, v = stub_evaluator(board, glob)
+    return p, -v
+
+
 def test_mcts_vs_mcts_routed_batch():
     a = MctsAgent(stub_evaluator, {"num_simulations": SIMS})
     b = MctsAgent(stub_evaluator, {"num_simulations": SIMS})
     check(a, b, ("mcts", "mcts"), 16, 500)
+
+
+def test_mcts_vs_mcts_routed_batch_two_evaluators():
+    """The shared search routes each gathered leaf row to its board's agent
+    by board id: two different evaluators (the stub and its negated value),
+    games ending at different plies (the gathered batch shrinks and shifts),
+    every game replayed by the oracle with each agent's own evaluator."""
+    a = MctsAgent(stub_evaluator, {"num_simulations": SIMS})
+    b = MctsAgent(neg_stub_evaluator, {"num_simulations": SIMS})
+    out = check(a, b, ("mcts", "mcts_neg"), 24, 600)
+    s = summarize(out)
+    assert s["wins"] + s["losses"] + s["draws"] == 24

@@ -1,17 +1,21 @@
 """bench.py's N > 1 path (barriers, max-over-ranks time, summed counts, one
 JSON line from rank 0) rehearsed with two ranks sharing this box's GPU over
 gloo (HZ_BENCH_REHEARSAL=1); the driver's real run uses one GPU per rank and
-RCCL.  Also the default single-rank contract fields."""
+RCCL.  Also the default single-rank contract fields, the selfplay sub-object
+and the config-4 exchange."""
 import json
 import os
 import subprocess
 import sys
 
 import pytest
+import torch
 
 from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
+
+SMALL_SP = ["--sp-boards", "256", "--sp-sims", "16", "--sp-warmup", "1", "--sp-moves", "2"]
 
 
 def _last_json(out):
@@ -20,30 +24,82 @@ def _last_json(out):
     return json.loads(lines[-1])
 
 
-def test_bench_two_ranks_rehearsal():
+def _torchrun(args, port, timeout=600):
     env = dict(os.environ, HZ_BENCH_REHEARSAL="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "4", "--warmup", "2", "--no-off-compare"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2"] + args
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
+    return r
+
+
+def _single(args, timeout=600):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r
+
+
+def test_bench_two_ranks_rehearsal():
+    r = _torchrun(["--steps", "2", "--warmup", "1", "--launches-per-step", "8", "--no-off-compare"] + SMALL_SP,
+                  29517)
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
     assert d["config"]["parallelism"] == "shard2"
     assert d["cpu_baseline"] is None
+    sp = d["selfplay"]
+    assert sp["n_gpus"] == 2 and sp["sims_per_s"] > 0
+    x = sp["exchange"]
+    # two ranks x 256 boards x 2 timed moves of records, all-gathered
+    assert x["records"] == 2 * 256 * 2 and x["bytes_per_rank_received"] == x["records"] * 336
 
 
 def test_bench_single_rank_contract():
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2", "--cpu-seconds", "1"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
+    r = _single(["--steps", "2", "--warmup", "1", "--launches-per-step", "16", "--cpu-seconds", "1",
+                 "--sp-cpu-seconds", "1"] + SMALL_SP)
     d = _last_json(r.stdout)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "selfplay"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2
-    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["games_per_step"] == 16 * 4096
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "issue_bound"):
         assert k in d["roofline"], k
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in d["cpu_baseline"], k
-    assert d["parity"].endswith(")") and "==" in d["parity"]
+    assert "4096/4096 boards bit-exact" in d["parity"]
+    sp = d["selfplay"]
+    for k in ("sims_per_s", "games_per_s", "nn_roofline", "tree_ms_per_move", "cpu_baseline", "exchange"):
+        assert k in sp, k
+    assert sp["exchange"] is None
+    assert sp["sims"] == 256 * 16 * 2 and 0 < sp["nn_rows_evaluated"] <= sp["sims"]
+    assert 0 < sp["nn_roofline"]["frac"] < 1
+    for k in ("value", "unit", "cores", "kind", "sample", "nn_cpu_ms_per_eval"):
+        assert k in sp["cpu_baseline"], k
+
+
+CFG4 = ["--config", "4", "--boards", "48", "--sims", "6", "--iterations", "2", "--warmup", "2"]
+
+
+def test_config4_exchange_two_ranks_equals_world1(tmp_path):
+    """Config 4 rehearsed at world 2 (gloo, both ranks on this GPU): every
+    rank's replay buffer holds the same records, in rank order; each rank's
+    own records equal a world-1 run over the same global boards bit for bit
+    (results do not depend on the GPU count); the example count is the sum of
+    the ranks' plies."""
+    r = _torchrun(CFG4 + ["--records-out", str(tmp_path / "w2")], 29519)
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["unit"] == "games/s" and d["exchange"]["records"] > 0
+    w2 = [torch.load(tmp_path / f"w2.rank{k}.pt", weights_only=True) for k in (0, 1)]
+    assert torch.equal(w2[0]["buffer"], w2[1]["buffer"])
+    solo = []
+    for k in (0, 1):
+        _single(CFG4 + ["--seed-base", str(48 * k), "--records-out", str(tmp_path / f"w1_{k}")])
+        solo.append(torch.load(tmp_path / f"w1_{k}.rank0.pt", weights_only=True))
+        assert torch.equal(w2[k]["own"], solo[k]["own"]), k
+    # two iterations: per iteration rank 0's records then rank 1's
+    own = [torch.split(w2[k]["own"], w2[k]["own_counts"].tolist()) for k in (0, 1)]
+    want = torch.cat([torch.cat((own[0][i], own[1][i])) for i in range(2)])
+    assert torch.equal(w2[0]["buffer"], want)
+    assert d["exchange"]["records"] == want.shape[0] == d["examples_per_iteration"] * 2

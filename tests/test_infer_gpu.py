@@ -34,6 +34,52 @@ def test_folded_gpu_matches_cpu_reference():
     assert (v.cpu() - v0.reshape(-1)).abs().max().item() <= 2e-3
 
 
+def test_folded_gpu_matches_fp64_reference_at_leaf_batch():
+    """The whole fused forward at the config-3 leaf batch (4096 encoder-like
+    boards), random BatchNorm statistics, against the unfolded network run in
+    float64 on the CPU: logits and values within 1e-4 (fp32 rounding of ~1,200-
+    term sums; the fp32 CPU network itself is checked to the same bound)."""
+    g = torch.Generator().manual_seed(11)
+    torch.manual_seed(1)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    n = 4096
+    board = (torch.rand(n, 38, 5, 7, generator=g) > 0.8).float()
+    glob = torch.rand(n, 42, generator=g)
+    with torch.no_grad():
+        l64, v64 = net.double()(board.double(), glob.double())
+        net.float()
+        l32, v32 = net(board, glob)
+    assert (l32.double() - l64).abs().max().item() <= 1e-4
+    fnet = FoldedNet(net.to("cuda"))
+    l1, v1 = fnet(board.cuda(), glob.cuda())
+    dl = (l1.cpu().double() - l64).abs().max().item()
+    dv = (v1.cpu().double() - v64).abs().max().item()
+    assert dl <= 1e-4 and dv <= 1e-4, (dl, dv)
+
+
+def test_folded_live_rows_equal_full_batch():
+    """With a device live-row count k, the HIP kernels compute rows [0, k)
+    exactly as in the full batch (row results do not depend on the batch)."""
+    g = torch.Generator().manual_seed(3)
+    torch.manual_seed(2)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    n = 1000
+    board = (torch.rand(n, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    glob = torch.rand(n, 42, generator=g).cuda()
+    fnet = FoldedNet(net.to("cuda"))
+    l0, v0 = fnet(board, glob)
+    pred = BatchedPredictor(net)
+    p0, pv0 = pred(board, glob)
+    for k in (0, 1, 7, 8, 9, 333, 1000):
+        live = torch.tensor([k], dtype=torch.int32, device="cuda")
+        l1, v1 = fnet(board, glob, live=live)
+        assert torch.equal(l1[:k], l0[:k]) and torch.equal(v1[:k], v0[:k]), k
+        p1, pv1 = pred(board, glob, None, live)
+        assert torch.equal(p1[:k], p0[:k]) and torch.equal(pv1[:k], pv0[:k]), k
+
+
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("batch", [1, 3, 4096])
 def test_bias_act_equals_torch_passes(batch, res):

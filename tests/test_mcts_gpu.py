@@ -121,34 +121,62 @@ def test_mcts_exact_keys_mode():
         assert (visits[b] == ov).all() and (counts[b, 0], counts[b, 1]) == (nn, ne), b
 
 
-def test_mcts_compacted_leaf_batch_matches_full_batch():
-    """Leaf batches compacted to the active boards (rounded up to the bucket,
-    padded with repeats) give every board the same search as the full batch:
-    identical visit counts and node/edge counts, stub evaluator, 30 % of the
-    boards inactive (including a partial bucket)."""
+def test_mcts_gathered_leaf_batch_matches_full_batch():
+    """Leaf batches gathered on the device (active boards whose leaf is not
+    terminal, MCTS.py:297-341) give every board the same search as the
+    one-row-per-board batch: identical visit counts and node/edge counts with
+    the stub evaluator, whether the evaluator takes the host-sliced batch or
+    the device row count; and fewer rows reach the evaluator.  30 % of the
+    boards inactive, positions late in the game so that terminal leaves occur."""
     from hzamd.env import BatchedEnv
     from hzamd.mcts import BatchedMCTS, stub_evaluator
     n, base, sims, cpuct = 700, 900, 16, 1.5
     g = torch.Generator().manual_seed(7)
     active = (torch.rand(n, generator=g) > 0.3).to(DEV)
+    plies = 40 + torch.arange(n, device=DEV) % 24
+
+    class DeviceRows:
+        device_rows = True
+
+        def __init__(self):
+            self.calls = []
+
+        def __call__(self, board, glob, rows, count):
+            k = int(count.item())
+            self.calls.append(k)
+            assert bool((rows[:k].diff() > 0).all())       # board order
+            pol = torch.full((n, 143), float("nan"), device=DEV)
+            val = torch.full((n,), float("nan"), device=DEV)
+            p, v = stub_evaluator(board[:k], glob[:k])
+            pol[:k], val[:k] = p, v
+            return pol, val
+
     out = []
-    for compact in (False, True):
+    for mode in ("full", "host", "device"):
         env = BatchedEnv(n, seed_base=base, device=DEV)
         env.reset()
-        for _ in range(9):
+        for p in range(64):
             mask, count = env.legal_mask()
-            env.step(env.rule_actions(mask, count))
+            act = env.rule_actions(mask, count)
+            env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+        act_b = active & ~env.done()
         mcts = BatchedMCTS(env, sims)
         calls = []
 
         def ev(board, glob):
             calls.append(board.shape[0])
             return stub_evaluator(board, glob)
-        v = mcts.search(ev, cpuct, active=active, compact=compact).clone()
-        out.append((v.cpu(), mcts.stats().clone().cpu(), calls))
-    (v0, c0, calls0), (v1, c1, calls1) = out
-    assert torch.equal(v0, v1)
-    assert torch.equal(c0[:, :2], c1[:, :2])
-    k = int(active.sum())
-    assert calls0 == [n] * sims and calls1 == [min(n, -(-k // 256) * 256)] * sims
-    assert bool((v1[~active.cpu()] == 0).all())
+        dr = DeviceRows()
+        v = mcts.search(dr if mode == "device" else ev, cpuct, active=act_b, gather=mode != "full").clone()
+        out.append((v.cpu(), mcts.stats().clone().cpu(), dr.calls if mode == "device" else calls,
+                    int(mcts.eval_rows.item())))
+        mcts.close()
+        env.close()
+    (v0, c0, calls0, r0), (v1, c1, calls1, r1), (v2, c2, calls2, r2) = out
+    assert torch.equal(v0, v1) and torch.equal(v0, v2)
+    assert torch.equal(c0[:, :2], c1[:, :2]) and torch.equal(c0[:, :2], c2[:, :2])
+    assert calls0 == [n] * sims and r0 == n * sims
+    assert sum(calls1) == r1 == r2 == sum(calls2)
+    k = int(act_b.sum())
+    assert max(calls1) <= k and r1 < k * sims        # terminal leaves were skipped
+    assert bool((v1[~act_b.cpu()] == 0).all())

@@ -15,11 +15,15 @@ DEV = "cuda:0"
 
 
 def replay(rec, sp, n, base, sims, cpuct, testing, tau0):
+    """Replays every board's game with the oracle; returns the expected z of
+    every record in SelfPlay.compact's order (trainer.py:517-527: the final
+    outcome from the recorded player's perspective, 0 for a draw)."""
     states = rec["states"].cpu().numpy()
     visits = rec["visits"].cpu().numpy()
     valid = rec["valid"].cpu().numpy()
     log = sp.noise_log
     final = rec["final"].cpu().numpy()
+    z = np.zeros(valid.shape, np.float32)
     for b in range(n):
         m = oracle.mt_seed(base + b)
         s = oracle.reset(m)
@@ -37,6 +41,12 @@ def replay(rec, sp, n, base, sims, cpuct, testing, tau0):
             ply += 1
         assert (unpack_ref(final[:, b]) == s).all(), b
         assert not valid[ply:, b].any()
+        w = int(s[75])                                    # winner: 0 / 1, negative = draw
+        outcome = 1.0 if w == 0 else -1.0 if w == 1 else 0.0
+        for p in range(ply):
+            player = int(unpack_ref(states[p, :, b])[72])
+            z[p, b] = outcome if player == 0 else -outcome
+    return z[valid]
 
 
 @pytest.mark.parametrize("testing", [True, False])
@@ -48,9 +58,11 @@ def test_selfplay_matches_oracle_replay(testing):
     sp = SelfPlay(n, stub_evaluator, cfg, seed_base=base, device=DEV)
     sp.keep_noise = True
     rec = sp.play()
-    replay(rec, sp, n, base, sims, cpuct, testing, 15)
+    z_want = replay(rec, sp, n, base, sims, cpuct, testing, 15)
     comp = sp.compact(rec)
     assert comp["states"].shape[0] == int(rec["valid"].sum())
+    assert np.array_equal(comp["z"].cpu().numpy(), z_want)
+    assert (z_want != 0).any()
     assert torch.allclose(comp["pi"].sum(1), torch.ones(comp["pi"].shape[0], device=comp["pi"].device))
     ex = sp.examples(comp)
     assert ex[0][0].shape == (38, 5, 7) and ex[0][1].shape == (42,) and ex[0][2].shape == (143,)

@@ -13,7 +13,7 @@ from hzamd.infer import pack_conv3x3  # noqa: E402
 
 lib = ctypes.CDLL(os.path.join(HERE, "libnet_diag.so"))
 vp = ctypes.c_void_p
-lib.hz_conv3x3_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp]
+lib.hz_conv3x3_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
 lib.hz_net_diag_stamps.argtypes = [vp]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 cl = torch.channels_last
@@ -25,7 +25,7 @@ r = torch.randn(B, 128, 5, 7, device="cuda", generator=g).contiguous(memory_form
 out = torch.empty_like(x)
 for _ in range(200):  # ~70 ms of back-to-back launches so the clock settles
     assert lib.hz_conv3x3_bias_act(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr(), out.data_ptr(), B,
-                                   torch.cuda.current_stream().cuda_stream) == 0
+                                   None, torch.cuda.current_stream().cuda_stream) == 0
 st = np.zeros((1024, 2, 10), dtype=np.uint64)
 assert lib.hz_net_diag_stamps(st.ctypes.data) == 0
 nwg = (B + 7) // 8
