@@ -287,6 +287,250 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// ---- the same conv on the bf16 MFMA, fp32-exact products (bf16x6) ---------
+//
+// v_mfma_f32_16x16x32_bf16 runs 16x the MACs per cycle of the f32 form
+// (MI355X_MICROARCH.md: 16 vs 32 cycles for 8192 vs 1024 MACs).  Every fp32
+// operand is split exactly into three bf16 pieces, a = a_h + a_m + a_l
+// (round-to-nearest at each step: |a_m| <= 2^-8 |a|, |a_l| <= 2^-16 |a|, and
+// the three pieces sum to a with no error), and
+//     a * b = sum over the pairs (i, j) with i + j <= 2 of a_i * b_j
+// up to the dropped pairs (m,l), (l,m), (l,l): |error| <= ~2^-23 |a b|, the
+// size of one fp32 rounding.  Each bf16 x bf16 product is exact in the MFMA's
+// fp32 accumulation, so the conv keeps fp32 accuracy (tests compare both
+// kernels against a float64 conv) with 6 bf16 MFMAs per product block:
+// 16/6 = 2.7x the f32 MFMA rate.
+//
+// Tiling as k_conv3x3_w8 (8 states = 280 rows per 512-thread workgroup;
+// wave = row half x 32 output channels: 9 x 2 accumulator tiles of 16x16).
+// The input is staged 32 channels at a time (one K-step of 32 per tap),
+// split into its three bf16 planes on the way into LDS (the split costs
+// VALU once per staged element, not per use); a cell is 3 x 64 B + 32 B of
+// padding (224 B: ds_read_b128 conflict-free for the A fragment's lane
+// groups), the grid has no halo: a neighbour outside the 5x7 board reads one
+// shared zero cell.  Weights are prepacked as bf16 planes
+// [tap][ci/32][plane][co][32].  Epilogue as k_conv3x3_w8 (fp32 in HBM).
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+constexpr int kX6Cell = 224;                         // bytes per staged cell
+constexpr int kX6Buf = (kCS * 35 + 1) * kX6Cell;      // one chunk of 8 states + the zero cell
+constexpr int kX6Stage = (kRows * 8 + 511) / 512;     // float4 loads per thread per chunk (5)
+
+__device__ __forceinline__ uint32_t bf16_bits(float v) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)v);
+}
+__device__ __forceinline__ float bf16_value(uint32_t b) { return __uint_as_float(b << 16); }
+
+// the three bf16 planes of four consecutive channels: 8 B per plane
+__device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 &l) {
+  uint32_t hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    hb[j] = bf16_bits(v[j]);
+    const float r1 = v[j] - bf16_value(hb[j]);
+    mb[j] = bf16_bits(r1);
+    lb[j] = bf16_bits(r1 - bf16_value(mb[j]));
+  }
+  h = make_uint2(hb[0] | hb[1] << 16, hb[2] | hb[3] << 16);
+  m = make_uint2(mb[0] | mb[1] << 16, mb[2] | mb[3] << 16);
+  l = make_uint2(lb[0] | lb[1] << 16, lb[2] | lb[3] << 16);
+}
+
+__global__ void __launch_bounds__(512, 1)
+    k_conv3x3_x6(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
+                 const float *__restrict__ res, float *__restrict__ out, int32_t batch,
+                 const int32_t *__restrict__ live) {
+  extern __shared__ float4 lds4[];
+  char *lds = (char *)lds4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
+  const int s0 = blockIdx.x * kCS;
+  if (live) batch = *live < batch ? *live : batch;
+  if (s0 >= batch) return;
+  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+  constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero cell in each buffer
+
+  if (t < 2 * kX6Cell / 16) {  // both buffers' zero cells
+    const int b = t / (kX6Cell / 16), k = t - b * (kX6Cell / 16);
+    *(float4 *)(lds + b * kX6Buf + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..)
+  f32x4 stg[kX6Stage];
+  int gsrc[kX6Stage], ldst[kX6Stage];
+#pragma unroll
+  for (int it = 0; it < kX6Stage; it++) {
+    int f = it * 512 + t;
+    f = f < kRows * 8 ? f : kRows * 8 - 1;
+    const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
+    gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
+    ldst[it] = sc * kX6Cell + 8 * part;
+  }
+#define HZ_X6_LOAD(q)                                                                     \
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
+  _Pragma("unroll") for (int it = 0; it < kX6Stage; it++)                                 \
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q)));
+  // the wait names the staged registers, so the split's arithmetic (which,
+  // unlike an LDS store, could move above a plain asm statement) waits too
+  static_assert(kX6Stage == 5, "HZ_X6_STORE ties five staging registers");
+#define HZ_X6_STORE(buf)                                                                  \
+  asm volatile("s_waitcnt vmcnt(0)"                                                       \
+               : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4])      \
+               :                                                                          \
+               : "memory");                                                               \
+  _Pragma("unroll") for (int it = 0; it < kX6Stage; it++) {                               \
+    uint2 h_, m_, l_;                                                                     \
+    split4(stg[it], h_, m_, l_);                                                          \
+    char *d_ = lds + (buf) * kX6Buf + ldst[it];                                           \
+    *(uint2 *)d_ = h_;                                                                    \
+    *(uint2 *)(d_ + 64) = m_;                                                             \
+    *(uint2 *)(d_ + 128) = l_;                                                            \
+  }
+
+  // A fragment of row block rb, tap: the lane's row r = (rh*9 + rb)*16 + (lane & 15)
+  // (clamped), its cell (h, w) of state s; neighbour (h + dh - 1, w + dw - 1)
+  // or the zero cell.  valid[rb] bit tap = the neighbour is on the board.
+  int cbase[kRB];
+  uint32_t valid[kRB];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    int r = (rh * kRB + rb) * 16 + (lane & 15);
+    r = r < kRows ? r : kRows - 1;
+    const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
+    cbase[rb] = r * kX6Cell + 16 * kg;
+    uint32_t v = 0;
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+      const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
+      v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
+    }
+    valid[rb] = v;
+  }
+  auto aoff = [&](int rb, int tap) -> int {
+    const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
+    return (valid[rb] >> tap) & 1 ? cbase[rb] + d : kZero + 16 * kg;
+  };
+
+  f32x4 acc[kRB][2];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
+
+  const int co0 = 32 * (w & 3) + (lane & 15);
+  // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
+  // wp[(((tap * 4 + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
+  const bf16x8 *wl = wp + co0 * 4 + kg;
+  auto bload = [&](int L, int p, int cb) -> bf16x8 {
+    const int q2 = L / 9, t2 = L - 9 * q2;
+    return wl[((t2 * 4 + q2) * 3 + p) * 512 + 64 * cb];
+  };
+
+  HZ_X6_LOAD(0)
+  HZ_X6_STORE(0)
+  __syncthreads();
+
+  bf16x8 b[3][2], bn[3][2];  // this K-step's B fragments, the next step's (loaded a step ahead)
+#pragma unroll
+  for (int p = 0; p < 3; p++) {
+    b[p][0] = bload(0, p, 0);
+    b[p][1] = bload(0, p, 1);
+  }
+
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const char *lb = lds + (q & 1) * kX6Buf;
+    if (q < 3) { HZ_X6_LOAD(q + 1) }
+    for (int tap = 0; tap < 9; tap++) {
+      const int L = q * 9 + tap, Ln = L + 1 < 36 ? L + 1 : 35;
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        bn[p][0] = bload(Ln, p, 0);
+        bn[p][1] = bload(Ln, p, 1);
+      }
+      // plane a of A against the planes b with a + b <= 2
+#pragma unroll
+      for (int pa = 0; pa < 3; pa++) {
+        bf16x8 a[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
+#pragma unroll
+        for (int pb = 0; pb < 3 - pa; pb++) {
+          const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
+#pragma unroll
+          for (int rb = 0; rb < kRB; rb++) {
+            acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
+            acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        b[p][0] = bn[p][0];
+        b[p][1] = bn[p][1];
+      }
+    }
+    if (q < 3) {
+      HZ_X6_STORE((q + 1) & 1)
+      __syncthreads();
+    }
+  }
+
+  const float bc0 = bias[co0], bc1 = bias[co0 + 16];
+  float *ob = out + (size_t)s0 * 35 * 128 + co0;
+  const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co0 : nullptr;
+  const int nrow = ns * 35;
+  float rv[kRB][2][4];
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const bool ok = rbase + j < nrow;
+      rv[rb][0][j] = rsb && ok ? rsb[(rbase + j) * 128] : 0.f;
+      rv[rb][1][j] = rsb && ok ? rsb[(rbase + j) * 128 + 16] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < kRB; rb++) {
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (rbase + j < nrow) {
+        float v0 = acc[rb][0][j] + bc0, v1 = acc[rb][1][j] + bc1;
+        if (rsb) {
+          v0 = v0 + rv[rb][0][j];
+          v1 = v1 + rv[rb][1][j];
+        }
+        ob[(rbase + j) * 128] = v0 > 0.f ? v0 : 0.f;
+        ob[(rbase + j) * 128 + 16] = v1 > 0.f ? v1 : 0.f;
+      }
+    }
+  }
+}
+#undef HZ_X6_LOAD
+#undef HZ_X6_STORE
+
+}  // namespace
+
+extern "C" int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res,
+                                      float *out, int32_t batch, const int32_t *live, void *stream) {
+  if (!x || !wpack6 || !bias || !out || batch < 0) return -1;
+  if (((uintptr_t)x | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)res) & 15) return -1;
+  if (batch == 0) return 0;
+  static std::atomic<uint64_t> init_mask{0};
+  const size_t lds = 2 * (size_t)kX6Buf;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL(k_conv3x3_x6, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, x,
+                     (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 #ifdef HZ_NET_DIAG
 extern "C" int hz_net_diag_stamps(uint64_t *host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;

@@ -32,6 +32,26 @@ def pack_conv3x3(w):
     return w.permute(2, 3, 1, 0).reshape(9, ci // 16, 16, co).permute(0, 1, 3, 2).contiguous()
 
 
+def split3_bf16(w):
+    """fp32 -> its three bf16 pieces (h, m, l) with h + m + l == w exactly
+    (round-to-nearest at each step), stacked on a new leading dim."""
+    w = w.float()
+    h = w.to(torch.bfloat16)
+    r = w - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    return torch.stack((h, m, lo))
+
+
+def pack_conv3x3_x6(w):
+    """[co][ci][3][3] fp32 -> bf16 planes [kh*3+kw][ci/32][plane][co][ci%32],
+    the layout hz_conv3x3_x6_bias_act reads (one 16-byte B fragment per lane)."""
+    co, ci = w.shape[0], w.shape[1]
+    p = split3_bf16(w)                                   # [3][co][ci][3][3]
+    p = p.permute(3, 4, 2, 0, 1).reshape(9, ci // 32, 32, 3, co)  # [tap][q][k][plane][co]
+    return p.permute(0, 1, 3, 4, 2).contiguous()         # [tap][q][plane][co][k]
+
+
 def _live_ptr(live):
     """Device int32 scalar bounding the rows the HIP kernels compute (None = all)."""
     if live is None:
@@ -63,6 +83,22 @@ def pack_stem(w):
     w48 = torch.zeros(w.shape[0], 48, 3, 3, dtype=w.dtype, device=w.device)
     w48[:, :w.shape[1]] = w
     return pack_conv3x3(w48)
+
+
+def _conv3x3_x6_act(x, wpack6, b, res=None, live=None):
+    """_conv3x3_act on the bf16 MFMA with fp32-exact products (bf16x6 split)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_conv3x3_x6_bias_act needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    if res is not None and (res.shape != x.shape or res.stride() != x.stride()):
+        raise NativeError("hz_conv3x3_x6_bias_act: residual layout differs from the activation")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    rc = lib().hz_conv3x3_x6_bias_act(x.data_ptr(), wpack6.data_ptr(), b.data_ptr(),
+                                      res.data_ptr() if res is not None else None, out.data_ptr(), x.shape[0],
+                                      _live_ptr(live), torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_conv3x3_x6_bias_act failed ({rc})")
+    return out
 
 
 def _stem_act(board, wpack, b, live=None):
@@ -127,9 +163,16 @@ class FoldedNet(nn.Module):
     is the HIP kernel (CUDA fp32 activations only; no CPU path).  Tests pass
     a plain-torch restatement to check the folding algebra on the CPU."""
 
-    def __init__(self, net, epilogue=None, native_conv=True):
+    # tower conv kernels: "x6" = bf16 MFMA with fp32-exact products (bf16x6
+    # split, hz_conv3x3_x6_bias_act), "f32" = the f32 MFMA (hz_conv3x3_bias_act)
+    TOWER_MFMA = ("x6", "f32")
+
+    def __init__(self, net, epilogue=None, native_conv=True, tower="x6"):
         super().__init__()
+        if tower not in self.TOWER_MFMA:
+            raise ValueError(f"tower must be one of {self.TOWER_MFMA}")
         self.src = net
+        self.tower = tower
         self.epilogue = epilogue or _bias_act
         self.native_conv = native_conv and epilogue is None
         self.refresh()
@@ -146,7 +189,8 @@ class FoldedNet(nn.Module):
             self.stem_packed = pack_stem(self.stem[0])
         self.packed = None
         if self.native_conv and self.blocks and self.blocks[0][0][0].shape[:2] == (128, 128):
-            self.packed = [(pack_conv3x3(w1), pack_conv3x3(w2)) for (w1, _), (w2, _) in self.blocks]
+            pk = pack_conv3x3_x6 if self.tower == "x6" else pack_conv3x3
+            self.packed = [(pk(w1), pk(w2)) for (w1, _), (w2, _) in self.blocks]
         self.pconv = _fold(n.policy_conv, n.policy_bn)
         self.vconv = _fold(n.value_conv, n.value_bn)
         # snapshots like the folded convs: an optimizer step on the source
@@ -174,9 +218,10 @@ class FoldedNet(nn.Module):
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
         if self.packed is not None:
+            conv = _conv3x3_x6_act if self.tower == "x6" else _conv3x3_act
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
-                y = _conv3x3_act(x, p1, b1, None, live)
-                x = _conv3x3_act(y, p2, b2, x, live)
+                y = conv(x, p1, b1, None, live)
+                x = conv(y, p2, b2, x, live)
         else:
             for (w1, b1), (w2, b2) in self.blocks:
                 y = ep(F.conv2d(x, w1, None, padding=1), b1)

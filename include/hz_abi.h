@@ -214,6 +214,14 @@ int hz_bias_act(float *x, const float *bias, const float *res, int64_t rows, int
 int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, const float *res, float *out,
                         int32_t batch, const int32_t *live, void *stream);
 
+/* hz_conv3x3_bias_act on the bf16 MFMA (v_mfma_f32_16x16x32_bf16) with
+ * fp32-exact products: x and w are split exactly into three bf16 pieces each
+ * and the six piece products of order <= 2 are accumulated in fp32 (the
+ * dropped ones are below one fp32 rounding).  wpack6 = bf16 planes
+ * [kh*3+kw][ci/32][plane h,m,l][co][ci%32] (hzamd/infer.py:pack_conv3x3_x6). */
+int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
+                           int32_t batch, const int32_t *live, void *stream);
+
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the
  * encoder writes it, out NHWC [batch][5][7][128], wpack = w with the input

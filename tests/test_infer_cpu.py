@@ -61,3 +61,24 @@ def test_refresh_tracks_weight_updates():
     glob = torch.rand(4, 42)
     with torch.no_grad():
         assert (f(board, glob)[0] - net(board, glob)[0]).abs().max().item() <= 1e-4
+
+
+def test_split3_bf16_is_exact():
+    """The bf16x6 conv's operand split: h + m + l == w exactly for fp32
+    values of every magnitude the network sees (and the pieces shrink by
+    >= 2^8 each, so the dropped piece products stay below fp32 rounding)."""
+    from hzamd.infer import pack_conv3x3_x6, split3_bf16
+    g = torch.Generator().manual_seed(0)
+    w = torch.cat([torch.randn(100000, generator=g) * s for s in (1e-6, 1e-3, 1.0, 1e3)])
+    h, m, lo = split3_bf16(w)
+    assert torch.equal(h.double() + m.double() + lo.double(), w.double())
+    nz = w != 0
+    assert bool((m.float().abs()[nz] <= w.abs()[nz] * 2.0 ** -8).all())
+    assert bool((lo.float().abs()[nz] <= w.abs()[nz] * 2.0 ** -16).all())
+    wc = torch.randn(128, 128, 3, 3, generator=g)
+    p = pack_conv3x3_x6(wc)
+    assert p.shape == (9, 4, 3, 128, 32) and p.dtype == torch.bfloat16
+    # tap (kh, kw) = (1, 2), ci 70 = chunk 2 lane 6, co 5, plane h
+    assert p[5, 2, 0, 5, 6] == wc[5, 70, 1, 2].to(torch.bfloat16)
+    rec = p.double().sum(2).permute(2, 1, 3, 0).reshape(128, 128, 3, 3)   # [co][ci][kh][kw]
+    assert torch.equal(rec, wc.double())

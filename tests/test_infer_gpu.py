@@ -114,14 +114,23 @@ def _conv_ref(x, w, b, res):
     return y.relu()
 
 
+def _tower_conv(kind):
+    from hzamd.infer import _conv3x3_act, _conv3x3_x6_act, pack_conv3x3, pack_conv3x3_x6
+    if kind == "f32":
+        return _conv3x3_act, pack_conv3x3
+    return _conv3x3_x6_act, pack_conv3x3_x6
+
+
+@pytest.mark.parametrize("kind", ["f32", "x6"])
 @pytest.mark.parametrize("batch", [1, 13, 64])
 @pytest.mark.parametrize("res", [False, True])
-def test_conv3x3_exact_on_integer_data(batch, res):
+def test_conv3x3_exact_on_integer_data(batch, res, kind):
     """Small-integer inputs and weights: every product and partial sum is
-    exact in fp32, so hz_conv3x3_bias_act must equal the fp64 conv exactly
-    (catches any operand-layout, tap or channel-order mistake; asymmetric
-    weights so a transposed tap or swapped co/ci shows)."""
-    from hzamd.infer import _conv3x3_act, pack_conv3x3
+    exact in fp32, so hz_conv3x3_bias_act (f32 MFMA) and
+    hz_conv3x3_x6_bias_act (bf16 MFMA, split operands) must equal the fp64
+    conv exactly (catches any operand-layout, tap or channel-order mistake;
+    asymmetric weights so a transposed tap or swapped co/ci shows)."""
+    _conv3x3_act, pack_conv3x3 = _tower_conv(kind)
     g = torch.Generator().manual_seed(batch * 2 + res)
     x = torch.randint(-3, 4, (batch, 128, 5, 7), generator=g).float()
     w = torch.randint(-2, 3, (128, 128, 3, 3), generator=g).float()
@@ -134,11 +143,12 @@ def test_conv3x3_exact_on_integer_data(batch, res):
     assert torch.equal(got.cpu(), want)
 
 
+@pytest.mark.parametrize("kind", ["f32", "x6"])
 @pytest.mark.parametrize("batch", [8, 4096])
-def test_conv3x3_matches_miopen_float(batch):
+def test_conv3x3_matches_miopen_float(batch, kind):
     """Real-valued data at the leaf-eval batch: within fp32 rounding of
     MIOpen's conv + the torch epilogue (|diff| <= 1e-4 on O(1) outputs)."""
-    from hzamd.infer import _conv3x3_act, pack_conv3x3
+    _conv3x3_act, pack_conv3x3 = _tower_conv(kind)
     g = torch.Generator(device="cuda").manual_seed(batch)
     cl = torch.channels_last
     x = torch.randn(batch, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
@@ -148,6 +158,33 @@ def test_conv3x3_matches_miopen_float(batch):
     want = (torch.nn.functional.conv2d(x, w, b, padding=1) + r).relu()
     got = _conv3x3_act(x, pack_conv3x3(w), b, r)
     assert (got - want).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("live", [None, 0, 1, 9, 300])
+def test_conv3x3_x6_fp32_accuracy_vs_fp64(live):
+    """Real-valued data (values not representable in bf16): the bf16x6 conv's
+    error against a float64 conv is at the f32 MFMA conv's level (both are
+    fp32 rounding: max |err| <= 2x the f32 kernel's + 1e-7; outputs reach
+    ~10, so both are a few 1e-6); with a live-row bound the rows computed
+    are unchanged."""
+    from hzamd.infer import _conv3x3_act, _conv3x3_x6_act, pack_conv3x3, pack_conv3x3_x6
+    n = 300
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(n, 128, 5, 7, generator=g).relu()
+    w = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+    b = torch.randn(128, generator=g) * 0.1
+    r = torch.randn(n, 128, 5, 7, generator=g)
+    want = _conv_ref(x, w, b, r)
+    cl = torch.channels_last
+    xc, rc = x.cuda().contiguous(memory_format=cl), r.cuda().contiguous(memory_format=cl)
+    e32 = (_conv3x3_act(xc, pack_conv3x3(w).cuda(), b.cuda(), rc).cpu().double() - want).abs().max().item()
+    full = _conv3x3_x6_act(xc, pack_conv3x3_x6(w).cuda(), b.cuda(), rc)
+    e6 = (full.cpu().double() - want).abs().max().item()
+    assert e6 <= 2 * e32 + 1e-7, (e6, e32)
+    if live is not None:
+        lv = torch.tensor([live], dtype=torch.int32, device="cuda")
+        part = _conv3x3_x6_act(xc, pack_conv3x3_x6(w).cuda(), b.cuda(), rc, lv)
+        assert torch.equal(part[:live], full[:live])
 
 
 @pytest.mark.parametrize("batch", [1, 5, 4096])

@@ -1,0 +1,42 @@
+"""Tower conv kernels at the leaf-eval batch: hz_conv3x3_bias_act (f32 MFMA)
+vs hz_conv3x3_x6_bias_act (bf16 MFMA, fp32-exact split products), HIP-event
+timed over back-to-back launches; prints one JSON line.
+Usage (GPU box): python tools/conv_bench.py [batch]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "harmonies-alphazero_amd")]
+
+import torch  # noqa: E402
+
+from hzamd.infer import _conv3x3_act, _conv3x3_x6_act, pack_conv3x3, pack_conv3x3_x6  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+cl = torch.channels_last
+g = torch.Generator(device="cuda").manual_seed(0)
+x = torch.randn(B, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
+w = torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.03
+b = torch.randn(128, device="cuda", generator=g)
+r = torch.randn(B, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=cl)
+flop = 2.0 * B * 35 * 128 * 1152
+out = {"batch": B, "gflop_per_conv": flop / 1e9}
+for name, fn, wp in (("f32", _conv3x3_act, pack_conv3x3(w)), ("x6", _conv3x3_x6_act, pack_conv3x3_x6(w))):
+    for _ in range(20):
+        fn(x, wp, b, r)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 100
+    e0.record()
+    for _ in range(reps):
+        fn(x, wp, b, r)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    out[name] = {"us": us, "tflops": flop / (us * 1e-6) / 1e12}
+k = 256  # float64 reference on the CPU for the first k states
+want = (torch.nn.functional.conv2d(x[:k].double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+        + r[:k].double().cpu()).relu()
+for name, fn, wp in (("f32", _conv3x3_act, pack_conv3x3(w)), ("x6", _conv3x3_x6_act, pack_conv3x3_x6(w))):
+    out[name]["max_abs_err_vs_fp64"] = (fn(x, wp, b, r)[:k].double().cpu() - want).abs().max().item()
+print(json.dumps(out))
