@@ -310,11 +310,23 @@ extern "C" int hz_conv3x3_bias_act(const float *x, const float *wpack, const flo
 // groups), the grid has no halo: a neighbour outside the 5x7 board reads one
 // shared zero cell.  Weights are prepacked as bf16 planes
 // [tap][ci/32][plane][co][32].  Epilogue as k_conv3x3_w8 (fp32 in HBM).
+#ifdef HZ_NET_DIAG
+#define HZ_STAMP(k)                                                                   \
+  if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][k] = __builtin_amdgcn_s_memtime();
+#define HZ_STAMP_RT(k)                                                                \
+  if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define HZ_STAMP(k)
+#define HZ_STAMP_RT(k)
+#endif
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 constexpr int kX6Cell = 224;                         // bytes per staged cell
-constexpr int kX6Buf = (kCS * 35 + 1) * kX6Cell;      // one chunk of 8 states + the zero cell
+constexpr int kBoardC = 38;                           // encoder board channels (stem input)
+constexpr int kX6Zero = 512;                          // bytes of zeros after the cells
+constexpr int kX6Buf = kCS * 35 * kX6Cell + kX6Zero;  // one chunk of 8 states + the zero region
+static_assert(kCS * 35 * kX6Cell % 256 == 0 && kX6Buf % 256 == 0, "zero region and buffers 256-B aligned");
 constexpr int kX6Stage = (kRows * 8 + 511) / 512;     // float4 loads per thread per chunk (5)
 
 __device__ __forceinline__ uint32_t bf16_bits(float v) {
@@ -337,6 +349,10 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
   l = make_uint2(lb[0] | lb[1] << 16, lb[2] | lb[3] << 16);
 }
 
+// NQ chunks of 32 input channels.  Stem: x is the encoder's NCHW board
+// [B][38][5][7] (channels >= 38 stage as zeros; NQ = 2), else an NHWC
+// [B][5][7][128] activation (NQ = 4).
+template <int NQ, bool Stem>
 __global__ void __launch_bounds__(512, 1)
     k_conv3x3_x6(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                  const float *__restrict__ res, float *__restrict__ out, int32_t batch,
@@ -348,10 +364,12 @@ __global__ void __launch_bounds__(512, 1)
   if (live) batch = *live < batch ? *live : batch;
   if (s0 >= batch) return;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
-  constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero cell in each buffer
+  constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero region in each buffer
+  HZ_STAMP(0)
+  HZ_STAMP_RT(8)
 
-  if (t < 2 * kX6Cell / 16) {  // both buffers' zero cells
-    const int b = t / (kX6Cell / 16), k = t - b * (kX6Cell / 16);
+  if (t < 2 * kX6Zero / 16) {  // both buffers' zero regions
+    const int b = t / (kX6Zero / 16), k = t - b * (kX6Zero / 16);
     *(float4 *)(lds + b * kX6Buf + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
@@ -363,13 +381,28 @@ __global__ void __launch_bounds__(512, 1)
     int f = it * 512 + t;
     f = f < kRows * 8 ? f : kRows * 8 - 1;
     const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
-    gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
+    if constexpr (Stem)  // board element (state, channel 4 part, cell); channel offset added per chunk
+      gsrc[it] = (s < ns ? s0 + s : s0 + ns - 1) * (kBoardC * 35) + 4 * part * 35 + cell;
+    else
+      gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
     ldst[it] = sc * kX6Cell + 8 * part;
   }
+  // stem: the four channels 32 q + 4 part + j of a slot, zero past channel 37
+  auto stem_load = [&](int it, int q) -> f32x4 {
+    f32x4 v;
+    const int c0 = 32 * q + 4 * ((it * 512 + t) & 7);
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC ? x[gsrc[it] + (32 * q + j) * 35] : 0.f;
+    return v;
+  };
 #define HZ_X6_LOAD(q)                                                                     \
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
-  _Pragma("unroll") for (int it = 0; it < kX6Stage; it++)                                 \
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q)));
+  if constexpr (Stem) {                                                                   \
+    _Pragma("unroll") for (int it = 0; it < kX6Stage; it++) stg[it] = stem_load(it, q);   \
+  } else {                                                                                \
+    _Pragma("unroll") for (int it = 0; it < kX6Stage; it++)                               \
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q))); \
+  }
   // the wait names the staged registers, so the split's arithmetic (which,
   // unlike an LDS store, could move above a plain asm statement) waits too
   static_assert(kX6Stage == 5, "HZ_X6_STORE ties five staging registers");
@@ -389,7 +422,9 @@ __global__ void __launch_bounds__(512, 1)
 
   // A fragment of row block rb, tap: the lane's row r = (rh*9 + rb)*16 + (lane & 15)
   // (clamped), its cell (h, w) of state s; neighbour (h + dh - 1, w + dw - 1)
-  // or the zero cell.  valid[rb] bit tap = the neighbour is on the board.
+  // or, off the board, the zero region at the same offset mod 256 (so the
+  // lane keeps the LDS banks its row would use).
+  // valid[rb] bit tap = the neighbour is on the board.
   int cbase[kRB];
   uint32_t valid[kRB];
 #pragma unroll
@@ -408,7 +443,8 @@ __global__ void __launch_bounds__(512, 1)
   }
   auto aoff = [&](int rb, int tap) -> int {
     const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
-    return (valid[rb] >> tap) & 1 ? cbase[rb] + d : kZero + 16 * kg;
+    const int a = cbase[rb] + d;
+    return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
   };
 
   f32x4 acc[kRB][2];
@@ -417,16 +453,18 @@ __global__ void __launch_bounds__(512, 1)
 
   const int co0 = 32 * (w & 3) + (lane & 15);
   // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
-  // wp[(((tap * 4 + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
+  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
   const bf16x8 *wl = wp + co0 * 4 + kg;
   auto bload = [&](int L, int p, int cb) -> bf16x8 {
     const int q2 = L / 9, t2 = L - 9 * q2;
-    return wl[((t2 * 4 + q2) * 3 + p) * 512 + 64 * cb];
+    return wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
   };
 
+  HZ_STAMP(1)
   HZ_X6_LOAD(0)
   HZ_X6_STORE(0)
   __syncthreads();
+  HZ_STAMP(2)
 
   bf16x8 b[3][2], bn[3][2];  // this K-step's B fragments, the next step's (loaded a step ahead)
 #pragma unroll
@@ -436,11 +474,11 @@ __global__ void __launch_bounds__(512, 1)
   }
 
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < NQ; q++) {
     const char *lb = lds + (q & 1) * kX6Buf;
-    if (q < 3) { HZ_X6_LOAD(q + 1) }
+    if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
     for (int tap = 0; tap < 9; tap++) {
-      const int L = q * 9 + tap, Ln = L + 1 < 36 ? L + 1 : 35;
+      const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
 #pragma unroll
       for (int p = 0; p < 3; p++) {
         bn[p][0] = bload(Ln, p, 0);
@@ -468,10 +506,11 @@ __global__ void __launch_bounds__(512, 1)
         b[p][1] = bn[p][1];
       }
     }
-    if (q < 3) {
+    if (q < NQ - 1) {
       HZ_X6_STORE((q + 1) & 1)
       __syncthreads();
     }
+    HZ_STAMP(3 + q)
   }
 
   const float bc0 = bias[co0], bc1 = bias[co0 + 16];
@@ -505,30 +544,48 @@ __global__ void __launch_bounds__(512, 1)
       }
     }
   }
+  HZ_STAMP(7)
+  HZ_STAMP_RT(9)
 }
 #undef HZ_X6_LOAD
+#undef HZ_STAMP
+#undef HZ_STAMP_RT
 #undef HZ_X6_STORE
 
 }  // namespace
+
+template <int NQ, bool Stem>
+static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
+                     int32_t batch, const int32_t *live, void *stream) {
+  static std::atomic<uint64_t> init_mask{0};
+  const size_t lds = 2 * (size_t)kX6Buf;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6<NQ, Stem>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL((k_conv3x3_x6<NQ, Stem>), dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream,
+                     x, (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 extern "C" int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res,
                                       float *out, int32_t batch, const int32_t *live, void *stream) {
   if (!x || !wpack6 || !bias || !out || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)res) & 15) return -1;
   if (batch == 0) return 0;
-  static std::atomic<uint64_t> init_mask{0};
-  const size_t lds = 2 * (size_t)kX6Buf;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
-  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3_x6, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
-      return 1;
-    init_mask.fetch_or(1ull << dev, std::memory_order_release);
-  }
-  hipLaunchKernelGGL(k_conv3x3_x6, dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream, x,
-                     (const bf16x8 *)wpack6, bias, res, out, batch, live);
-  return hipGetLastError() == hipSuccess ? 0 : 1;
+  return launch_x6<4, false>(x, wpack6, bias, res, out, batch, live, stream);
+}
+
+extern "C" int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *bias, float *out,
+                                      int32_t batch, const int32_t *live, void *stream) {
+  if (!board || !wpack6 || !bias || !out || batch < 0) return -1;
+  if (((uintptr_t)wpack6 | (uintptr_t)out) & 15) return -1;
+  if (batch == 0) return 0;
+  return launch_x6<2, true>(board, wpack6, bias, nullptr, out, batch, live, stream);
 }
 
 #ifdef HZ_NET_DIAG

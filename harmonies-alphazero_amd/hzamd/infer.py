@@ -101,6 +101,29 @@ def _conv3x3_x6_act(x, wpack6, b, res=None, live=None):
     return out
 
 
+def pack_stem_x6(w):
+    """Stem weights [128][38][3][3] with the input channels zero-padded to 64,
+    packed like pack_conv3x3_x6 (hz_stem3x3_x6_bias_act's layout)."""
+    w64 = torch.zeros(w.shape[0], 64, 3, 3, dtype=w.dtype, device=w.device)
+    w64[:, :w.shape[1]] = w
+    return pack_conv3x3_x6(w64)
+
+
+def _stem_x6_act(board, wpack6, b, live=None):
+    """_stem_act on the bf16 MFMA with fp32-exact products (bf16x6 split)."""
+    if not (board.is_cuda and board.dtype == torch.float32 and board.shape[1:] == (38, 5, 7)):
+        raise NativeError("hz_stem3x3_x6_bias_act needs a CUDA fp32 [B,38,5,7] board")
+    board = board.contiguous()
+    out = torch.empty(board.shape[0], 128, 5, 7, dtype=torch.float32, device=board.device,
+                      memory_format=torch.channels_last)
+    rc = lib().hz_stem3x3_x6_bias_act(board.data_ptr(), wpack6.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                      board.shape[0], _live_ptr(live),
+                                      torch.cuda.current_stream(board.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_stem3x3_x6_bias_act failed ({rc})")
+    return out
+
+
 def _stem_act(board, wpack, b, live=None):
     """relu(conv3x3(board) + b) from the encoder's NCHW board, NHWC out, one HIP launch."""
     if not (board.is_cuda and board.dtype == torch.float32 and board.shape[1:] == (38, 5, 7)):
@@ -163,8 +186,9 @@ class FoldedNet(nn.Module):
     is the HIP kernel (CUDA fp32 activations only; no CPU path).  Tests pass
     a plain-torch restatement to check the folding algebra on the CPU."""
 
-    # tower conv kernels: "x6" = bf16 MFMA with fp32-exact products (bf16x6
-    # split, hz_conv3x3_x6_bias_act), "f32" = the f32 MFMA (hz_conv3x3_bias_act)
+    # stem + tower conv kernels: "x6" = bf16 MFMA with fp32-exact products
+    # (bf16x6 split: hz_stem3x3_x6_bias_act, hz_conv3x3_x6_bias_act), "f32" =
+    # the f32 MFMA (hz_stem3x3_bias_act, hz_conv3x3_bias_act)
     TOWER_MFMA = ("x6", "f32")
 
     def __init__(self, net, epilogue=None, native_conv=True, tower="x6"):
@@ -186,7 +210,7 @@ class FoldedNet(nn.Module):
         # (conv + bias + skip + ReLU); other widths use MIOpen + hz_bias_act
         self.stem_packed = None
         if self.native_conv and self.stem[0].shape == (128, 38, 3, 3):
-            self.stem_packed = pack_stem(self.stem[0])
+            self.stem_packed = pack_stem_x6(self.stem[0]) if self.tower == "x6" else pack_stem(self.stem[0])
         self.packed = None
         if self.native_conv and self.blocks and self.blocks[0][0][0].shape[:2] == (128, 128):
             pk = pack_conv3x3_x6 if self.tower == "x6" else pack_conv3x3
@@ -213,8 +237,8 @@ class FoldedNet(nn.Module):
         w, b = self.stem
         if self.stem_packed is None or self.packed is None:
             live = None
-        if self.stem_packed is not None:
-            x = _stem_act(board, self.stem_packed, b, live)  # reads the NCHW board directly
+        if self.stem_packed is not None:  # reads the NCHW board directly
+            x = (_stem_x6_act if self.tower == "x6" else _stem_act)(board, self.stem_packed, b, live)
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
         if self.packed is not None:

@@ -228,6 +228,11 @@ int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias
  * channels zero-padded to 48, packed as for hz_conv3x3_bias_act. */
 int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bias, float *out, int32_t batch,
                         const int32_t *live, void *stream);
+/* the stem on the bf16 MFMA with fp32-exact products (as hz_conv3x3_x6_bias_act);
+ * wpack6 = w with the input channels zero-padded to 64, packed as there
+ * (hzamd/infer.py:pack_stem_x6). */
+int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *bias, float *out, int32_t batch,
+                           const int32_t *live, void *stream);
 
 /* The heads of model.py:336-351 up to their linear layers, BN folded:
  * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)

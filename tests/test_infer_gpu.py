@@ -187,6 +187,21 @@ def test_conv3x3_x6_fp32_accuracy_vs_fp64(live):
         assert torch.equal(part[:live], full[:live])
 
 
+def test_stem_x6_fp32_accuracy_vs_fp64():
+    """Encoder-like boards (0, 1/3, 2/3, 1, bag fractions: not bf16 values):
+    the bf16x6 stem's error vs a float64 conv is at the f32 stem's level."""
+    from hzamd.infer import _stem_act, _stem_x6_act, pack_stem, pack_stem_x6
+    g = torch.Generator().manual_seed(4)
+    n = 200
+    board = torch.randint(0, 4, (n, 38, 5, 7), generator=g).float() / 3.0
+    w = torch.randn(128, 38, 3, 3, generator=g) * 0.1
+    b = torch.randn(128, generator=g) * 0.1
+    want = _conv_ref(board, w, b, None)
+    e32 = (_stem_act(board.cuda(), pack_stem(w).cuda(), b.cuda()).cpu().double() - want).abs().max().item()
+    e6 = (_stem_x6_act(board.cuda(), pack_stem_x6(w).cuda(), b.cuda()).cpu().double() - want).abs().max().item()
+    assert e6 <= 2 * e32 + 1e-7, (e6, e32)
+
+
 @pytest.mark.parametrize("batch", [1, 5, 4096])
 def test_heads_match_torch(batch):
     """hz_heads == conv1x1 + bias + ReLU, NCHW flatten, concat with glob for
@@ -207,11 +222,15 @@ def test_heads_match_torch(batch):
     assert torch.equal(pcat[:, 70:], glob) and torch.equal(vcat[:, 35:], glob)
 
 
+@pytest.mark.parametrize("kind", ["f32", "x6"])
 @pytest.mark.parametrize("batch", [1, 13, 64])
-def test_stem_exact_on_integer_data(batch):
-    """hz_stem3x3_bias_act on small-integer data equals the fp64 conv exactly
-    (NCHW board in, NHWC out; channel padding 38 -> 48 must contribute 0)."""
-    from hzamd.infer import _stem_act, pack_stem
+def test_stem_exact_on_integer_data(batch, kind):
+    """hz_stem3x3_bias_act / hz_stem3x3_x6_bias_act on small-integer data
+    equal the fp64 conv exactly (NCHW board in, NHWC out; channel padding
+    38 -> 48 / 64 must contribute 0)."""
+    from hzamd.infer import _stem_act, _stem_x6_act, pack_stem, pack_stem_x6
+    if kind == "x6":
+        _stem_act, pack_stem = _stem_x6_act, pack_stem_x6
     g = torch.Generator().manual_seed(100 + batch)
     board = torch.randint(-3, 4, (batch, 38, 5, 7), generator=g).float()
     w = torch.randint(-2, 3, (128, 38, 3, 3), generator=g).float()

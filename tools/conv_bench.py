@@ -11,7 +11,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "harmonies-alphazero_amd")]
 
 import torch  # noqa: E402
 
-from hzamd.infer import _conv3x3_act, _conv3x3_x6_act, pack_conv3x3, pack_conv3x3_x6  # noqa: E402
+from hzamd.infer import (_conv3x3_act, _conv3x3_x6_act, _stem_act, _stem_x6_act, pack_conv3x3,  # noqa: E402
+                         pack_conv3x3_x6, pack_stem, pack_stem_x6)
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 cl = torch.channels_last
@@ -39,4 +40,19 @@ want = (torch.nn.functional.conv2d(x[:k].double().cpu(), w.double().cpu(), b.dou
         + r[:k].double().cpu()).relu()
 for name, fn, wp in (("f32", _conv3x3_act, pack_conv3x3(w)), ("x6", _conv3x3_x6_act, pack_conv3x3_x6(w))):
     out[name]["max_abs_err_vs_fp64"] = (fn(x, wp, b, r)[:k].double().cpu() - want).abs().max().item()
+# the stem (38 -> 128 channels, NCHW board in)
+board = (torch.rand(B, 38, 5, 7, device="cuda", generator=g) > 0.7).float()
+ws = torch.randn(128, 38, 3, 3, device="cuda", generator=g) * 0.1
+sflop = 2.0 * B * 35 * 128 * 342
+for name, fn, wp in (("stem_f32", _stem_act, pack_stem(ws)), ("stem_x6", _stem_x6_act, pack_stem_x6(ws))):
+    for _ in range(20):
+        fn(board, wp, b)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(100):
+        fn(board, wp, b)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 100 * 1e3
+    out[name] = {"us": us, "tflops_algorithmic": sflop / (us * 1e-6) / 1e12}
 print(json.dumps(out))

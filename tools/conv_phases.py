@@ -1,4 +1,4 @@
-"""Phase timing of k_conv3x3_w8 from the stamped diagnostic build
+"""Phase timing of k_conv3x3_w8 (or, with argument 2 = x6, k_conv3x3_x6) from the stamped diagnostic build
 (tools/libnet_diag.so, -DHZ_NET_DIAG): per workgroup, waves 0 and 4 stamp
 s_memtime at kernel start, after the halo/map setup, after chunk 0 is in
 LDS, at the end of each of the 4 chunks and after the epilogue (+ realtime
@@ -9,29 +9,33 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "harmonies-alphazero_amd"))
-from hzamd.infer import pack_conv3x3  # noqa: E402
+from hzamd.infer import pack_conv3x3, pack_conv3x3_x6  # noqa: E402
 
 lib = ctypes.CDLL(os.path.join(HERE, "libnet_diag.so"))
 vp = ctypes.c_void_p
 lib.hz_conv3x3_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
+lib.hz_conv3x3_x6_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
 lib.hz_net_diag_stamps.argtypes = [vp]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+X6 = len(sys.argv) > 2 and sys.argv[2] == "x6"
+fn = lib.hz_conv3x3_x6_bias_act if X6 else lib.hz_conv3x3_bias_act
+pack = pack_conv3x3_x6 if X6 else pack_conv3x3
 cl = torch.channels_last
 g = torch.Generator(device="cuda").manual_seed(0)
 x = torch.randn(B, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
-w = pack_conv3x3(torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.05)
+w = pack(torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.05)
 b = torch.randn(128, device="cuda", generator=g)
 r = torch.randn(B, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=cl)
 out = torch.empty_like(x)
 for _ in range(200):  # ~70 ms of back-to-back launches so the clock settles
-    assert lib.hz_conv3x3_bias_act(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr(), out.data_ptr(), B,
+    assert fn(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr(), out.data_ptr(), B,
                                    None, torch.cuda.current_stream().cuda_stream) == 0
 st = np.zeros((1024, 2, 10), dtype=np.uint64)
 assert lib.hz_net_diag_stamps(st.ctypes.data) == 0
 nwg = (B + 7) // 8
 s = st[:nwg].astype(np.int64)
 names = ["setup", "chunk0_stage", "chunk0", "chunk1", "chunk2", "chunk3", "epilogue"]
-res = {"batch": B, "workgroups": nwg}
+res = {"batch": B, "workgroups": nwg, "kernel": "k_conv3x3_x6" if X6 else "k_conv3x3_w8"}
 for wv in range(2):
     d = np.diff(s[:, wv, :8], axis=1)
     res[f"wave{4 * wv}_median_cycles"] = {n: float(np.median(d[:, i])) for i, n in enumerate(names)}
