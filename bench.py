@@ -70,7 +70,7 @@ def parse():
                     help="skip the chance-ahead-off comparison run (profiling)")
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
                          "moves with the network; 4: whole self-play iterations + the RCCL all-gather into "
@@ -629,14 +629,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     launches = [0]  # hz_play launches so far: launch k plays every board's episode k
 
-    def one_launch(ev=None, g=games, s=steps):
+    def one_launch(_unused=None, g=games, s=steps):
         # hz_play: HarmoniesGameState() on every board fused with rule-driven
         # play to the end of the game, one launch
-        if ev:
-            ev[0].record(stream)
         env.rollout(MAX_PLIES, games_done=g, steps_done=s, reset=True)
-        if ev:
-            ev[1].record(stream)
         launches[0] += 1
 
     # first batch (episode 0: board b seeded seed_base + rank*n + b) doubles as
@@ -671,15 +667,18 @@ def main():
     elapsed = time.perf_counter() - t0
     last_ep = launches[0] - 1
     last_state = env.export_state()
-    # the dominant kernel's average launch duration, from HIP events around
-    # each launch on its stream, in a separate loop of the same launches (the
-    # event markers would otherwise sit between the timed launches)
+    # the dominant kernel's average launch duration: HIP events on the env's
+    # stream around a block of K back-to-back launches (no markers between
+    # them), outside the timed region; rocprofv3's per-dispatch average for
+    # k_rollout (profiles/<round>/stats) is the figure it must agree with
     K = min(T, 512)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
     for i in range(K):
-        one_launch(evs[i], games, steps)
+        one_launch(None, games, steps)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / K
+    kern_ms = ev0.elapsed_time(ev1) / K
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
     longest = int(steps_t.max())

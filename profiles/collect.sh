@@ -14,14 +14,16 @@ OUT=$REPO/gpurun_out/$R
 mkdir -p "$OUT/stats"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
-  python3 "$REPO/bench.py" --steps 50 --warmup 3 --no-cpu-baseline --no-off-compare > "$OUT/stats/bench_under_prof.json"
+  python3 "$REPO/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-off-compare --sp-cpu-seconds 0 \
+  > "$OUT/stats/bench_under_prof.json"
 k=0
 for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
          "SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS" \
          "FETCH_SIZE" "WRITE_SIZE"; do
   mkdir -p "$OUT/pmc/p$k"
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc/p$k" -o run -- \
-    python3 "$REPO/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-off-compare > "$OUT/pmc/p$k/bench.json"
+    python3 "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-off-compare --no-selfplay \
+    > "$OUT/pmc/p$k/bench.json"
   k=$((k+1))
 done
 python3 "$REPO/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc/summary.json"
