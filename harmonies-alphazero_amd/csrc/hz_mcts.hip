@@ -230,7 +230,135 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
   if (t == kGatherThreads - 1) count[0] = part[t];
 }
 
+// ------------------------------------------------ turn-end chance, in parallel
+// At a turn end (phase place_tile_3) every child of the leaf refills the one
+// missing pile from the same bag: _draw_tiles(3) = random.sample(range(n), 3)
+// over the same flat bag (harmonies_engine.py:120-137), child after child on
+// the board's stream (MCTS.py:171-176).  Only the stream position couples the
+// children.  With n > 21 (random.py's set method: every pick is
+// _randbelow(n), a repeat of the child's own earlier pick is drawn again),
+// the wave produces 64 tempered words at a time (twisting the generation in
+// place 64 words at a time: a block's sources are either old words beyond
+// it or new words before it), each lane tests its word against n, and one
+// wave-uniform scalar walk over the accepted words (readlane) groups them
+// into the children's three picks.  Returns the stream cursor (pos | tw <<
+// 16, as MTS) after the last child's third pick; script[c] = the pile the
+// c-th child draws, as replenish() records it.
+__device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, uint64_t misc, int nl, int lane,
+                                       uint64_t *script) {
+  int cnt[6];
+  uint32_t n = 0;
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    cnt[t] = bag_n(misc, t);
+    n += (uint32_t)cnt[t];
+  }
+  const int kb = 32 - __clz(n);
+  int pos = cursor & 0xFFFF, tw = cursor >> 16;
+  int c = 0, got = 0;
+  uint32_t j0 = 0, j1 = 0;
+  // child c's picks, kept by lane c & 63 (children >= 64 in the second set)
+  uint32_t p0 = 0, p1 = 0, p2 = 0, q0 = 0, q1 = 0, q2 = 0;
+  for (;;) {
+    if (pos >= kMT) {  // next generation
+      pos = 0;
+      tw = 0;
+    }
+    const int need = pos + kWave < kMT ? pos + kWave : kMT;
+    while (tw < need) {  // twist [tw, tw + 64) of the current generation
+      const int i = tw + lane;
+      uint32_t nw = 0;
+      if (i < kMT) {
+        const uint32_t cur = w[i], nxt = w[i + 1 < kMT ? i + 1 : 0];
+        const uint32_t far = w[i < 227 ? i + 397 : (i < 623 ? i - 227 : 396)];
+        nw = twist_word(cur, nxt, far);
+      }
+      __builtin_amdgcn_wave_barrier();  // every lane has read before any writes
+      if (i < kMT) w[i] = nw;
+      __builtin_amdgcn_wave_barrier();
+      tw = tw + kWave < kMT ? tw + kWave : kMT;
+    }
+    const int i = pos + lane;
+    const uint32_t r = i < kMT ? temper(w[i]) >> (32 - kb) : n;
+    uint64_t acc = __ballot(r < n);
+    int last = -1;  // window offset of the word that completed the last child
+    while (acc) {
+      const int src = __builtin_ctzll(acc);  // wave-uniform
+      acc &= acc - 1;
+      const uint32_t v = __builtin_amdgcn_readlane(r, src);
+      if ((got >= 1 && v == j0) || (got >= 2 && v == j1)) continue;  // repeat: drawn again
+      if (got == 0) {
+        j0 = v;
+        got = 1;
+      } else if (got == 1) {
+        j1 = v;
+        got = 2;
+      } else {
+        if (lane == (c & 63)) {
+          if (c < kWave) {
+            p0 = j0;
+            p1 = j1;
+            p2 = v;
+          } else {
+            q0 = j0;
+            q1 = j1;
+            q2 = v;
+          }
+        }
+        got = 0;
+        if (++c == nl) {
+          last = src;
+          break;
+        }
+      }
+    }
+    if (last >= 0) {
+      pos += last + 1;
+      break;
+    }
+    pos = need;
+  }
+  // lane c: the tiles at flat indices p0, p1, p2 (insertion order water, plant,
+  // wood, stone, field, building: constants.py:41) -> the pile, the script
+  constexpr uint32_t kOrder = WATER | (PLANT << 3) | (WOOD << 6) | (STONE << 9) | (FIELD << 12) | (BUILDING << 15);
+  const uint32_t e0 = (uint32_t)cnt[WATER], e1 = e0 + (uint32_t)cnt[PLANT], e2 = e1 + (uint32_t)cnt[WOOD];
+  const uint32_t e3 = e2 + (uint32_t)cnt[STONE], e4 = e3 + (uint32_t)cnt[FIELD];
+  auto tile = [&](uint32_t x) {
+    const uint32_t o = (uint32_t)(x >= e0) + (uint32_t)(x >= e1) + (uint32_t)(x >= e2) + (uint32_t)(x >= e3) +
+                       (uint32_t)(x >= e4);
+    return __builtin_amdgcn_ubfe(kOrder, 3 * o, 3);
+  };
+  if (lane < nl) script[lane] = (((1ull << 45) - 1) & ~0x1FFull) | tile(p0) | tile(p1) << 3 | tile(p2) << 6;
+  if (lane + kWave < nl)
+    script[lane + kWave] = (((1ull << 45) - 1) & ~0x1FFull) | tile(q0) | tile(q1) << 3 | tile(q2) << 6;
+  return pos | (tw << 16);
+}
+
 // ---------------------------------------------------------- expand + backup
+#ifdef HZ_DIAG
+// diagnostic build only (tools/expand_phases.py): per board, s_memtime at the
+// phase boundaries of k_expand_backup + flags; written to this buffer alone
+__device__ uint64_t g_exp_stamps[16384][12];
+// one asm statement fenced by scheduling barriers, so the stamp stays where it
+// is written (cdna_hip_programming.md §7, in-kernel stamps)
+__device__ __forceinline__ uint64_t xstamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define HZ_XSTAMP(k) \
+  {                                                          \
+    const uint64_t t_ = xstamp();                            \
+    if (lane == 0 && b < 16384) g_exp_stamps[b][k] = t_;     \
+  }
+#define HZ_XFLAG(k, v) \
+  if (lane == 0 && b < 16384) g_exp_stamps[b][k] = (uint64_t)(v);
+#else
+#define HZ_XSTAMP(k)
+#define HZ_XFLAG(k, v)
+#endif
 struct ExpandLds {
   uint32_t mt[kMT];
   uint64_t script[kChildSlots];
@@ -253,6 +381,8 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
   __shared__ ExpandLds L;
   int b = blockIdx.x;
   int lane = threadIdx.x;
+  HZ_XSTAMP(0)
+  HZ_XFLAG(10, 0)
   int leaf = m.leaf[b];
   if (leaf < 0) return;
   int32_t *cnt = m.counts + (size_t)b * 4;
@@ -273,16 +403,37 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
     uint64_t mk[3];
     int nl = legal_mask(ls, mk);
     bool noisy = leaf == 0 && !testing && noise;
+    HZ_XSTAMP(1)
     if (nl > 0 && nl <= kMaxChildren && m.node_ne[nb + leaf] == 0) {
       bool turn_end = phase_of(ls.misc) == PH_P3;
+      HZ_XFLAG(10, 1 | (turn_end ? 2 : 0) | (nl << 8))
       if (turn_end) {
         // the children's _end_turn_actions draw from the board's stream in
         // child order (MCTS.py:171-176): replay that sequence once, serially,
         // on an LDS copy of the stream
         uint32_t *g = mtw + (size_t)b * kMT;
-        for (int i = lane; i < kMT; i += kWave) L.mt[i] = g[i];
+        {  // all ten of the lane's words in flight at once (one memory round trip)
+          uint32_t v[(kMT + kWave - 1) / kWave];
+#pragma unroll
+          for (int k = 0; k < (kMT + kWave - 1) / kWave; k++) {
+            const int i = lane + kWave * k;
+            v[k] = i < kMT ? g[i] : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < (kMT + kWave - 1) / kWave; k++) {
+            const int i = lane + kWave * k;
+            if (i < kMT) L.mt[i] = v[k];
+          }
+        }
         __syncthreads();
-        if (lane == 0) {
+        int bag = 0;
+#pragma unroll
+        for (int t = 0; t < 6; t++) bag += bag_n(ls.misc, t);
+        if (npiles_of(ls.piles) == 4 && bag > 21) {
+          // one pile per child, random.sample's set method: the wave-parallel form
+          const int cur = turn_end_draws_parallel(L.mt, mtcur[b], ls.misc, nl, lane, L.script);
+          if (lane == 0) mtcur[b] = cur;
+        } else if (lane == 0) {  // fewer piles or the pool method: one lane, serially
           StreamDraw<MT> draw{MT(L.mt, mtcur[b])};
           for (int c = 0; c < nl; c++) {
             State tmp = ls;
@@ -291,8 +442,9 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
           mtcur[b] = draw.m.cursor();
         }
         __syncthreads();
-        for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];
+        for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];  // stores: no round trip to wait for
       }
+      HZ_XSTAMP(2)
       // children: lane handles child c = lane and lane + 64
       for (int c = lane; c < kChildSlots; c += kWave) {
         if (c < nl) {
@@ -313,6 +465,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
         }
       }
       __syncthreads();
+      HZ_XSTAMP(3)
       // transpositions (MCTS.py:177-204): a child whose key is already in the
       // tree reuses that node (flag 1), or is skipped if it is the leaf itself
       // (flag 2) ...
@@ -339,21 +492,53 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
         }
       }
       __syncthreads();
+      HZ_XSTAMP(4)
       // ... and among the remaining children the first of equal keys creates
-      // the node, later siblings reuse it (flag 3: child[c] = that sibling)
-      for (int c = lane; c < kChildSlots; c += kWave) {
-        if (c >= nl || L.flag[c] != 0) continue;
-        uint64_t h = L.hash[c];
-        for (int c2 = 0; c2 < c; c2++) {
-          if (L.flag[c2] != 0 || L.hash[c2] != h) continue;
-          bool eq = true;
+      // the node, later siblings reuse it (flag 3: child[c] = that sibling).
+      // Wave-uniform walk over the new children c2 in ascending order: c2's
+      // hash is broadcast from its lane's register (readlane), every lane
+      // compares it with its own children's; keys are compared only on equal
+      // hashes.  The first match is the target (a target is never itself a
+      // duplicate: it has no earlier equal sibling).
+      {
+        const int c0 = lane, c1 = lane + kWave;
+        const bool new0 = c0 < nl && L.flag[c0] == 0, new1 = c1 < nl && L.flag[c1] == 0;
+        const uint64_t h0 = new0 ? L.hash[c0] : 0, h1 = new1 ? L.hash[c1] : 0;
+        const uint64_t cand[2] = {__ballot(new0), __ballot(new1)};
+        int dup0 = -1, dup1 = -1;
 #pragma unroll
-          for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c][w];
-          if (eq) {
-            L.flag[c] = 3;
-            L.child[c] = c2;
-            break;
+        for (int r = 0; r < 2; r++) {
+          uint64_t rest = cand[r];
+          while (rest) {
+            const int src = __builtin_ctzll(rest);  // wave-uniform
+            rest &= rest - 1;
+            const int c2 = src + r * kWave;
+            const uint64_t hv = r == 0 ? h0 : h1;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)hv, src);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(hv >> 32), src);
+            const uint64_t hc2 = (uint64_t)hi << 32 | lo;
+            if (new0 && dup0 < 0 && c2 < c0 && h0 == hc2) {
+              bool eq = true;
+#pragma unroll
+              for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c0][w];
+              if (eq) dup0 = c2;
+            }
+            if (new1 && dup1 < 0 && c2 < c1 && h1 == hc2) {
+              bool eq = true;
+#pragma unroll
+              for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c1][w];
+              if (eq) dup1 = c2;
+            }
           }
+        }
+        __syncthreads();  // every lane has read the flags before any is rewritten
+        if (dup0 >= 0) {
+          L.flag[c0] = 3;
+          L.child[c0] = dup0;
+        }
+        if (dup1 >= 0) {
+          L.flag[c1] = 3;
+          L.child[c1] = dup1;
         }
       }
       __syncthreads();
@@ -372,6 +557,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
         n_edges += __popcll(be);
       }
       __syncthreads();
+      HZ_XSTAMP(5)
       if (base_n + n_new > m.max_nodes || base_e + n_edges > m.max_edges) {
         if (lane == 0) cnt[3] = 1;  // capacity exhausted: leave the leaf unexpanded
       } else {
@@ -419,6 +605,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
       cnt[3] = 2;
     }
   }
+  HZ_XSTAMP(6)
   // back_fill: every path edge gets N += 1, W += v * (+1 if the edge's mover
   // is the leaf's player else -1)
   int d = m.depth[b];
@@ -429,6 +616,11 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
     m.edge_n[eb + e] += 1;
     m.edge_w[eb + e] = __dadd_rn(m.edge_w[eb + e], v * dir);
   }
+#ifdef HZ_DIAG
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  HZ_XSTAMP(7)
+  HZ_XFLAG(11, d)
 }
 
 // root visit counts by action (MCTS.py:355-376)
@@ -561,6 +753,13 @@ int hz_mcts_stats(hz_mcts *m, int32_t *counts) {
              ? 1
              : 0;
 }
+
+#ifdef HZ_DIAG
+int hz_mcts_diag_stamps(uint64_t *host) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_exp_stamps), sizeof(g_exp_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int hz_mcts_leaf_ptrs(hz_mcts *m, int32_t **leaf, int32_t **leaf_gidx) {
   if (!m) return -1;
