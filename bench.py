@@ -174,7 +174,8 @@ def bench_loop(args, dev, rank, world):
               "best_model_filename": "best_model.pth.tar"}
     mm = ModelManager(model_cfg, train_cfg)
     tr = Trainer(mm, mcts_cfg, sp_cfg, train_cfg, eval_mcts_config={"num_simulations": args.eval_sims},
-                 seed_base=args.seed_base, log=lambda *_: None)
+                 seed_base=args.seed_base,
+                 log=lambda *a: print(f"[config5 r{rank}]", *a, file=sys.stderr, flush=True))
     # warm-up iteration (kernels, allocator), then the timed ones
     tr.iteration = 0
     tr.execute_self_play_phase(tr.best_model_manager)
