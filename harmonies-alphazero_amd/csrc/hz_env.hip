@@ -43,6 +43,12 @@ struct hz_env {
   int32_t *ring_k1[3];       // [nrow] draws draw1 completed
   int calls;                 // hz_play calls (ring and play-slot rotation)
   int primed, slot_valid[2];
+  // where board b's current stream lives: -1 = mt (its own), k = ahead_mt[k]
+  // (an hz_play board that replayed a prepared episode keeps playing on the
+  // prepared copy; it is copied into mt only when something else needs it:
+  // materialize(), before any other entry point that reads streams)
+  int32_t *mt_src;           // [n]
+  int lazy;                  // some board may have mt_src >= 0
 };
 
 #ifdef HZ_DIAG
@@ -413,32 +419,6 @@ struct PlayDraw {
     return p9;
   }
 };
-
-// copy the streams of boards in `mask` from `src` to `dst` (both board-major
-// spans of nb x 624 words), threads [t0, t0 + nt) of the block; eight 16-B
-// loads in flight per thread
-__device__ __forceinline__ void copy_streams(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src, int nb,
-                                             int t, int nt, uint64_t mask) {
-  constexpr int U = 8;
-  int total4 = nb * (kMT / 4);
-  for (int q0 = 0; q0 < total4; q0 += nt * U) {
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {  // unconditional (clamped) loads: the values stay in registers
-      int q = q0 + u * nt + t;
-      v[u] = reinterpret_cast<const uint4 *>(src)[q < total4 ? q : total4 - 1];
-    }
-    // consumed here, unconditionally: otherwise each load is sunk into its
-    // guarded store's block and waited for alone (one load in flight)
-#pragma unroll
-    for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      int q = q0 + u * nt + t;
-      if (q < total4 && ((mask >> ((q * 4) / kMT)) & 1)) reinterpret_cast<uint4 *>(dst)[q] = v[u];
-    }
-  }
-}
 
 // Chance-ahead preparation: a three-stage pipeline in the blocks of each
 // hz_play launch beyond the playing ones (4 x 64 blocks of 162 KB LDS: one
@@ -824,7 +804,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     uint64_t *__restrict__ prep_pile, int32_t *__restrict__ prep_cur,
                                                     const int32_t *__restrict__ prep_ep, Ring rs, Ring r1,
                                                     Ring r2, long nrow, const uint32_t *__restrict__ ahead_rule,
-                                                    uint32_t *__restrict__ prep_rule) {
+                                                    uint32_t *__restrict__ prep_rule, int32_t *__restrict__ mt_src,
+                                                    int src_slot) {
 #ifdef HZ_DIAG
   uint64_t role_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -857,7 +838,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #ifdef HZ_DIAG
   if (g_role_only >= 0 && g_role_only != 3) return;
 #endif
-  __shared__ uint64_t s_lds_mask, s_recopy_mask;
+  __shared__ uint64_t s_lds_mask;
   int tid = threadIdx.x;
   int lane = tid & 63;
   bool w0 = __builtin_amdgcn_readfirstlane(tid) < 64;  // wave-uniform: wave 0 plays
@@ -880,7 +861,6 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
   }
   int ep0 = act ? episode[b] : 0;
   bool seeded = reset_first && act && ahead_tag && ahead_tag[b] == ep0;
-  uint64_t seededmask = __ballot(seeded);
   // the episode's rule hashes into rows [0, kRulePlies) of each seeded
   // lane's LDS column (a seeded lane replays its script and never keeps its
   // stream in LDS), all four waves, issued with the tag loads
@@ -910,10 +890,10 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #ifdef HZ_DIAG_ROLES_ONLY
   if (w0 && act) HZ_PHASE(13, role_t0, b);
 #endif
-  if (!w0) {
-    // waves 1-3: the prepared streams become the boards' streams while wave 0 plays
-    if (seededmask) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid - 64, kStageThreads - 64, seededmask);
-  } else if (act) {
+  // a board replaying a prepared episode plays on to the end on the
+  // prepared stream in ahead_mt (mt_src); it reaches the board's own mt
+  // only if something else needs it (materialize)
+  if (w0 && act) {
     PlayDraw draw{LdsMT(lane, reset_first ? kMTSeeded : pos[b]), seeded, false, 0, ahead_draws, 0, 0, 0, 0,
                   MT(ahead_mt ? ahead_mt + (size_t)b * kMT : nullptr, 0),
                   ahead_cur ? ahead_cur + (size_t)ahead_draws * n + b : nullptr};
@@ -1054,6 +1034,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     if (lds_used) pos[b] = draw.m.cursor();
     else if (draw.fell) pos[b] = draw.gm.cursor();
     else pos[b] = ahead_cur[(size_t)draw.d * n + b];
+    mt_src[b] = lds_used ? -1 : src_slot;
     ply[b] = g_ply;
     seed[b] = sd;
 #if defined(HZ_DIAG) && !defined(HZ_DIAG_ROLES_ONLY)
@@ -1065,20 +1046,13 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     if (games_done) games_done[b] = games;
     if (steps_done) steps_done[b] = steps;
     if (ep_final) ep_final[b] = episode[b];
-    uint64_t lm = __ballot(lds_used), rm = __ballot(!lds_used && draw.fell);
-    if (lane == 0) {
-      s_lds_mask = lm;
-      s_recopy_mask = rm;
-    }
+    uint64_t lm = __ballot(lds_used);
+    if (lane == 0) s_lds_mask = lm;
   }
-  if (w0 && !act && lane == 0 && actmask == 0) {
-    s_lds_mask = 0;
-    s_recopy_mask = 0;
-  }
+  if (w0 && !act && lane == 0 && actmask == 0) s_lds_mask = 0;
   __syncthreads();
-  uint64_t lds_mask = s_lds_mask & actmask, recopy = s_recopy_mask & actmask;
+  uint64_t lds_mask = s_lds_mask & actmask;
   if (lds_mask) stage_mt(g, nb, tid, lds_mask, false);
-  if (recopy) copy_streams(g, ahead_mt + (size_t)b0 * kMT, nb, tid, kStageThreads, recopy);
 #ifdef HZ_DIAG
   if (g_stamps && threadIdx.x < 64 && act) g_stamps[(size_t)b * 16 + 5] = __builtin_amdgcn_s_memtime() - role_t0;
 #endif
@@ -1167,6 +1141,33 @@ inline int launch_err() {
 }  // namespace
 
 // ======================================================================= ABI
+// boards whose stream lives in a play slot (mt_src >= 0): copy it into the
+// board's own stream, one wave per board
+__global__ void __launch_bounds__(64) k_mt_materialize(uint32_t *__restrict__ mt, const uint32_t *__restrict__ a0,
+                                                      const uint32_t *__restrict__ a1, int32_t *__restrict__ mt_src,
+                                                      int n) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int src = mt_src[b];
+  if (src < 0) return;
+  const uint32_t *from = (src ? a1 : a0) + (size_t)b * kMT;
+  uint32_t *to = mt + (size_t)b * kMT;
+  uint32_t v[(kMT + 63) / 64];
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++) v[k] = lane + 64 * k < kMT ? from[lane + 64 * k] : 0u;
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++)
+    if (lane + 64 * k < kMT) to[lane + 64 * k] = v[k];
+  if (lane == 0) mt_src[b] = -1;
+}
+
+static int materialize(hz_env *e) {
+  if (!e->lazy) return 0;
+  hipLaunchKernelGGL(k_mt_materialize, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ahead_mt[0], e->ahead_mt[1],
+                     e->mt_src, e->n);
+  e->lazy = 0;
+  return launch_err();
+}
+
 extern "C" {
 
 hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
@@ -1198,13 +1199,15 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
             hipMalloc(&e->pos, n * sizeof(int32_t)) == hipSuccess &&
             hipMalloc(&e->ply, n * sizeof(int32_t)) == hipSuccess &&
             hipMalloc(&e->episode, n * sizeof(int32_t)) == hipSuccess &&
-            hipMalloc(&e->seed, n * sizeof(uint64_t)) == hipSuccess;
+            hipMalloc(&e->seed, n * sizeof(uint64_t)) == hipSuccess &&
+            hipMalloc(&e->mt_src, n * sizeof(int32_t)) == hipSuccess;
   if (ok) {
     ok = hipMemset(e->state, 0, n * 6 * sizeof(uint64_t)) == hipSuccess &&
          hipMemset(e->pos, 0, n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->ply, 0, n * sizeof(int32_t)) == hipSuccess &&
          hipMemset(e->episode, 0, n * sizeof(int32_t)) == hipSuccess &&
-         hipMemset(e->seed, 0, n * sizeof(uint64_t)) == hipSuccess;
+         hipMemset(e->seed, 0, n * sizeof(uint64_t)) == hipSuccess &&
+         hipMemset(e->mt_src, 0xff, n * sizeof(int32_t)) == hipSuccess;
   }
   for (int k = 0; ok && k < 2; k++) {
     ok = hipMalloc(&e->ahead_mt[k], n * kMT * sizeof(uint32_t)) == hipSuccess &&
@@ -1258,6 +1261,7 @@ void hz_env_destroy(hz_env *e) {
   if (e->ply) (void)hipFree(e->ply);
   if (e->episode) (void)hipFree(e->episode);
   if (e->seed) (void)hipFree(e->seed);
+  if (e->mt_src) (void)hipFree(e->mt_src);
   free(e);
 }
 
@@ -1270,7 +1274,10 @@ int hz_env_set_stream(hz_env *e, void *stream) {
 }
 
 uint64_t *hz_env_state_ptr(hz_env *e) { return e ? e->state : nullptr; }
-uint32_t *hz_env_mt_ptr(hz_env *e) { return e ? e->mt : nullptr; }
+uint32_t *hz_env_mt_ptr(hz_env *e) {  // the streams are made current first (materialize)
+  if (!e || materialize(e)) return nullptr;
+  return e->mt;
+}
 int32_t *hz_env_mt_pos_ptr(hz_env *e) { return e ? e->pos : nullptr; }
 int32_t *hz_env_ply_ptr(hz_env *e) { return e ? e->ply : nullptr; }
 uint64_t *hz_env_seed_ptr(hz_env *e) { return e ? e->seed : nullptr; }
@@ -1287,6 +1294,7 @@ int hz_env_set_seed_ahead(hz_env *e, int32_t draws) {
 
 int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   if (!e) return -1;
+  if (int err = materialize(e)) return err;  // unselected boards keep their streams
   e->primed = 0;  // episode counters move outside hz_play's plan
   hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
@@ -1301,6 +1309,7 @@ int hz_legal_mask(hz_env *e, uint64_t *mask, int32_t *count) {
 
 int hz_step(hz_env *e, const int16_t *action, int32_t *status) {
   if (!e || !action) return -1;
+  if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_step, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
                      e->n, action, status);
   return launch_err();
@@ -1329,6 +1338,7 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
 
 int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
   if (!e || !action) return -1;
+  if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_greedy, dim3(e->n), dim3(64), 0, e->stream, e->state, e->mt, e->pos, e->n, sel, action);
   return launch_err();
 }
@@ -1349,6 +1359,10 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
+  // hz_rollout continues the current games on their streams; hz_play starts
+  // every board's next game (its old stream is dead)
+  if (!reset_first)
+    if (int err = materialize(e)) return err;
   uint32_t *ahead_mt = nullptr;
   const int32_t *ahead_tag = nullptr;
   const uint64_t *ahead_pile = nullptr;
@@ -1388,9 +1402,10 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
                      e->ahead_cur[w], e->ep_final[w], ring(c3), ring((c3 + 2) % kRing), ring((c3 + 1) % kRing),
-                     (long)e->nrow, ahead_rule, e->ahead_rule[w]);
+                     (long)e->nrow, ahead_rule, e->ahead_rule[w], e->mt_src, ahead_mt ? r : -1);
   int err = launch_err();
   if (err) return err;
+  if (ahead_mt) e->lazy = 1;
   if (pipe) {
     e->slot_valid[w] = 1;
     e->calls++;
@@ -1414,6 +1429,7 @@ int hz_export_state(hz_env *e, uint64_t *state, uint32_t *mt, int32_t *mt_index)
   if (state && hipMemcpyAsync(state, e->state, n * 6 * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream))
     return 1;
   if (mt || mt_index) {
+    if (int err = materialize(e)) return err;
     hipLaunchKernelGGL(k_mt_normalize, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->mt, e->pos, e->n,
                        mt_index);
     int r = launch_err();
@@ -1430,6 +1446,7 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
   if (state && hipMemcpyAsync(e->state, state, n * 6 * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream))
     return 1;
   if (mt) {
+    if (int err = materialize(e)) return err;  // (then every board's stream is its own)
     if (hipMemcpyAsync(e->mt, mt, n * kMT * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream)) return 1;
     hipLaunchKernelGGL(k_mt_import, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->pos, e->n, mt_index);
     return launch_err();
@@ -1439,6 +1456,7 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
 
 int hz_replenish(hz_env *e, const uint8_t *sel) {
   if (!e) return -1;
+  if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,
                      0);
   return launch_err();
@@ -1446,6 +1464,7 @@ int hz_replenish(hz_env *e, const uint8_t *sel) {
 
 int hz_end_turn(hz_env *e, const uint8_t *sel) {
   if (!e) return -1;
+  if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,
                      1);
   return launch_err();

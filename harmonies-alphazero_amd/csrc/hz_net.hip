@@ -360,10 +360,13 @@ __global__ void __launch_bounds__(512, 1)
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
-  const int s0 = blockIdx.x * kCS;
+  // the live rows are spread over the whole grid (launched for `batch`): a
+  // gathered leaf batch smaller than `batch` gives every workgroup fewer
+  // states (and row blocks) instead of idling the tail of the grid
   if (live) batch = *live < batch ? *live : batch;
-  if (s0 >= batch) return;
-  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+  const int s0 = (int)(((int64_t)blockIdx.x * batch) / gridDim.x);
+  const int ns = (int)(((int64_t)(blockIdx.x + 1) * batch) / gridDim.x) - s0;  // 0 .. kCS
+  if (ns <= 0) return;
   constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero region in each buffer
   HZ_STAMP(0)
   HZ_STAMP_RT(8)
@@ -388,9 +391,13 @@ __global__ void __launch_bounds__(512, 1)
     ldst[it] = sc * kX6Cell + 8 * part;
   }
   // stem: the four channels 32 q + 4 part + j of a slot, zero past channel 37
+  // (part from the clamped slot index, as in gsrc: an unclamped part would
+  // read up to 26 channels past a state, beyond the end of the last one)
   auto stem_load = [&](int it, int q) -> f32x4 {
     f32x4 v;
-    const int c0 = 32 * q + 4 * ((it * 512 + t) & 7);
+    int f = it * 512 + t;
+    f = f < kRows * 8 ? f : kRows * 8 - 1;
+    const int c0 = 32 * q + 4 * (f & 7);
 #pragma unroll
     for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC ? x[gsrc[it] + (32 * q + j) * 35] : 0.f;
     return v;
@@ -420,7 +427,11 @@ __global__ void __launch_bounds__(512, 1)
     *(uint2 *)(d_ + 128) = l_;                                                            \
   }
 
-  // A fragment of row block rb, tap: the lane's row r = (rh*9 + rb)*16 + (lane & 15)
+  // Row blocks are interleaved over the row halves (wave rh takes blocks
+  // 2 rb + rh), so a partial tile's row blocks stay balanced between the two
+  // waves of each SIMD; nv = this wave's row blocks holding live rows.
+  const int nblk = (ns * 35 + 15) / 16, nv = (nblk - rh + 1) / 2;
+  // A fragment of row block rb, tap: the lane's row r = (2 rb + rh)*16 + (lane & 15)
   // (clamped), its cell (h, w) of state s; neighbour (h + dh - 1, w + dw - 1)
   // or, off the board, the zero region at the same offset mod 256 (so the
   // lane keeps the LDS banks its row would use).
@@ -429,7 +440,7 @@ __global__ void __launch_bounds__(512, 1)
   uint32_t valid[kRB];
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    int r = (rh * kRB + rb) * 16 + (lane & 15);
+    int r = (2 * rb + rh) * 16 + (lane & 15);
     r = r < kRows ? r : kRows - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
     cbase[rb] = r * kX6Cell + 16 * kg;
@@ -473,44 +484,50 @@ __global__ void __launch_bounds__(512, 1)
     b[p][1] = bload(0, p, 1);
   }
 
+  // the K loop; a partial tile (a gathered batch's tail) skips the row
+  // blocks past its live rows (wave-uniform tests)
+  {
 #pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const char *lb = lds + (q & 1) * kX6Buf;
-    if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
-    for (int tap = 0; tap < 9; tap++) {
-      const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
-#pragma unroll
-      for (int p = 0; p < 3; p++) {
-        bn[p][0] = bload(Ln, p, 0);
-        bn[p][1] = bload(Ln, p, 1);
-      }
-      // plane a of A against the planes b with a + b <= 2
-#pragma unroll
-      for (int pa = 0; pa < 3; pa++) {
-        bf16x8 a[kRB];
-#pragma unroll
-        for (int rb = 0; rb < kRB; rb++) a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
-#pragma unroll
-        for (int pb = 0; pb < 3 - pa; pb++) {
-          const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
-#pragma unroll
-          for (int rb = 0; rb < kRB; rb++) {
-            acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
-            acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
+    for (int q = 0; q < NQ; q++) {
+      const char *lb = lds + (q & 1) * kX6Buf;
+      if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
+      for (int tap = 0; tap < 9; tap++) {
+        const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
+  #pragma unroll
+        for (int p = 0; p < 3; p++) {
+          bn[p][0] = bload(Ln, p, 0);
+          bn[p][1] = bload(Ln, p, 1);
+        }
+        // plane a of A against the planes b with a + b <= 2
+  #pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          bf16x8 a[kRB];
+  #pragma unroll
+          for (int rb = 0; rb < kRB; rb++)
+            if (rb < nv) a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
+  #pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++) {
+            const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
+  #pragma unroll
+            for (int rb = 0; rb < kRB; rb++) {
+              if (rb >= nv) continue;
+              acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
+              acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
+            }
           }
         }
+  #pragma unroll
+        for (int p = 0; p < 3; p++) {
+          b[p][0] = bn[p][0];
+          b[p][1] = bn[p][1];
+        }
       }
-#pragma unroll
-      for (int p = 0; p < 3; p++) {
-        b[p][0] = bn[p][0];
-        b[p][1] = bn[p][1];
+      if (q < NQ - 1) {
+        HZ_X6_STORE((q + 1) & 1)
+        __syncthreads();
       }
+      HZ_STAMP(3 + q)
     }
-    if (q < NQ - 1) {
-      HZ_X6_STORE((q + 1) & 1)
-      __syncthreads();
-    }
-    HZ_STAMP(3 + q)
   }
 
   const float bc0 = bias[co0], bc1 = bias[co0 + 16];
@@ -520,7 +537,7 @@ __global__ void __launch_bounds__(512, 1)
   float rv[kRB][2][4];
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+    const int rbase = (2 * rb + rh) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const bool ok = rbase + j < nrow;
@@ -530,7 +547,7 @@ __global__ void __launch_bounds__(512, 1)
   }
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+    const int rbase = (2 * rb + rh) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (rbase + j < nrow) {

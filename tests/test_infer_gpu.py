@@ -187,6 +187,46 @@ def test_conv3x3_x6_fp32_accuracy_vs_fp64(live):
         assert torch.equal(part[:live], full[:live])
 
 
+@pytest.mark.parametrize("batch", [1, 7, 15, 29, 300])
+def test_kernels_read_nothing_past_their_inputs(batch):
+    """Every input is the prefix of a buffer whose tail is NaN: a kernel that
+    reads past its last state (or past a state's 38 board channels into the
+    next one, which the zero weight rows would otherwise hide) turns
+    outputs into NaN.  The stems and tower convs at the small batch sizes the
+    arena's routed leaf batches take."""
+    from hzamd.infer import (_conv3x3_act, _conv3x3_x6_act, _stem_act, _stem_x6_act, pack_conv3x3,
+                             pack_conv3x3_x6, pack_stem, pack_stem_x6)
+    g = torch.Generator(device="cuda").manual_seed(batch)
+    cl = torch.channels_last
+    board = torch.full((batch + 2, 38, 5, 7), float("nan"), device="cuda")
+    board[:batch] = (torch.rand(batch, 38, 5, 7, device="cuda", generator=g) > 0.7).float()
+    ws = torch.randn(128, 38, 3, 3, device="cuda", generator=g) * 0.1
+    b = torch.randn(128, device="cuda", generator=g) * 0.1
+    for stem, pack in ((_stem_act, pack_stem), (_stem_x6_act, pack_stem_x6)):
+        assert bool(torch.isfinite(stem(board[:batch], pack(ws), b)).all())
+    x = torch.full((batch + 2, 128, 5, 7), float("nan"), device="cuda").contiguous(memory_format=cl)
+    x[:batch] = torch.randn(batch, 128, 5, 7, device="cuda", generator=g)
+    w = torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.03
+    for conv, pack in ((_conv3x3_act, pack_conv3x3), (_conv3x3_x6_act, pack_conv3x3_x6)):
+        y = conv(x[:batch], pack(w), b, x[:batch])
+        assert bool(torch.isfinite(y).all())
+
+
+def test_folded_small_batches_match_large_batch():
+    """FoldedNet on the small batches of a routed arena search (1..30 rows)
+    gives each row the result it gets in a large batch."""
+    g = torch.Generator().manual_seed(8)
+    torch.manual_seed(3)
+    net = HarmoniesNet().eval().cuda()
+    board = (torch.rand(64, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    glob = torch.rand(64, 42, generator=g).cuda()
+    fnet = FoldedNet(net)
+    l0, v0 = fnet(board, glob)
+    for k in (1, 2, 7, 15, 30):
+        l1, v1 = fnet(board[:k].clone(), glob[:k].clone())
+        assert torch.allclose(l1, l0[:k], atol=1e-5) and torch.allclose(v1, v0[:k], atol=1e-5), k
+
+
 def test_stem_x6_fp32_accuracy_vs_fp64():
     """Encoder-like boards (0, 1/3, 2/3, 1, bag fractions: not bf16 values):
     the bf16x6 stem's error vs a float64 conv is at the f32 stem's level."""

@@ -40,6 +40,20 @@ want = (torch.nn.functional.conv2d(x[:k].double().cpu(), w.double().cpu(), b.dou
         + r[:k].double().cpu()).relu()
 for name, fn, wp in (("f32", _conv3x3_act, pack_conv3x3(w)), ("x6", _conv3x3_x6_act, pack_conv3x3_x6(w))):
     out[name]["max_abs_err_vs_fp64"] = (fn(x, wp, b, r)[:k].double().cpu() - want).abs().max().item()
+# x6 with a device live-row count (gathered leaf batches): us per call
+wp6 = pack_conv3x3_x6(w)
+out["x6_live_us"] = {}
+for lv in (4096, 3500, 3000, 2049, 2048, 1000, 256):
+    lt = torch.tensor([lv], dtype=torch.int32, device="cuda")
+    for _ in range(5):
+        _conv3x3_x6_act(x, wp6, b, r, lt)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        _conv3x3_x6_act(x, wp6, b, r, lt)
+    e1.record()
+    torch.cuda.synchronize()
+    out["x6_live_us"][lv] = e0.elapsed_time(e1) / 50 * 1e3
 # the stem (38 -> 128 channels, NCHW board in)
 board = (torch.rand(B, 38, 5, 7, device="cuda", generator=g) > 0.7).float()
 ws = torch.randn(128, 38, 3, 3, device="cuda", generator=g) * 0.1
