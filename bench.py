@@ -49,6 +49,8 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 PIPELINE_DEPTH = 4         # hz_play launches until every board replays a fully prepared episode
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+X6_PRODUCTS = 6                # bf16 MFMAs per fp32 product block in the x6 kernels
 CLOCK_GHZ = 2.4            # MI355X peak engine clock (cycle figures of the issue-bound view)
 MT_SEED_STEPS = 1246       # init_by_array's two 623-step passes: the seeding chain per reset
 MT_STEP_FLOOR_CYCLES = 17  # tools/alu_chain.py: the bare MT recurrence per step
@@ -449,10 +451,14 @@ def selfplay_probe(args, dev, rank, world):
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
                "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
                "nn_rows_evaluated": rows, "sims": sims_done,
-               "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": nn_tf / FP32_MFMA_PEAK_TFLOPS if nn_tf else None,
-                               "flop_per_eval": fl, "basis": "whole leaf-eval forward (HIP events around "
-                                                             "each call) incl. the linear layers"},
+               "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS,
+                               "unit": "TFLOP/s",
+                               "frac": nn_tf / (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS) if nn_tf else None,
+                               "flop_per_eval": fl,
+                               "basis": "fp32 FLOP of the whole leaf-eval forward (HIP events around each call, incl. "
+                                        "the linear layers) against the bf16 MFMA's dense peak / 6 (the stem and "
+                                        "tower convs issue six bf16 MFMAs per fp32 product block); the f32 MFMA "
+                                        f"peak is {FP32_MFMA_PEAK_TFLOPS} TFLOP/s"},
                "exchange": exchange, "dtype": "fp32", "n_gpus": world}
         if cpu_roots is not None and args.sp_cpu_seconds > 0:
             out["cpu_baseline"] = selfplay_cpu_baseline(cpu_roots, sp.noise_log[0][0], sims, args.sp_cpu_seconds)

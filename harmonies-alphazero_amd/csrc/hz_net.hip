@@ -360,13 +360,10 @@ __global__ void __launch_bounds__(512, 1)
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
-  // the live rows are spread over the whole grid (launched for `batch`): a
-  // gathered leaf batch smaller than `batch` gives every workgroup fewer
-  // states (and row blocks) instead of idling the tail of the grid
-  if (live) batch = *live < batch ? *live : batch;
-  const int s0 = (int)(((int64_t)blockIdx.x * batch) / gridDim.x);
-  const int ns = (int)(((int64_t)(blockIdx.x + 1) * batch) / gridDim.x) - s0;  // 0 .. kCS
-  if (ns <= 0) return;
+  const int s0 = blockIdx.x * kCS;
+  if (live) batch = *live < batch ? *live : batch;  // rows past the live count are not computed
+  if (s0 >= batch) return;
+  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
   constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero region in each buffer
   HZ_STAMP(0)
   HZ_STAMP_RT(8)
@@ -427,11 +424,7 @@ __global__ void __launch_bounds__(512, 1)
     *(uint2 *)(d_ + 128) = l_;                                                            \
   }
 
-  // Row blocks are interleaved over the row halves (wave rh takes blocks
-  // 2 rb + rh), so a partial tile's row blocks stay balanced between the two
-  // waves of each SIMD; nv = this wave's row blocks holding live rows.
-  const int nblk = (ns * 35 + 15) / 16, nv = (nblk - rh + 1) / 2;
-  // A fragment of row block rb, tap: the lane's row r = (2 rb + rh)*16 + (lane & 15)
+  // A fragment of row block rb, tap: the lane's row r = (rh*9 + rb)*16 + (lane & 15)
   // (clamped), its cell (h, w) of state s; neighbour (h + dh - 1, w + dw - 1)
   // or, off the board, the zero region at the same offset mod 256 (so the
   // lane keeps the LDS banks its row would use).
@@ -440,7 +433,7 @@ __global__ void __launch_bounds__(512, 1)
   uint32_t valid[kRB];
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    int r = (2 * rb + rh) * 16 + (lane & 15);
+    int r = (rh * kRB + rb) * 16 + (lane & 15);
     r = r < kRows ? r : kRows - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
     cbase[rb] = r * kX6Cell + 16 * kg;
@@ -484,8 +477,6 @@ __global__ void __launch_bounds__(512, 1)
     b[p][1] = bload(0, p, 1);
   }
 
-  // the K loop; a partial tile (a gathered batch's tail) skips the row
-  // blocks past its live rows (wave-uniform tests)
   {
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
@@ -504,13 +495,12 @@ __global__ void __launch_bounds__(512, 1)
           bf16x8 a[kRB];
   #pragma unroll
           for (int rb = 0; rb < kRB; rb++)
-            if (rb < nv) a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
+            a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
   #pragma unroll
           for (int pb = 0; pb < 3 - pa; pb++) {
             const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
   #pragma unroll
             for (int rb = 0; rb < kRB; rb++) {
-              if (rb >= nv) continue;
               acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
               acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
             }
@@ -537,7 +527,7 @@ __global__ void __launch_bounds__(512, 1)
   float rv[kRB][2][4];
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (2 * rb + rh) * 16 + 4 * kg;
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const bool ok = rbase + j < nrow;
@@ -547,7 +537,7 @@ __global__ void __launch_bounds__(512, 1)
   }
 #pragma unroll
   for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (2 * rb + rh) * 16 + 4 * kg;
+    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (rbase + j < nrow) {
