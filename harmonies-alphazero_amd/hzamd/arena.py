@@ -58,14 +58,25 @@ class _Routed:
     """One leaf batch, each row evaluated by its board's searching agent.
     BatchedMCTS gathers the leaves that need the network (device_rows):
     row j belongs to board rows[j], so the agent is picked by rows[j], never
-    by the row's position."""
+    by the row's position.  When both evaluators take device row counts
+    (BatchedPredictor), both run on the whole gathered batch and each row
+    keeps its agent's result: no host round trip per simulation (the arena's
+    batches are a few dozen rows, so two whole forwards cost what two halves
+    do); otherwise the rows are split on the host."""
 
     device_rows = True
 
     def __init__(self, eval_a, eval_b, a_rows):
         self.eval_a, self.eval_b, self.a_rows = eval_a, eval_b, a_rows
+        self.both_device = bool(getattr(eval_a, "device_rows", False) and getattr(eval_b, "device_rows", False))
 
     def __call__(self, board, glob, rows=None, count=None):
+        if rows is not None and self.both_device:
+            pa, va = self.eval_a(board, glob, rows, count)
+            pb, vb = self.eval_b(board, glob, rows, count)
+            a = self.a_rows.index_select(0, rows.to(torch.int64).clamp(0, self.a_rows.numel() - 1))
+            return (torch.where(a.unsqueeze(1), pa.to(torch.float32), pb.to(torch.float32)),
+                    torch.where(a, va.reshape(-1).to(torch.float32), vb.reshape(-1).to(torch.float32)))
         if rows is not None:
             k = int(count.item())
             board, glob = board[:k], glob[:k]

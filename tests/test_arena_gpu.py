@@ -67,6 +67,28 @@ def test_mcts_vs_mcts_routed_batch():
     check(a, b, ("mcts", "mcts"), 16, 500)
 
 
+class _DeviceRows:
+    """A device-row evaluator (as BatchedPredictor): called on the whole
+    gathered buffers with the live count left on the device."""
+
+    device_rows = True
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self, board, glob, rows=None, count=None):
+        return self.fn(board, glob)
+
+
+def test_mcts_vs_mcts_routed_device_rows_two_evaluators():
+    """The no-round-trip routing (both evaluators on the whole gathered
+    batch, rows picked by their board's agent) plays the same games as the
+    oracle with each agent's own evaluator."""
+    a = MctsAgent(_DeviceRows(stub_evaluator), {"num_simulations": SIMS})
+    b = MctsAgent(_DeviceRows(neg_stub_evaluator), {"num_simulations": SIMS})
+    check(a, b, ("mcts", "mcts_neg"), 24, 700)
+
+
 def test_mcts_vs_mcts_routed_batch_two_evaluators():
     """The shared search routes each gathered leaf row to its board's agent
     by board id: two different evaluators (the stub and its negated value),
