@@ -40,6 +40,17 @@ want = (torch.nn.functional.conv2d(x[:k].double().cpu(), w.double().cpu(), b.dou
         + r[:k].double().cpu()).relu()
 for name, fn, wp in (("f32", _conv3x3_act, pack_conv3x3(w)), ("x6", _conv3x3_x6_act, pack_conv3x3_x6(w))):
     out[name]["max_abs_err_vs_fp64"] = (fn(x, wp, b, r)[:k].double().cpu() - want).abs().max().item()
+# x6 without the residual (the first conv of a block): the epilogue's share
+for _ in range(20):
+    _conv3x3_x6_act(x, pack_conv3x3_x6(w), b, None)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+wp6n = pack_conv3x3_x6(w)
+e0.record()
+for _ in range(100):
+    _conv3x3_x6_act(x, wp6n, b, None)
+e1.record()
+torch.cuda.synchronize()
+out["x6_nores_us"] = e0.elapsed_time(e1) / 100 * 1e3
 # x6 with a device live-row count (gathered leaf batches): us per call
 wp6 = pack_conv3x3_x6(w)
 out["x6_live_us"] = {}
