@@ -387,18 +387,34 @@ __global__ void __launch_bounds__(512, 1)
       gsrc[it] = (s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
     ldst[it] = sc * kX6Cell + 8 * part;
   }
-  // stem: the four channels 32 q + 4 part + j of a slot, zero past channel 37
-  // (part from the clamped slot index, as in gsrc: an unclamped part would
-  // read up to 26 channels past a state, beyond the end of the last one)
+  // stem: the four channels 32 q + 4 part + j of a slot (part from the
+  // clamped slot index, as in gsrc: an unclamped part would read up to 26
+  // channels past a state, beyond the end of the last one).  Channel 37
+  // (phase / 3: 1/3 and 2/3 are not bf16 values) stages as its three bf16
+  // pieces in slots 37, 38, 39, whose weights are packed as the planes
+  // (h, m, l), (h, m, 0), (h, 0, 0) of w37: the same six products as
+  // splitting it in place, but every staged value of an encoder board is then
+  // a bf16 value, which lets the chunk skip the A pieces' products (below).
+  // Slots past 39 stage as zeros.
   auto stem_load = [&](int it, int q) -> f32x4 {
     f32x4 v;
     int f = it * 512 + t;
     f = f < kRows * 8 ? f : kRows * 8 - 1;
     const int c0 = 32 * q + 4 * (f & 7);
+    if (c0 == 36) {
+      v[0] = x[gsrc[it] + (32 * q) * 35];
+      const float p = x[gsrc[it] + (32 * q + 1) * 35];
+      const float h = bf16_value(bf16_bits(p)), r = p - h, m = bf16_value(bf16_bits(r));
+      v[1] = h;
+      v[2] = m;
+      v[3] = bf16_value(bf16_bits(r - m));
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC ? x[gsrc[it] + (32 * q + j) * 35] : 0.f;
+      for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC - 1 ? x[gsrc[it] + (32 * q + j) * 35] : 0.f;
+    }
     return v;
   };
+  static_assert(kBoardC == 38, "stem_load places the phase channel 37 in slots 37-39");
 #define HZ_X6_LOAD(q)                                                                     \
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
   if constexpr (Stem) {                                                                   \
@@ -422,6 +438,17 @@ __global__ void __launch_bounds__(512, 1)
     *(uint2 *)d_ = h_;                                                                    \
     *(uint2 *)(d_ + 64) = m_;                                                             \
     *(uint2 *)(d_ + 128) = l_;                                                            \
+    pieces |= m_.x | m_.y | l_.x | l_.y;                                                  \
+  }
+  // the chunk's A pieces m, l are all zero (every staged value is a bf16
+  // value: an encoder board's stem input): only the h plane's three products
+  // are issued.  Workgroup-uniform; the tower always takes all six.
+#define HZ_X6_SYNC(dst)                                                                   \
+  if constexpr (Stem) {                                                                   \
+    dst = __builtin_amdgcn_readfirstlane(__syncthreads_or(pieces != 0));                  \
+    pieces = 0;                                                                           \
+  } else {                                                                                \
+    __syncthreads();                                                                      \
   }
 
   // A fragment of row block rb, tap: the lane's row r = (rh*9 + rb)*16 + (lane & 15)
@@ -464,10 +491,13 @@ __global__ void __launch_bounds__(512, 1)
     return wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
   };
 
+  uint32_t pieces = 0;
+  int npa = 3, npa_next = 3;  // A planes issued for this chunk, the next one
   HZ_STAMP(1)
   HZ_X6_LOAD(0)
   HZ_X6_STORE(0)
-  __syncthreads();
+  HZ_X6_SYNC(npa)
+  if constexpr (Stem) npa = npa ? 3 : 1;
   HZ_STAMP(2)
 
   bf16x8 b[3][2], bn[3][2];  // this K-step's B fragments, the next step's (loaded a step ahead)
@@ -492,6 +522,7 @@ __global__ void __launch_bounds__(512, 1)
         // plane a of A against the planes b with a + b <= 2
   #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
+          if (pa >= npa) break;
           bf16x8 a[kRB];
   #pragma unroll
           for (int rb = 0; rb < kRB; rb++)
@@ -514,7 +545,8 @@ __global__ void __launch_bounds__(512, 1)
       }
       if (q < NQ - 1) {
         HZ_X6_STORE((q + 1) & 1)
-        __syncthreads();
+        HZ_X6_SYNC(npa_next)
+        if constexpr (Stem) npa = npa_next ? 3 : 1;
       }
       HZ_STAMP(3 + q)
     }
@@ -558,6 +590,7 @@ __global__ void __launch_bounds__(512, 1)
 #undef HZ_STAMP
 #undef HZ_STAMP_RT
 #undef HZ_X6_STORE
+#undef HZ_X6_SYNC
 
 }  // namespace
 
@@ -658,6 +691,224 @@ extern "C" int hz_heads(const float *x, const float *hw, const float *hb, const 
   if (batch == 0) return 0;
   hipLaunchKernelGGL(k_heads, dim3((batch + 3) / 4), dim3(256), 0, (hipStream_t)stream, x, hw, hb, glob, pcat,
                      vcat, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// ---- the whole head: 1x1 convs, linear layers, softmax, tanh ----------------
+//
+// model.py:336-357 after the tower, plus ModelManager.predict's softmax
+// (model.py:100-104), for the default head shapes (2 + 1 head filters, 143
+// actions, 256 hidden units, 42 globals): one launch instead of hz_heads,
+// three GEMMs and five elementwise passes (38 us against 86-98 us at batch
+// 4096, tools/conv_bench.py).  kHS = 8 states per 256-thread workgroup:
+//   1. wave w computes the 1x1 convs of states w and w + 4 (lane = cell, as
+//      k_heads) into LDS, state-minor: pin[112][8] (policy 70 || glob 42),
+//      vin[77][8] (value 35 || glob 42);
+//   2. thread a < 143 computes logit a of the 8 states (wpT[j][a]: the
+//      threads' weight loads are coalesced; the inputs are LDS broadcasts);
+//   3. thread h computes hidden unit h of the 8 states, relu, times w2[h];
+//      the 256 products are summed per state (wave reduction + 4 partials);
+//   4. wave w applies the softmax to states w and w + 4.
+// Phase stamps (tools/head_phases.py): ~30 k cycles for the 1x1 convs (the
+// 73 MB read of the tower output), ~23 k for the policy layer, ~18 k for the
+// value layer: every workgroup reads all 143 KB of the linear weights from
+// L2 (73 MB in total, as much as the activations; 16 states per workgroup
+// would halve that but spills).
+// fp32 throughout; the sums run in a different order than hipBLASLt's, so
+// results agree with the PyTorch layers to fp32 rounding.
+namespace {
+
+constexpr int kHS = 8, kAct = 143, kHid = 256, kGlob = 42, kPIn = 70 + kGlob, kVIn = 35 + kGlob;
+
+#ifdef HZ_NET_DIAG  // phase stamps of wave 0 (tools/head_phases.py)
+#define HZ_HSTAMP(k)                                                                  \
+  if (t == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][0][k] = __builtin_amdgcn_s_memtime();
+#define HZ_HSTAMP_RT(k)                                                               \
+  if (t == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][0][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define HZ_HSTAMP(k)
+#define HZ_HSTAMP_RT(k)
+#endif
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// out[s] = sum_j w[j * ld + col] * in[j][s] over the kHS states, as NB blocks
+// of J / NB rows.  A workgroup visits the blocks starting from block
+// blockIdx % NB: the workgroups, which all run at once, then read different
+// weight rows at a time rather than all queueing on the same L2 lines (all
+// starting at row 0 made the policy layer 57 k cycles).  The block partials
+// are added in block order, so the result does not depend on the workgroup.
+template <int J, int NB>
+__device__ __forceinline__ void fcn(const float *__restrict__ w, int ld, int col, const float4 (*in)[kHS / 4],
+                                    float (&out)[kHS]) {
+  static_assert(J % NB == 0, "whole blocks");
+  constexpr int JB = J / NB;
+  float part[NB][kHS];
+  const int r0 = blockIdx.x % NB;
+  for (int bi = 0; bi < NB; bi++) {
+    int blk = r0 + bi;
+    blk -= blk >= NB ? NB : 0;
+    const float *wb = w + blk * JB * ld + col;
+    const float4(*ib)[kHS / 4] = in + blk * JB;
+    float p[kHS] = {};
+#pragma unroll
+    for (int j = 0; j < JB; j++) {  // the block's weight loads all in flight
+      const float wv = wb[j * ld];
+#pragma unroll
+      for (int q = 0; q < kHS / 4; q++) {
+        const float4 v = ib[j][q];
+        p[4 * q] += wv * v.x, p[4 * q + 1] += wv * v.y, p[4 * q + 2] += wv * v.z, p[4 * q + 3] += wv * v.w;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int s = 0; s < kHS; s++) part[b][s] = b == blk ? p[s] : part[b][s];
+  }
+#pragma unroll
+  for (int s = 0; s < kHS; s++) {
+    float o = part[0][s];
+#pragma unroll
+    for (int b = 1; b < NB; b++) o += part[b][s];
+    out[s] = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, const float *__restrict__ glob,
+                                                  const float *__restrict__ hw, const float *__restrict__ hb,
+                                                  const float *__restrict__ wpT, const float *__restrict__ bp,
+                                                  const float *__restrict__ w1T, const float *__restrict__ b1,
+                                                  const float *__restrict__ w2, const float *__restrict__ b2,
+                                                  float *__restrict__ logits, float *__restrict__ probs,
+                                                  float *__restrict__ value, int32_t batch,
+                                                  const int32_t *__restrict__ live) {
+  __shared__ float4 w4[3][32];
+  __shared__ float4 pin[kPIn][kHS / 4];
+  __shared__ float4 vin[kVIn][kHS / 4];
+  __shared__ float lg[kHS][kAct + 1];
+  __shared__ float vpart[4][kHS];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (live) batch = *live < batch ? *live : batch;
+  const int s0 = blockIdx.x * kHS;
+  if (s0 >= batch) return;
+  const int ns = batch - s0 < kHS ? batch - s0 : kHS;
+  HZ_HSTAMP(0)
+  HZ_HSTAMP_RT(8)
+  if (t < 96) w4[t >> 5][t & 31] = ((const float4 *)hw)[t];
+  for (int i = t; i < kHS * kGlob; i += 256) {
+    const int sl = i / kGlob, g = i - kGlob * sl;
+    const float v = glob[(size_t)(s0 + (sl < ns ? sl : ns - 1)) * kGlob + g];
+    ((float *)pin[70 + g])[sl] = v;
+    ((float *)vin[35 + g])[sl] = v;
+  }
+  __syncthreads();
+  HZ_HSTAMP(1)
+
+  // 1. heads' 1x1 convs (rows past the batch reread its last state)
+#pragma unroll
+  for (int pr = 0; pr < kHS / 8; pr++) {
+    if (lane >= 35) break;
+    const int sa = w + 8 * pr, sb = sa + 4;
+    const float4 *xa = (const float4 *)(x + ((size_t)(s0 + (sa < ns ? sa : ns - 1)) * 35 + lane) * 128);
+    const float4 *xb = (const float4 *)(x + ((size_t)(s0 + (sb < ns ? sb : ns - 1)) * 35 + lane) * 128);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 32; k++) {
+      const float4 u = xa[k], v = xb[k], p = w4[0][k], q = w4[1][k], r = w4[2][k];
+      a0 += u.x * p.x + u.y * p.y + u.z * p.z + u.w * p.w;
+      a1 += u.x * q.x + u.y * q.y + u.z * q.z + u.w * q.w;
+      a2 += u.x * r.x + u.y * r.y + u.z * r.z + u.w * r.w;
+      c0 += v.x * p.x + v.y * p.y + v.z * p.z + v.w * p.w;
+      c1 += v.x * q.x + v.y * q.y + v.z * q.z + v.w * q.w;
+      c2 += v.x * r.x + v.y * r.y + v.z * r.z + v.w * r.w;
+    }
+    const float h0 = hb[0], h1 = hb[1], h2 = hb[2];
+    a0 += h0, a1 += h1, a2 += h2, c0 += h0, c1 += h1, c2 += h2;
+    ((float *)pin[lane])[sa] = a0 > 0.f ? a0 : 0.f;
+    ((float *)pin[35 + lane])[sa] = a1 > 0.f ? a1 : 0.f;
+    ((float *)vin[lane])[sa] = a2 > 0.f ? a2 : 0.f;
+    ((float *)pin[lane])[sb] = c0 > 0.f ? c0 : 0.f;
+    ((float *)pin[35 + lane])[sb] = c1 > 0.f ? c1 : 0.f;
+    ((float *)vin[lane])[sb] = c2 > 0.f ? c2 : 0.f;
+  }
+  __syncthreads();
+  HZ_HSTAMP(2)
+
+  // 2. policy logits
+  if (t < kAct) {
+    float acc[kHS];
+    fcn<kPIn, 8>(wpT, kAct, t, pin, acc);
+    const float bb = bp[t];
+#pragma unroll
+    for (int s = 0; s < kHS; s++) lg[s][t] = acc[s] + bb;
+  }
+  HZ_HSTAMP(3)
+
+  // 3. value: hidden unit t, relu, times w2[t], summed over the units
+  {
+    float acc[kHS];
+    fcn<kVIn, 7>(w1T, kHid, t, vin, acc);
+    const float bb = b1[t], wo = w2[t];
+#pragma unroll
+    for (int s = 0; s < kHS; s++) {
+      float hv = acc[s] + bb;
+      hv = hv > 0.f ? hv : 0.f;
+      const float c = wave_sum(hv * wo);
+      if (lane == 0) vpart[w][s] = c;
+    }
+  }
+  __syncthreads();
+  HZ_HSTAMP(4)
+  if (t < ns) value[s0 + t] = tanhf(((vpart[0][t] + vpart[1][t]) + (vpart[2][t] + vpart[3][t])) + b2[0]);
+
+  // 4. softmax over all 143 logits (model.py:104: no legality mask)
+#pragma unroll
+  for (int k = 0; k < kHS / 4; k++) {
+    const int sl = w + 4 * k;
+    if (sl >= ns) break;
+    const bool has2 = lane + 128 < kAct;
+    const float l0 = lg[sl][lane], l1 = lg[sl][lane + 64], l2 = has2 ? lg[sl][lane + 128] : -INFINITY;
+    const size_t o = (size_t)(s0 + sl) * kAct;
+    if (logits) {
+      logits[o + lane] = l0;
+      logits[o + lane + 64] = l1;
+      if (has2) logits[o + lane + 128] = l2;
+    }
+    if (probs) {
+      const float m = wave_max(fmaxf(fmaxf(l0, l1), l2));
+      const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = has2 ? expf(l2 - m) : 0.f;
+      const float inv = 1.f / wave_sum((e0 + e1) + e2);
+      probs[o + lane] = e0 * inv;
+      probs[o + lane + 64] = e1 * inv;
+      if (has2) probs[o + lane + 128] = e2 * inv;
+    }
+  }
+  HZ_HSTAMP(5)
+  HZ_HSTAMP_RT(9)
+}
+#undef HZ_HSTAMP
+#undef HZ_HSTAMP_RT
+
+}  // namespace
+
+extern "C" int hz_heads_fc(const float *x, const float *glob, const float *hw, const float *hb, const float *wpT,
+                           const float *bp, const float *w1T, const float *b1, const float *w2, const float *b2,
+                           float *logits, float *probs, float *value, int32_t batch, const int32_t *live,
+                           void *stream) {
+  if (!x || !glob || !hw || !hb || !wpT || !bp || !w1T || !b1 || !w2 || !b2 || !value || batch < 0) return -1;
+  if (((uintptr_t)x | (uintptr_t)hw) & 15) return -1;
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(k_heads_fc, dim3((batch + kHS - 1) / kHS), dim3(256), 0, (hipStream_t)stream, x, glob, hw,
+                     hb, wpT, bp, w1T, b1, w2, b2, logits, probs, value, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -57,6 +57,7 @@ _SIGS = {
     "hz_bias_act": ([_vp, _vp, _vp, _c.c_int64, _c.c_int32, _vp], _c.c_int),
     "hz_conv3x3_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_heads": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_heads_fc": ([_vp] * 13 + [_c.c_int32, _vp, _vp], _c.c_int),
     "hz_conv3x3_x6_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_stem3x3_x6_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_stem3x3_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),

@@ -102,11 +102,19 @@ def _conv3x3_x6_act(x, wpack6, b, res=None, live=None):
 
 
 def pack_stem_x6(w):
-    """Stem weights [128][38][3][3] with the input channels zero-padded to 64,
-    packed like pack_conv3x3_x6 (hz_stem3x3_x6_bias_act's layout)."""
+    """Stem weights [128][38][3][3] packed like pack_conv3x3_x6
+    (hz_stem3x3_x6_bias_act's layout) over 64 input slots: channels 0-37,
+    then channel 37's weights again in slots 38 and 39, where the kernel
+    stages the phase channel's bf16 pieces m and l; slot 38 keeps the planes
+    (h, m), slot 39 only h, so each piece meets the weight pieces of the
+    six-product split; slots 40-63 are zero."""
     w64 = torch.zeros(w.shape[0], 64, 3, 3, dtype=w.dtype, device=w.device)
     w64[:, :w.shape[1]] = w
-    return pack_conv3x3_x6(w64)
+    w64[:, 38] = w64[:, 39] = w[:, 37]
+    p = pack_conv3x3_x6(w64)                             # [tap][q][plane][co][32]
+    p[:, 1, 2, :, 6] = 0                                 # slot 38: planes h, m
+    p[:, 1, 1:, :, 7] = 0                                # slot 39: plane h
+    return p
 
 
 def _stem_x6_act(board, wpack6, b, live=None):
@@ -155,6 +163,26 @@ def _heads(x, glob, hw, hb, live=None):
     return pcat, vcat
 
 
+def _heads_fc(x, glob, hw, hb, fc, live=None, logits=True, probs=False):
+    """The whole head in one HIP launch (hz_heads_fc): -> (logits [B,143] or
+    None, softmax probabilities [B,143] or None, value [B])."""
+    B = x.shape[0]
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_heads_fc needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    glob = glob.to(torch.float32).contiguous()
+    lo = torch.empty(B, 143, dtype=torch.float32, device=x.device) if logits else None
+    pr = torch.empty(B, 143, dtype=torch.float32, device=x.device) if probs else None
+    v = torch.empty(B, dtype=torch.float32, device=x.device)
+    ptr = (lambda t: t.data_ptr() if t is not None else None)
+    rc = lib().hz_heads_fc(x.data_ptr(), glob.data_ptr(), hw.data_ptr(), hb.data_ptr(),
+                           *(t.data_ptr() for t in fc), ptr(lo), ptr(pr), v.data_ptr(), B, _live_ptr(live),
+                           torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_heads_fc failed ({rc})")
+    return lo, pr, v
+
+
 def _bias_act(x, b, res=None):
     """x = relu(x + b[c] (+ res)) in place over an NHWC activation."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)):
@@ -191,12 +219,13 @@ class FoldedNet(nn.Module):
     # the f32 MFMA (hz_stem3x3_bias_act, hz_conv3x3_bias_act)
     TOWER_MFMA = ("x6", "f32")
 
-    def __init__(self, net, epilogue=None, native_conv=True, tower="x6"):
+    def __init__(self, net, epilogue=None, native_conv=True, tower="x6", fused_head=True):
         super().__init__()
         if tower not in self.TOWER_MFMA:
             raise ValueError(f"tower must be one of {self.TOWER_MFMA}")
         self.src = net
         self.tower = tower
+        self.fused_head = fused_head
         self.epilogue = epilogue or _bias_act
         self.native_conv = native_conv and epilogue is None
         self.refresh()
@@ -228,11 +257,28 @@ class FoldedNet(nn.Module):
                 and n.policy_fc.in_features == 112 and n.value_fc1.in_features == 77):
             self.heads = (torch.cat((self.pconv[0].reshape(2, 128), self.vconv[0].reshape(1, 128))).contiguous(),
                           torch.cat((self.pconv[1], self.vconv[1])).contiguous())
+        # ... and, for the default linear shapes, the linear layers, softmax and
+        # tanh too (hz_heads_fc: weights transposed so its loads coalesce)
+        self.fc = None
+        if (self.heads is not None and self.fused_head and n.policy_fc.out_features == 143
+                and n.value_fc1.out_features == 256 and n.value_fc2.out_features == 1):
+            self.fc = (self.pfc[0].t().contiguous(), self.pfc[1].contiguous(), self.vfc1[0].t().contiguous(),
+                       self.vfc1[1].contiguous(), self.vfc2[0].reshape(-1).contiguous(),
+                       self.vfc2[1].contiguous())
 
     @torch.no_grad()
     def forward(self, board, glob, live=None):
         """live (CUDA int32 [1], optional): only rows < live[0] are needed;
         the HIP kernels skip the others (their outputs are unspecified)."""
+        return self._run(board, glob, live, probs=False)
+
+    @torch.no_grad()
+    def predict(self, board, glob, live=None):
+        """ModelManager.predict for a batch (model.py:100-104): (softmax over
+        all 143 logits [B,143], value [B])."""
+        return self._run(board, glob, live, probs=True)
+
+    def _run(self, board, glob, live, probs):
         ep = self.epilogue
         w, b = self.stem
         if self.stem_packed is None or self.packed is None:
@@ -250,16 +296,20 @@ class FoldedNet(nn.Module):
             for (w1, b1), (w2, b2) in self.blocks:
                 y = ep(F.conv2d(x, w1, None, padding=1), b1)
                 x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
+        if self.fc is not None:
+            lo, pr, v = _heads_fc(x, glob, *self.heads, self.fc, live=live, logits=not probs, probs=probs)
+            return (pr, v) if probs else (lo, v.unsqueeze(1))
         if self.heads is not None:
             pcat, vcat = _heads(x, glob, *self.heads, live=live)
             logits = F.linear(pcat, *self.pfc)
             v = F.linear(vcat, *self.vfc1).relu_()
-            return logits, torch.tanh(F.linear(v, *self.vfc2))
-        w, b = self.pconv
-        p = F.conv2d(x, w, b).relu_().flatten(1)               # NCHW order, as model.py flattens
-        logits = F.linear(torch.cat((p, glob), 1), *self.pfc)
-        w, b = self.vconv
-        v = F.conv2d(x, w, b).relu_().flatten(1)
-        v = F.linear(torch.cat((v, glob), 1), *self.vfc1).relu_()
-        v = torch.tanh(F.linear(v, *self.vfc2))
-        return logits, v
+            v = torch.tanh(F.linear(v, *self.vfc2))
+        else:
+            w, b = self.pconv
+            p = F.conv2d(x, w, b).relu_().flatten(1)               # NCHW order, as model.py flattens
+            logits = F.linear(torch.cat((p, glob), 1), *self.pfc)
+            w, b = self.vconv
+            v = F.conv2d(x, w, b).relu_().flatten(1)
+            v = F.linear(torch.cat((v, glob), 1), *self.vfc1).relu_()
+            v = torch.tanh(F.linear(v, *self.vfc2))
+        return (torch.softmax(logits, 1), v.reshape(-1)) if probs else (logits, v)

@@ -200,7 +200,7 @@ class BatchedPredictor:
             with torch.autocast(device_type="cuda", dtype=self.dtype):
                 logits, value = self.model(board, glob)
         elif self.fast is not None:
-            logits, value = self.fast(board, glob, live=count)
+            return self.fast.predict(board, glob, live=count)
         else:
             logits, value = self.model(board, glob)
         return torch.softmax(logits.float(), dim=1), value.float().reshape(-1)

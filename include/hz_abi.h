@@ -240,6 +240,16 @@ int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *
  * x NHWC [batch][5][7][128] (16-byte aligned), hw [3][128], hb [3]. */
 int hz_heads(const float *x, const float *hw, const float *hb, const float *glob, float *pcat, float *vcat,
              int32_t batch, const int32_t *live, void *stream);
+/* The whole head for the default shapes (2 + 1 head filters, 143 actions,
+ * 256 hidden units, 42 globals): the 1x1 convs as hz_heads, then
+ * logits = pcat . wpT + bp (model.py:341-344; wpT = policy_fc.weight^T
+ * [112][143]), value = tanh(w2 . relu(vcat . w1T + b1) + b2) (model.py:352-355;
+ * w1T [77][256], w2 [256], b2 [1]) and ModelManager.predict's softmax
+ * (model.py:100-104).  logits [batch][143] and probs [batch][143] are
+ * optional (NULL: not written); value [batch]. */
+int hz_heads_fc(const float *x, const float *glob, const float *hw, const float *hb, const float *wpT,
+                const float *bp, const float *w1T, const float *b1, const float *w2, const float *b2, float *logits,
+                float *probs, float *value, int32_t batch, const int32_t *live, void *stream);
 
 /* ---- build info ---------------------------------------------------------- */
 const char *hz_version(void);

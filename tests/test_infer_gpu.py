@@ -26,6 +26,7 @@ def test_folded_gpu_matches_cpu_reference():
     fnet = FoldedNet(gnet)
     # the default net must take the native kernels, not the MIOpen fallback
     assert fnet.stem_packed is not None and fnet.packed is not None and fnet.heads is not None
+    assert fnet.fc is not None
     l1, v1 = fnet(board.cuda(), glob.cuda())
     assert (l1.cpu() - l0).abs().max().item() <= 2e-3
     assert (v1.cpu() - v0).abs().max().item() <= 2e-3
@@ -279,3 +280,77 @@ def test_stem_exact_on_integer_data(batch, kind):
     got = _stem_act(board.cuda(), pack_stem(w).cuda(), b.cuda())
     assert got.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(got.cpu(), want)
+
+
+@pytest.mark.parametrize("batch", [1, 7, 300, 4096])
+def test_fused_head_matches_layers(batch):
+    """hz_heads_fc (1x1 convs, both linear layers, softmax, tanh in one launch)
+    against hz_heads + the PyTorch linear layers + torch.softmax / tanh on
+    the same tower output, random BatchNorm statistics: within fp32
+    summation-order rounding; with a live-row bound, the live rows match."""
+    from hzamd.infer import _heads_fc
+    g = torch.Generator().manual_seed(40 + batch)
+    torch.manual_seed(batch)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    net = net.cuda()
+    fused, split = FoldedNet(net), FoldedNet(net, fused_head=False)
+    assert fused.fc is not None and split.fc is None
+    cl = torch.channels_last
+    x = torch.randn(batch, 128, 5, 7, generator=g).relu().cuda().contiguous(memory_format=cl)
+    glob = torch.rand(batch, 42, generator=g).cuda()
+    with torch.no_grad():
+        pcat = torch.cat((torch.nn.functional.conv2d(x, *split.pconv).relu().flatten(1), glob), 1)
+        vcat = torch.cat((torch.nn.functional.conv2d(x, *split.vconv).relu().flatten(1), glob), 1)
+        l0 = torch.nn.functional.linear(pcat, *split.pfc)
+        v0 = torch.tanh(torch.nn.functional.linear(torch.nn.functional.linear(vcat, *split.vfc1).relu(),
+                                                   *split.vfc2)).reshape(-1)
+    lo, pr, v = _heads_fc(x, glob, *fused.heads, fused.fc, logits=True, probs=True)
+    assert (lo - l0).abs().max().item() <= 2e-5 * max(1.0, l0.abs().max().item())
+    assert (pr - torch.softmax(l0, 1)).abs().max().item() <= 1e-6
+    assert (v - v0).abs().max().item() <= 2e-6
+    assert torch.allclose(pr.sum(1), torch.ones(batch, device="cuda"), atol=1e-5)
+    k = max(1, batch // 2 - 3)
+    live = torch.tensor([k], dtype=torch.int32, device="cuda")
+    lo2, pr2, v2 = _heads_fc(x, glob, *fused.heads, fused.fc, live=live, logits=True, probs=True)
+    assert torch.equal(lo2[:k], lo[:k]) and torch.equal(pr2[:k], pr[:k]) and torch.equal(v2[:k], v[:k])
+    # the folded forward and predict give the same numbers through either head
+    board = (torch.rand(batch, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    lf, vf = fused(board, glob)
+    ls, vs = split(board, glob)
+    assert vf.shape == vs.shape == (batch, 1)
+    assert (lf - ls).abs().max().item() <= 2e-5 * max(1.0, ls.abs().max().item())
+    assert (vf - vs).abs().max().item() <= 2e-6
+    pf, vpf = fused.predict(board, glob)
+    assert (pf - torch.softmax(ls, 1)).abs().max().item() <= 1e-6 and vpf.shape == (batch,)
+
+
+def test_stem_x6_encoder_boards_take_exact_path():
+    """Real encoder boards (channels 0-36 in {0, 1}, the phase channel 37 in
+    {0, 1/3, 2/3}): every staged value is a bf16 value once channel 37 is
+    staged as its three pieces, so the stem issues only the h plane's
+    products; the result must still carry all six products of channel 37's
+    split: error vs a float64 conv at the f32 stem's level (a lost piece of
+    1/3 would show as ~1e-3)."""
+    from hzamd.env import BatchedEnv
+    from hzamd.infer import _stem_act, _stem_x6_act, pack_stem, pack_stem_x6
+    n = 600
+    env = BatchedEnv(n, seed_base=21, device="cuda")
+    env.reset()
+    plies = torch.arange(n, device="cuda") % 50
+    for p in range(50):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+    board, _ = env.encode()
+    env.close()
+    ph = board[:, 37].amax((1, 2))
+    assert bool(((ph - 1 / 3).abs() < 1e-6).any()) and bool(((ph - 2 / 3).abs() < 1e-6).any())
+    g = torch.Generator().manual_seed(9)
+    w = torch.randn(128, 38, 3, 3, generator=g) * 0.1
+    b = torch.randn(128, generator=g) * 0.1
+    want = _conv_ref(board.cpu(), w, b, None)
+    e32 = (_stem_act(board, pack_stem(w).cuda(), b.cuda()).cpu().double() - want).abs().max().item()
+    got = _stem_x6_act(board, pack_stem_x6(w).cuda(), b.cuda())
+    e6 = (got.cpu().double() - want).abs().max().item()
+    assert e6 <= 2 * e32 + 1e-7, (e6, e32)

@@ -80,4 +80,40 @@ for name, fn, wp in (("stem_f32", _stem_act, pack_stem(ws)), ("stem_x6", _stem_x
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 100 * 1e3
     out[name] = {"us": us, "tflops_algorithmic": sflop / (us * 1e-6) / 1e12}
+
+
+def timed(fn, reps=100):
+    for _ in range(10):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+# the stem on a board with non-bf16 values everywhere (the six-product path
+# an encoder board, all of whose staged values are bf16 values, avoids)
+board_g = board * 0.3
+wps = pack_stem_x6(ws)
+out["stem_x6_general_us"] = timed(lambda: _stem_x6_act(board_g, wps, b))
+# the head: hz_heads_fc against hz_heads + three linear layers + softmax + tanh
+from hzamd.infer import FoldedNet, _heads, _heads_fc  # noqa: E402
+from hzamd.net import HarmoniesNet  # noqa: E402
+fn = FoldedNet(HarmoniesNet().eval().cuda())
+glob = torch.rand(B, 42, device="cuda", generator=g)
+F = torch.nn.functional
+
+
+def split_head():
+    pcat, vcat = _heads(x, glob, *fn.heads)
+    lo = F.linear(pcat, *fn.pfc)
+    v = torch.tanh(F.linear(F.linear(vcat, *fn.vfc1).relu_(), *fn.vfc2))
+    return torch.softmax(lo, 1), v
+
+
+out["head_split_us"] = timed(split_head)
+out["head_fused_us"] = timed(lambda: _heads_fc(x, glob, *fn.heads, fn.fc, logits=False, probs=True))
 print(json.dumps(out))
