@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/hz_abi.h"
 
@@ -327,7 +328,7 @@ constexpr int kBoardC = 38;                           // encoder board channels 
 constexpr int kX6Zero = 512;                          // bytes of zeros after the cells
 constexpr int kX6Buf = kCS * 35 * kX6Cell + kX6Zero;  // one chunk of 8 states + the zero region
 static_assert(kCS * 35 * kX6Cell % 256 == 0 && kX6Buf % 256 == 0, "zero region and buffers 256-B aligned");
-constexpr int kX6Stage = (kRows * 8 + 511) / 512;     // float4 loads per thread per chunk (5)
+constexpr int kX6SmallMax = 768;                      // batches up to this run one state per workgroup
 
 __device__ __forceinline__ uint32_t bf16_bits(float v) {
   return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)v);
@@ -352,34 +353,47 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
 // NQ chunks of 32 input channels.  Stem: x is the encoder's NCHW board
 // [B][38][5][7] (channels >= 38 stage as zeros; NQ = 2), else an NHWC
 // [B][5][7][128] activation (NQ = 4).
-template <int NQ, bool Stem>
-__global__ void __launch_bounds__(512, 1)
+// CS states per workgroup: 8 (8 waves: row half x 32 output channels, 9 row
+// blocks each), or 1 for small batches (4 waves: 32 output channels, the
+// state's 35 rows as 3 row blocks): a workgroup's time is its waves' MFMA
+// chain (8 states: ~175 k cycles, ~73 us, however few states are live), and
+// the arena's batches of a few dozen boards fill only a few CUs; one state
+// per group cuts each wave's chain to a third at 48/35 rows of waste.
+template <int NQ, bool Stem, int CS>
+__global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
     k_conv3x3_x6(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                  const float *__restrict__ res, float *__restrict__ out, int32_t batch,
                  const int32_t *__restrict__ live) {
+  static_assert(CS == 8 || CS == 1, "8 or 1 states per workgroup");
+  constexpr int kRowsT = CS * 35;                  // output rows of the group
+  constexpr int kRBT = CS == 8 ? 9 : 3;            // row blocks of 16 per wave
+  constexpr int kThreads = (CS == 8 ? 2 : 1) * 256;
+  constexpr int kStg = (kRowsT * 8 + kThreads - 1) / kThreads;  // float4 staged per thread per chunk
+  constexpr int kZero = (CS * 35 * kX6Cell + 255) / 256 * 256;   // zero region: 256-B aligned (banks)
+  constexpr int kBufT = kZero + kX6Zero;                          // one chunk's buffer + zero region
+  static_assert((kThreads / 256) * kRBT * 16 >= kRowsT, "row blocks cover the rows");
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
-  const int s0 = blockIdx.x * kCS;
+  const int s0 = blockIdx.x * CS;
   if (live) batch = *live < batch ? *live : batch;  // rows past the live count are not computed
   if (s0 >= batch) return;
-  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
-  constexpr int kZero = kCS * 35 * kX6Cell;  // byte offset of the zero region in each buffer
+  const int ns = batch - s0 < CS ? batch - s0 : CS;
   HZ_STAMP(0)
   HZ_STAMP_RT(8)
 
   if (t < 2 * kX6Zero / 16) {  // both buffers' zero regions
     const int b = t / (kX6Zero / 16), k = t - b * (kX6Zero / 16);
-    *(float4 *)(lds + b * kX6Buf + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4 *)(lds + b * kBufT + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
   // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..)
-  f32x4 stg[kX6Stage];
-  int gsrc[kX6Stage], ldst[kX6Stage];
+  f32x4 stg[kStg];
+  int gsrc[kStg], ldst[kStg];
 #pragma unroll
-  for (int it = 0; it < kX6Stage; it++) {
-    int f = it * 512 + t;
-    f = f < kRows * 8 ? f : kRows * 8 - 1;
+  for (int it = 0; it < kStg; it++) {
+    int f = it * kThreads + t;
+    f = f < kRowsT * 8 ? f : kRowsT * 8 - 1;
     const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
     if constexpr (Stem)  // board element (state, channel 4 part, cell); channel offset added per chunk
       gsrc[it] = (s < ns ? s0 + s : s0 + ns - 1) * (kBoardC * 35) + 4 * part * 35 + cell;
@@ -398,8 +412,8 @@ __global__ void __launch_bounds__(512, 1)
   // Slots past 39 stage as zeros.
   auto stem_load = [&](int it, int q) -> f32x4 {
     f32x4 v;
-    int f = it * 512 + t;
-    f = f < kRows * 8 ? f : kRows * 8 - 1;
+    int f = it * kThreads + t;
+    f = f < kRowsT * 8 ? f : kRowsT * 8 - 1;
     const int c0 = 32 * q + 4 * (f & 7);
     if (c0 == 36) {
       v[0] = x[gsrc[it] + (32 * q) * 35];
@@ -418,23 +432,26 @@ __global__ void __launch_bounds__(512, 1)
 #define HZ_X6_LOAD(q)                                                                     \
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                        \
   if constexpr (Stem) {                                                                   \
-    _Pragma("unroll") for (int it = 0; it < kX6Stage; it++) stg[it] = stem_load(it, q);   \
+    _Pragma("unroll") for (int it = 0; it < kStg; it++) stg[it] = stem_load(it, q);       \
   } else {                                                                                \
-    _Pragma("unroll") for (int it = 0; it < kX6Stage; it++)                               \
+    _Pragma("unroll") for (int it = 0; it < kStg; it++)                                   \
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(x + gsrc[it] + 32 * (q))); \
   }
   // the wait names the staged registers, so the split's arithmetic (which,
   // unlike an LDS store, could move above a plain asm statement) waits too
-  static_assert(kX6Stage == 5, "HZ_X6_STORE ties five staging registers");
+  static_assert(kStg == 5 || kStg == 2, "HZ_X6_STORE ties five or two staging registers");
 #define HZ_X6_STORE(buf)                                                                  \
-  asm volatile("s_waitcnt vmcnt(0)"                                                       \
-               : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4])      \
-               :                                                                          \
-               : "memory");                                                               \
-  _Pragma("unroll") for (int it = 0; it < kX6Stage; it++) {                               \
+  if constexpr (kStg == 5)                                                                \
+    asm volatile("s_waitcnt vmcnt(0)"                                                     \
+                 : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4])    \
+                 :                                                                        \
+                 : "memory");                                                             \
+  else                                                                                    \
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[0]), "+v"(stg[1]) : : "memory");         \
+  _Pragma("unroll") for (int it = 0; it < kStg; it++) {                                   \
     uint2 h_, m_, l_;                                                                     \
     split4(stg[it], h_, m_, l_);                                                          \
-    char *d_ = lds + (buf) * kX6Buf + ldst[it];                                           \
+    char *d_ = lds + (buf) * kBufT + ldst[it];                                            \
     *(uint2 *)d_ = h_;                                                                    \
     *(uint2 *)(d_ + 64) = m_;                                                             \
     *(uint2 *)(d_ + 128) = l_;                                                            \
@@ -456,12 +473,12 @@ __global__ void __launch_bounds__(512, 1)
   // or, off the board, the zero region at the same offset mod 256 (so the
   // lane keeps the LDS banks its row would use).
   // valid[rb] bit tap = the neighbour is on the board.
-  int cbase[kRB];
-  uint32_t valid[kRB];
+  int cbase[kRBT];
+  uint32_t valid[kRBT];
 #pragma unroll
-  for (int rb = 0; rb < kRB; rb++) {
-    int r = (rh * kRB + rb) * 16 + (lane & 15);
-    r = r < kRows ? r : kRows - 1;
+  for (int rb = 0; rb < kRBT; rb++) {
+    int r = (rh * kRBT + rb) * 16 + (lane & 15);
+    r = r < kRowsT ? r : kRowsT - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
     cbase[rb] = r * kX6Cell + 16 * kg;
     uint32_t v = 0;
@@ -478,9 +495,9 @@ __global__ void __launch_bounds__(512, 1)
     return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
   };
 
-  f32x4 acc[kRB][2];
+  f32x4 acc[kRBT][2];
 #pragma unroll
-  for (int rb = 0; rb < kRB; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
+  for (int rb = 0; rb < kRBT; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
 
   const int co0 = 32 * (w & 3) + (lane & 15);
   // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
@@ -510,7 +527,7 @@ __global__ void __launch_bounds__(512, 1)
   {
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
-      const char *lb = lds + (q & 1) * kX6Buf;
+      const char *lb = lds + (q & 1) * kBufT;
       if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
       for (int tap = 0; tap < 9; tap++) {
         const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
@@ -523,15 +540,15 @@ __global__ void __launch_bounds__(512, 1)
   #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
           if (pa >= npa) break;
-          bf16x8 a[kRB];
+          bf16x8 a[kRBT];
   #pragma unroll
-          for (int rb = 0; rb < kRB; rb++)
+          for (int rb = 0; rb < kRBT; rb++)
             a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
   #pragma unroll
           for (int pb = 0; pb < 3 - pa; pb++) {
             const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
   #pragma unroll
-            for (int rb = 0; rb < kRB; rb++) {
+            for (int rb = 0; rb < kRBT; rb++) {
               acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
               acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
             }
@@ -556,10 +573,10 @@ __global__ void __launch_bounds__(512, 1)
   float *ob = out + (size_t)s0 * 35 * 128 + co0;
   const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co0 : nullptr;
   const int nrow = ns * 35;
-  float rv[kRB][2][4];
+  float rv[kRBT][2][4];
 #pragma unroll
-  for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+  for (int rb = 0; rb < kRBT; rb++) {
+    const int rbase = (rh * kRBT + rb) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const bool ok = rbase + j < nrow;
@@ -568,8 +585,8 @@ __global__ void __launch_bounds__(512, 1)
     }
   }
 #pragma unroll
-  for (int rb = 0; rb < kRB; rb++) {
-    const int rbase = (rh * kRB + rb) * 16 + 4 * kg;
+  for (int rb = 0; rb < kRBT; rb++) {
+    const int rbase = (rh * kRBT + rb) * 16 + 4 * kg;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (rbase + j < nrow) {
@@ -594,22 +611,39 @@ __global__ void __launch_bounds__(512, 1)
 
 }  // namespace
 
-template <int NQ, bool Stem>
-static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
-                     int32_t batch, const int32_t *live, void *stream) {
+template <int NQ, bool Stem, int CS>
+static int launch_x6_cs(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
+                        int32_t batch, const int32_t *live, void *stream) {
   static std::atomic<uint64_t> init_mask{0};
-  const size_t lds = 2 * (size_t)kX6Buf;
+  const size_t lds = 2 * (size_t)((CS * 35 * kX6Cell + 255) / 256 * 256 + kX6Zero);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3_x6<NQ, Stem>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6<NQ, Stem, CS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
-  hipLaunchKernelGGL((k_conv3x3_x6<NQ, Stem>), dim3((batch + kCS - 1) / kCS), dim3(512), lds, (hipStream_t)stream,
-                     x, (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  hipLaunchKernelGGL((k_conv3x3_x6<NQ, Stem, CS>), dim3((batch + CS - 1) / CS), dim3(CS == 8 ? 512 : 256), lds,
+                     (hipStream_t)stream, x, (const bf16x8 *)wpack6, bias, res, out, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// batches of at most this many rows (the buffer's, known on the host) run
+// one state per workgroup; HZ_X6_SMALL_MAX overrides it (tools/conv_bench.py)
+static int32_t x6_small_max() {
+  static const int32_t v = [] {
+    const char *e = getenv("HZ_X6_SMALL_MAX");
+    return e ? (int32_t)atoi(e) : (int32_t)kX6SmallMax;
+  }();
+  return v;
+}
+
+template <int NQ, bool Stem>
+static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
+                     int32_t batch, const int32_t *live, void *stream) {
+  return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1>(x, wpack6, bias, res, out, batch, live, stream)
+                                 : launch_x6_cs<NQ, Stem, 8>(x, wpack6, bias, res, out, batch, live, stream);
 }
 
 extern "C" int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res,

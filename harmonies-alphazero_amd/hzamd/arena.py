@@ -35,8 +35,11 @@ class MctsAgent:
     """get_best_action_and_pi with an evaluator (e.g. BatchedPredictor(model))
     and an evaluation config (deterministic: testing=True, no noise)."""
 
-    def __init__(self, evaluator, mcts_config=None, exact_keys=False):
+    def __init__(self, evaluator, mcts_config=None, exact_keys=False, graph=True):
         self.evaluator = evaluator
+        # device-row evaluators replay each search's simulation as a HIP graph
+        # (BatchedMCTS.search(graph=True)): the arena's batches are launch-bound
+        self.graph = graph
         self.cfg = dict(MCTS_EVAL, **(mcts_config or {}))
         if not self.cfg.get("testing", False) or self.cfg.get("dirichlet_epsilon", 0) != 0:
             raise ValueError("arena MctsAgent plays the deterministic evaluation search (testing=True, eps=0)")
@@ -46,7 +49,8 @@ class MctsAgent:
     def _search(self, env, mask, evaluator):
         if self.mcts is None or self.mcts.env is not env:
             self.mcts = BatchedMCTS(env, self.cfg["num_simulations"], exact_keys=self.exact_keys)
-        v = self.mcts.search(evaluator, self.cfg["cpuct"], active=mask, noise=None, eps=0.0, testing=True)
+        v = self.mcts.search(evaluator, self.cfg["cpuct"], active=mask, noise=None, eps=0.0, testing=True,
+                             graph=self.graph and env.device.type == "cuda")
         zeros = torch.zeros(env.n, dtype=torch.bool, device=env.device)
         return choose_actions(v, zeros, torch.zeros(env.n, dtype=torch.float64, device=env.device))
 
@@ -69,6 +73,7 @@ class _Routed:
     def __init__(self, eval_a, eval_b, a_rows):
         self.eval_a, self.eval_b, self.a_rows = eval_a, eval_b, a_rows
         self.both_device = bool(getattr(eval_a, "device_rows", False) and getattr(eval_b, "device_rows", False))
+        self.capturable = self.both_device and all(getattr(e, "capturable", False) for e in (eval_a, eval_b))
 
     def __call__(self, board, glob, rows=None, count=None):
         if rows is not None and self.both_device:

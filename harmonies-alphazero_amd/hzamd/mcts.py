@@ -107,21 +107,55 @@ class BatchedMCTS:
         return self.counts
 
     # -- one full search per board -------------------------------------------
+    def _device_step(self, evaluator, cpuct, active, noise, eps, testing):
+        """One simulation with a device-row evaluator: no host round trip."""
+        self.select(cpuct, active)
+        board, glob, rows, count = self.gather_leaves()
+        self.eval_rows += count
+        policy, value = evaluator(board, glob, rows, count)
+        self.expand_backup(policy, value, noise, eps, testing, gathered=True)
+
+    def _capture_step(self, evaluator, cpuct, active, eps, testing):
+        """One simulation captured as a HIP graph (select, gather + encode,
+        the evaluator's kernels, expand + backup): replaying it costs one
+        launch instead of ~60.  Noise is passed as NULL: the kernel reads it
+        only when it expands the root, which the first (eager) simulation does
+        (hz_mcts.hip k_expand_backup: noisy = leaf == 0 && !testing && noise)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._sync()  # the handles launch on the capture stream
+            self._device_step(evaluator, cpuct, active, None, eps, testing)
+        self._sync()
+        return g
+
     def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None,
-               gather=True):
+               gather=True, graph=False):
         """get_best_action_and_pi's simulation loop (MCTS.py:288-352) for every
         active board; returns root visit counts int32 [n, 143].
 
         gather (default): each simulation evaluates only the leaves that need
         the network (module docstring); `eval_rows` counts them on the device.
         gather=False evaluates one row per board (terminal leaves and inactive
-        boards included, their results unused), as before."""
+        boards included, their results unused), as before.
+
+        graph: simulations 2.. replay one captured HIP graph, for small,
+        launch-bound batches (the arena's few dozen boards); taken only with
+        a device-row evaluator that declares `capturable = True` (no host
+        reads, no allocations outside PyTorch's allocator), as
+        BatchedPredictor does for the folded network; otherwise ignored."""
         if active is not None:
             active = active.to(device=self.device, dtype=torch.uint8).contiguous()
         self.begin(active)
         self.eval_rows.zero_()
         device_rows = bool(getattr(evaluator, "device_rows", False))
-        for _ in range(self.num_simulations if sims is None else int(sims)):
+        total = self.num_simulations if sims is None else int(sims)
+        if graph and gather and device_rows and getattr(evaluator, "capturable", False) and total > 1:
+            self._device_step(evaluator, cpuct, active, noise, eps, testing)
+            g = self._capture_step(evaluator, cpuct, active, eps, testing)
+            for _ in range(total - 1):
+                g.replay()
+            return self.result()
+        for _ in range(total):
             self.select(cpuct, active)
             if not gather:
                 board, glob = self.encode_leaves()
@@ -184,6 +218,9 @@ class BatchedPredictor:
         if fold and hasattr(model, "residual_blocks"):
             from .infer import FoldedNet
             self.fast = FoldedNet(model)
+        # the folded fp32 path is HIP kernels + PyTorch ops only: it can be
+        # captured in a HIP graph (BatchedMCTS.search(graph=True))
+        self.capturable = self.fast is not None and (dtype is None or dtype == torch.float32)
 
     def refresh(self):
         """Re-fold after the model's weights changed."""

@@ -72,6 +72,7 @@ class _DeviceRows:
     gathered buffers with the live count left on the device."""
 
     device_rows = True
+    capturable = True  # the stub is PyTorch ops only: the arena's searches replay HIP graphs
 
     def __init__(self, fn):
         self.fn = fn
@@ -99,3 +100,43 @@ def test_mcts_vs_mcts_routed_batch_two_evaluators():
     out = check(a, b, ("mcts", "mcts_neg"), 24, 600)
     s = summarize(out)
     assert s["wins"] + s["losses"] + s["draws"] == 24
+
+
+@pytest.mark.parametrize("testing", [True, False])
+def test_graph_replayed_search_matches_eager(testing):
+    """search(graph=True): simulation 1 eager (it expands the roots, with the
+    Dirichlet noise when not testing), simulations 2.. one captured HIP graph
+    replayed.  With the real network on both sides of a routed arena batch
+    (BatchedPredictor x 2, the arena's evaluator), the visit counts, tree
+    sizes and evaluated-row count equal the eager search's."""
+    from hzamd.arena import _Routed
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, BatchedPredictor
+    from hzamd.net import HarmoniesNet
+    torch.manual_seed(0)
+    pa = BatchedPredictor(HarmoniesNet().eval().to(DEV))
+    pb = BatchedPredictor(HarmoniesNet().eval().to(DEV))
+    n = 40
+    noise = torch.distributions.Dirichlet(torch.full((69,), 0.3)).sample((n,)).double()
+    plies = torch.arange(n, device=DEV) % 30
+    out = []
+    for graph in (False, True):
+        env = BatchedEnv(n, seed_base=55, device=DEV)
+        env.reset()
+        for p in range(30):
+            mask, count = env.legal_mask()
+            act = env.rule_actions(mask, count)
+            env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+        ev = _Routed(pa, pb, (torch.arange(n, device=DEV) % 3) == 0)
+        mcts = BatchedMCTS(env, 24)
+        v = mcts.search(ev, 2.0, active=~env.done(), noise=None if testing else noise, eps=0.25,
+                        testing=testing, graph=graph).clone()
+        out.append((v.cpu(), mcts.stats().clone().cpu(), int(mcts.eval_rows.item())))
+        _, mt, idx = env.export_state(with_mt=True)
+        out[-1] += (mt.cpu(), idx.cpu())
+        mcts.close()
+        env.close()
+    (v0, c0, r0, m0, i0), (v1, c1, r1, m1, i1) = out
+    assert int(v0.sum()) > 0
+    assert torch.equal(v0, v1) and torch.equal(c0, c1) and r0 == r1
+    assert torch.equal(m0, m1) and torch.equal(i0, i1)

@@ -354,3 +354,27 @@ def test_stem_x6_encoder_boards_take_exact_path():
     got = _stem_x6_act(board, pack_stem_x6(w).cuda(), b.cuda())
     e6 = (got.cpu().double() - want).abs().max().item()
     assert e6 <= 2 * e32 + 1e-7, (e6, e32)
+
+
+def test_x6_small_batch_kernel_matches_large_batch_kernel():
+    """Batches of at most 768 rows run the one-state-per-workgroup variant of
+    the x6 conv and stem: each row's products and sums are issued in the same
+    order as in the eight-state variant, so a row's output is bit-identical
+    whichever variant computed it."""
+    from hzamd.infer import _conv3x3_x6_act, _stem_x6_act, pack_conv3x3_x6, pack_stem_x6
+    g = torch.Generator(device="cuda").manual_seed(77)
+    cl = torch.channels_last
+    big = 1100
+    x = torch.randn(big, 128, 5, 7, device="cuda", generator=g).relu().contiguous(memory_format=cl)
+    r = torch.randn(big, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=cl)
+    w = pack_conv3x3_x6(torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.03)
+    b = torch.randn(128, device="cuda", generator=g)
+    board = (torch.rand(big, 38, 5, 7, device="cuda", generator=g) > 0.8).float()
+    board[:, 37] = (torch.arange(big, device="cuda") % 4).float().view(-1, 1, 1) / 3.0
+    ws = pack_stem_x6(torch.randn(128, 38, 3, 3, device="cuda", generator=g) * 0.1)
+    full = _conv3x3_x6_act(x, w, b, r)
+    sfull = _stem_x6_act(board, ws, b)
+    for k in (1, 30, 767):
+        sub = _conv3x3_x6_act(x[:k].contiguous(memory_format=cl), w, b, r[:k].contiguous(memory_format=cl))
+        assert torch.equal(sub, full[:k]), k
+        assert torch.equal(_stem_x6_act(board[:k].contiguous(), ws, b), sfull[:k]), k

@@ -27,8 +27,10 @@ if "b" in stage:
     torch.manual_seed(1)
     a = HarmoniesNet().cuda().eval()
     b = HarmoniesNet().cuda().eval()
-    t = time.time()
-    out, _, plies = play_games(MctsAgent(BatchedPredictor(a), {"num_simulations": sims}),
-                               MctsAgent(BatchedPredictor(b), {"num_simulations": sims}), n, seed_base=10**9)
-    torch.cuda.synchronize()
-    print("nets", summarize(out), plies, f"{time.time() - t:.1f}s", flush=True)
+    for graph in (False, True):  # eager simulations, then each search's simulations replayed as a HIP graph
+        t = time.time()
+        out, _, plies = play_games(MctsAgent(BatchedPredictor(a), {"num_simulations": sims}, graph=graph),
+                                   MctsAgent(BatchedPredictor(b), {"num_simulations": sims}, graph=graph), n,
+                                   seed_base=10**9)
+        torch.cuda.synchronize()
+        print("nets", "graph" if graph else "eager", summarize(out), plies, f"{time.time() - t:.1f}s", flush=True)

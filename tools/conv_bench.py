@@ -116,4 +116,10 @@ def split_head():
 
 out["head_split_us"] = timed(split_head)
 out["head_fused_us"] = timed(lambda: _heads_fc(x, glob, *fn.heads, fn.fc, logits=False, probs=True))
+# the x6 conv at small batches (<= HZ_X6_SMALL_MAX rows: one state per workgroup)
+out["x6_small_max"] = int(os.environ.get("HZ_X6_SMALL_MAX", "768"))
+out["x6_batch_us"] = {}
+for bs in (8, 32, 64, 128, 256, 512, 768, 1024, 2048):
+    xs, rs = x[:bs].contiguous(memory_format=cl), r[:bs].contiguous(memory_format=cl)
+    out["x6_batch_us"][bs] = timed(lambda: _conv3x3_x6_act(xs, wp6, b, rs), reps=50)
 print(json.dumps(out))
