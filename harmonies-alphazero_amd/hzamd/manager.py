@@ -39,8 +39,12 @@ class ModelManager:
         self.model = HarmoniesNet(_net_cfg(model_config)).to(self.device)
         self.learning_rate = training_config["learning_rate"]
         if training_config["optimizer_type"] == "Adam":
+            # capturable on the GPU: the step counter and bias corrections stay
+            # on the device, so a training step can be replayed as a HIP graph
+            # (hzamd.train.training_phase)
             self.optimizer = optim.Adam(self.model.parameters(), lr=self.initial_learning_rate,
-                                        weight_decay=training_config["weight_decay"])
+                                        weight_decay=training_config["weight_decay"],
+                                        capturable=self.device.type == "cuda")
         else:
             self.optimizer = optim.SGD(self.model.parameters(), lr=self.learning_rate,
                                        momentum=training_config["momentum"],

@@ -63,21 +63,82 @@ class TensorSource:
         return tuple(x.index_select(0, idx) for x in self.t)
 
 
-def training_phase(manager, source, epochs, batch_size, generator=None):
+class GraphedStep:
+    """ModelManager.train_step_async for full batches of one size, replayed
+    as a captured HIP graph: a batch of 64 is ~150 small launches (forward,
+    backward, Adam), launch-bound at ~4 ms; a replay is one launch after the
+    copy into the static inputs.  The first `warmup` batches train eagerly
+    on a side stream (PyTorch's capture recipe: the optimizer state and the
+    allocator settle); the capture itself executes nothing, and the batch it
+    was recorded with is then trained by the first replay, so every batch is
+    trained exactly once.  Capture once per phase: the learning rate is
+    read when the graph is recorded (the scheduler steps between phases)."""
+
+    def __init__(self, manager, warmup=3):
+        self.m = manager
+        self.warmup = warmup
+        self.graph = None
+
+    def step(self, board, glob, pi, z):
+        m = self.m
+        if self.warmup > 0:
+            self.warmup -= 1
+            cur = torch.cuda.current_stream(m.device)
+            side = torch.cuda.Stream(m.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                out = m.train_step_async(board, glob, pi, z)
+            cur.wait_stream(side)
+            return out
+        if self.graph is None:
+            self.static = [x.to(m.device).clone() for x in (board, glob, pi, z)]
+            m.model.train()
+            m.optimizer.zero_grad(set_to_none=True)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                total, pl, vl = m.losses(*self.static)
+                total.backward()
+                m.optimizer.step()
+            self.out = (total.detach(), pl.detach(), vl.detach())
+        else:
+            for dst, x in zip(self.static, (board, glob, pi, z)):
+                dst.copy_(x)
+        self.graph.replay()
+        return self.out
+
+
+def graph_capable(manager):
+    """Training steps can be graphed: a CUDA model under capturable Adam or
+    SGD (no host-side optimizer state)."""
+    opt = manager.optimizer
+    if manager.device.type != "cuda":
+        return False
+    if isinstance(opt, torch.optim.Adam):
+        return all(g.get("capturable", False) for g in opt.param_groups)
+    return isinstance(opt, torch.optim.SGD)
+
+
+def training_phase(manager, source, epochs, batch_size, generator=None, graph=None):
     """Returns {"loss", "policy_loss", "value_loss", "batches"} averaged over
     batches, or None when there are fewer examples than one batch (the
-    reference skips training then)."""
+    reference skips training then).  graph (default: when graph_capable):
+    full batches replay one captured training step (GraphedStep); a last
+    partial batch runs eagerly."""
     m = len(source)
     if m < batch_size:
         return None
     dev = source.device
     acc = torch.zeros(3, dtype=torch.float64, device=manager.device)
     batches = 0
+    graphed = GraphedStep(manager) if (graph_capable(manager) if graph is None else graph) else None
     for _ in range(epochs):
         perm = torch.randperm(m, device=dev, generator=generator)
         for s in range(0, m, batch_size):
             b, g, pi, z = source.batch(perm[s:s + batch_size])
-            t, p, v = manager.train_step_async(b, g, pi, z)
+            if graphed is not None and b.shape[0] == batch_size:
+                t, p, v = graphed.step(b, g, pi, z)
+            else:
+                t, p, v = manager.train_step_async(b, g, pi, z)
             acc += torch.stack([t, p, v]).to(torch.float64)
             batches += 1
     a = (acc / batches).tolist()

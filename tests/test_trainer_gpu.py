@@ -65,3 +65,52 @@ def test_training_loop_end_to_end(tmp_path):
     assert len(tr2.replay_buffer) == len(tr.replay_buffer)
     hist2 = tr2.run_training_loop()
     assert [h["iteration"] for h in hist2] == [3]
+
+
+@pytest.mark.parametrize("net", ["test", "default"])
+def test_graphed_training_phase_matches_eager(net):
+    """training_phase with full batches replayed as a captured HIP graph
+    (GraphedStep: 3 eager warm-up batches, then one graph per phase) trains
+    every batch once, as the eager loop does: same batch count, losses and
+    weights equal to fp32 rounding after two epochs with a partial batch."""
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    from hzamd.train import TensorSource, graph_capable, training_phase
+    from test_manager_cpu import MODEL_CFG, TRAIN_CFG
+    mcfg = MODEL_CFG if net == "test" else dict(DEFAULT)
+    tcfg = dict(TRAIN_CFG, device="cuda:0", weight_decay=1e-4)
+    g = torch.Generator().manual_seed(3)
+    M, B = 64 * 6 + 10, 64
+    board = (torch.rand(M, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    glob = torch.rand(M, 42, generator=g).cuda()
+    pi = torch.softmax(torch.rand(M, 143, generator=g), 1).cuda()
+    z = torch.randint(-1, 2, (M,), generator=g).float().cuda()
+    out = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        mgr = ModelManager(mcfg, tcfg)
+        assert graph_capable(mgr)
+        res = training_phase(mgr, TensorSource(board, glob, pi, z), epochs=2, batch_size=B,
+                             generator=torch.Generator(device="cuda").manual_seed(5), graph=graph)
+        out.append((res, {k: v.detach().clone() for k, v in mgr.model.state_dict().items()}))
+    (r0, w0), (r1, w1) = out
+    assert r0["batches"] == r1["batches"] == 14
+    # the default net's eager training is not reproducible run to run (its
+    # backward kernels' rounding differs between runs; 14 Adam steps amplify
+    # it: tools/train_graph_check.py shows eager-vs-eager spreads as large as
+    # graph-vs-eager): losses to 2e-2 there; the small test net, which pins
+    # the mechanism (warm-up, static inputs, replay), to 1e-4 and its weights
+    tol = 1e-4 if net == "test" else 2e-2
+    for k in ("loss", "policy_loss", "value_loss"):
+        assert abs(r0[k] - r1[k]) <= tol * max(1.0, abs(r0[k])), (k, r0[k], r1[k])
+    if net != "test":
+        return
+    for k, v in w0.items():
+        if k.endswith("conv.bias") or k.endswith(("conv1.bias", "conv2.bias")):
+            # a conv bias feeding a BatchNorm has a zero gradient up to
+            # rounding, which Adam rescales to lr-sized steps: noise only
+            continue
+        if v.dtype.is_floating_point:
+            assert torch.allclose(v, w1[k], rtol=1e-3, atol=1e-5), k
+        else:
+            assert torch.equal(v, w1[k]), k
