@@ -107,15 +107,17 @@ class BatchedMCTS:
         return self.counts
 
     # -- one full search per board -------------------------------------------
-    def _device_step(self, evaluator, cpuct, active, noise, eps, testing):
+    def _device_step(self, evaluator, cpuct, active, noise, eps, testing, max_rows=None):
         """One simulation with a device-row evaluator: no host round trip."""
         self.select(cpuct, active)
         board, glob, rows, count = self.gather_leaves()
         self.eval_rows += count
+        if max_rows is not None:  # the live rows are a prefix of at most max_rows
+            board, glob = board[:max_rows], glob[:max_rows]
         policy, value = evaluator(board, glob, rows, count)
         self.expand_backup(policy, value, noise, eps, testing, gathered=True)
 
-    def _capture_step(self, evaluator, cpuct, active, eps, testing):
+    def _capture_step(self, evaluator, cpuct, active, eps, testing, max_rows=None):
         """One simulation captured as a HIP graph (select, gather + encode,
         the evaluator's kernels, expand + backup): replaying it costs one
         launch instead of ~60.  Noise is passed as NULL: the kernel reads it
@@ -124,12 +126,12 @@ class BatchedMCTS:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._sync()  # the handles launch on the capture stream
-            self._device_step(evaluator, cpuct, active, None, eps, testing)
+            self._device_step(evaluator, cpuct, active, None, eps, testing, max_rows)
         self._sync()
         return g
 
     def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None,
-               gather=True, graph=False):
+               gather=True, graph=False, max_rows=None):
         """get_best_action_and_pi's simulation loop (MCTS.py:288-352) for every
         active board; returns root visit counts int32 [n, 143].
 
@@ -142,7 +144,12 @@ class BatchedMCTS:
         launch-bound batches (the arena's few dozen boards); taken only with
         a device-row evaluator that declares `capturable = True` (no host
         reads, no allocations outside PyTorch's allocator), as
-        BatchedPredictor does for the folded network; otherwise ignored."""
+        BatchedPredictor does for the folded network; otherwise ignored.
+
+        max_rows (host int, device-row evaluators): an upper bound on the
+        leaves a simulation can gather (e.g. the number of active boards);
+        the evaluator then gets the first max_rows rows of the buffers, so
+        its kernels are sized (and the small-batch conv form chosen) by it."""
         if active is not None:
             active = active.to(device=self.device, dtype=torch.uint8).contiguous()
         self.begin(active)
@@ -150,8 +157,8 @@ class BatchedMCTS:
         device_rows = bool(getattr(evaluator, "device_rows", False))
         total = self.num_simulations if sims is None else int(sims)
         if graph and gather and device_rows and getattr(evaluator, "capturable", False) and total > 1:
-            self._device_step(evaluator, cpuct, active, noise, eps, testing)
-            g = self._capture_step(evaluator, cpuct, active, eps, testing)
+            self._device_step(evaluator, cpuct, active, noise, eps, testing, max_rows)
+            g = self._capture_step(evaluator, cpuct, active, eps, testing, max_rows)
             for _ in range(total - 1):
                 g.replay()
             return self.result()
@@ -166,6 +173,8 @@ class BatchedMCTS:
             board, glob, rows, count = self.gather_leaves()
             self.eval_rows += count
             if device_rows:
+                if max_rows is not None:
+                    board, glob = board[:max_rows], glob[:max_rows]
                 policy, value = evaluator(board, glob, rows, count)
             else:
                 k = int(count.item())  # one host read per simulation

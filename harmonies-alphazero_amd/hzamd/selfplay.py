@@ -74,8 +74,11 @@ class SelfPlay:
         _, count = env.legal_mask()
         noise, u = self.noise.draw(self.step_counter, count, cfg["dirichlet_alpha"])
         self.step_counter += 1
+        # the leaf batch holds at most one row per active board: size the
+        # network's launches by that (late in the games most boards are done)
+        n_active = max(1, int(active.sum()))
         v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
-                             eps=cfg["dirichlet_epsilon"], testing=testing)
+                             eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=n_active)
         explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
         act = choose_actions(v, explore, u)
         if self.keep_noise:

@@ -140,10 +140,12 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
 
         def __init__(self):
             self.calls = []
+            self.shapes = []
 
         def __call__(self, board, glob, rows, count):
             k = int(count.item())
             self.calls.append(k)
+            self.shapes.append(board.shape[0])
             assert bool((rows[:k].diff() > 0).all())       # board order
             pol = torch.full((n, 143), float("nan"), device=DEV)
             val = torch.full((n,), float("nan"), device=DEV)
@@ -152,7 +154,7 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
             return pol, val
 
     out = []
-    for mode in ("full", "host", "device"):
+    for mode in ("full", "host", "device", "device_max"):
         env = BatchedEnv(n, seed_base=base, device=DEV)
         env.reset()
         for p in range(64):
@@ -167,14 +169,19 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
             calls.append(board.shape[0])
             return stub_evaluator(board, glob)
         dr = DeviceRows()
-        v = mcts.search(dr if mode == "device" else ev, cpuct, active=act_b, gather=mode != "full").clone()
-        out.append((v.cpu(), mcts.stats().clone().cpu(), dr.calls if mode == "device" else calls,
+        k_act = int(act_b.sum())
+        v = mcts.search(dr if mode.startswith("device") else ev, cpuct, active=act_b, gather=mode != "full",
+                        max_rows=k_act if mode == "device_max" else None).clone()
+        if mode == "device_max":  # the evaluator saw buffers of the active-board count
+            assert dr.shapes == [k_act] * sims
+        out.append((v.cpu(), mcts.stats().clone().cpu(), dr.calls if mode.startswith("device") else calls,
                     int(mcts.eval_rows.item())))
         mcts.close()
         env.close()
-    (v0, c0, calls0, r0), (v1, c1, calls1, r1), (v2, c2, calls2, r2) = out
-    assert torch.equal(v0, v1) and torch.equal(v0, v2)
+    (v0, c0, calls0, r0), (v1, c1, calls1, r1), (v2, c2, calls2, r2), (v3, c3, calls3, r3) = out
+    assert torch.equal(v0, v1) and torch.equal(v0, v2) and torch.equal(v0, v3)
     assert torch.equal(c0[:, :2], c1[:, :2]) and torch.equal(c0[:, :2], c2[:, :2])
+    assert torch.equal(c0[:, :2], c3[:, :2]) and calls3 == calls2 and r3 == r2
     assert calls0 == [n] * sims and r0 == n * sims
     assert sum(calls1) == r1 == r2 == sum(calls2)
     k = int(act_b.sum())
