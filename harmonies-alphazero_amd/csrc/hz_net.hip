@@ -569,34 +569,58 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
     }
   }
 
-  const float bc0 = bias[co0], bc1 = bias[co0 + 16];
-  float *ob = out + (size_t)s0 * 35 * 128 + co0;
-  const float *rsb = res ? res + (size_t)s0 * 35 * 128 + co0 : nullptr;
+  // Epilogue, out = relu((acc + bias) + res), through a per-wave LDS
+  // transpose of each 16x16 tile: a lane then holds 4 consecutive output
+  // channels of one row, so the residual loads and the stores are float4
+  // (a quarter of the memory instructions of per-element ones, which took
+  // ~17-21 k cycles per workgroup with the MFMA pipes idle).  The tile lives
+  // in buffer 0, which no wave reads after the last chunk's barrier (the last
+  // chunk is in buffer 1: NQ is even).
+  static_assert(NQ % 2 == 0, "the last chunk is staged in buffer 1");
+  constexpr int kTS = 20;  // tile row stride (floats): 16-B aligned rows, conflict-free column writes
+  static_assert(kThreads / 64 * 16 * kTS * 4 <= kZero, "per-wave tiles fit in buffer 0");
+  float *tile = (float *)lds + w * 16 * kTS;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
+  const int cow = 32 * (w & 3) + tcol;  // this lane's first output channel (column block 0)
   const int nrow = ns * 35;
-  float rv[kRBT][2][4];
+  const size_t gbase = (size_t)s0 * 35 * 128;
+  float4 rv[kRBT][2];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    const int rbase = (rh * kRBT + rb) * 16 + 4 * kg;
+    const int row = (rh * kRBT + rb) * 16 + trow;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const bool ok = rbase + j < nrow;
-      rv[rb][0][j] = rsb && ok ? rsb[(rbase + j) * 128] : 0.f;
-      rv[rb][1][j] = rsb && ok ? rsb[(rbase + j) * 128 + 16] : 0.f;
-    }
+    for (int cb = 0; cb < 2; cb++)
+      rv[rb][cb] = res && row < nrow ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  const float4 bv[2] = {*(const float4 *)(bias + cow), *(const float4 *)(bias + cow + 16)};
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    const int rbase = (rh * kRBT + rb) * 16 + 4 * kg;
+    const int row = (rh * kRBT + rb) * 16 + trow;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      if (rbase + j < nrow) {
-        float v0 = acc[rb][0][j] + bc0, v1 = acc[rb][1][j] + bc1;
-        if (rsb) {
-          v0 = v0 + rv[rb][0][j];
-          v1 = v1 + rv[rb][1][j];
+    for (int cb = 0; cb < 2; cb++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) tile[(4 * kg + j) * kTS + (lane & 15)] = acc[rb][cb][j];
+      __builtin_amdgcn_wave_barrier();
+      const float4 a4 = *(const float4 *)(tile + trow * kTS + tcol);
+      __builtin_amdgcn_wave_barrier();
+      if (row < nrow) {
+        float4 v;
+        v.x = a4.x + bv[cb].x;
+        v.y = a4.y + bv[cb].y;
+        v.z = a4.z + bv[cb].z;
+        v.w = a4.w + bv[cb].w;
+        if (res) {
+          v.x = v.x + rv[rb][cb].x;
+          v.y = v.y + rv[rb][cb].y;
+          v.z = v.z + rv[rb][cb].z;
+          v.w = v.w + rv[rb][cb].w;
         }
-        ob[(rbase + j) * 128] = v0 > 0.f ? v0 : 0.f;
-        ob[(rbase + j) * 128 + 16] = v1 > 0.f ? v1 : 0.f;
+        v.x = v.x > 0.f ? v.x : 0.f;
+        v.y = v.y > 0.f ? v.y : 0.f;
+        v.z = v.z > 0.f ? v.z : 0.f;
+        v.w = v.w > 0.f ? v.w : 0.f;
+        *(float4 *)(out + gbase + (size_t)row * 128 + cow + 16 * cb) = v;
       }
     }
   }
