@@ -124,10 +124,12 @@ class BatchedMCTS:
         only when it expands the root, which the first (eager) simulation does
         (hz_mcts.hip k_expand_backup: noisy = leaf == 0 && !testing && noise)."""
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._sync()  # the handles launch on the capture stream
-            self._device_step(evaluator, cpuct, active, None, eps, testing, max_rows)
-        self._sync()
+        try:
+            with torch.cuda.graph(g):
+                self._sync()  # the handles launch on the capture stream
+                self._device_step(evaluator, cpuct, active, None, eps, testing, max_rows)
+        finally:
+            self._sync()  # back on the caller's stream, captured or not
         return g
 
     def search(self, evaluator, cpuct, active=None, noise=None, eps=0.25, testing=True, sims=None,
