@@ -187,3 +187,64 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
     k = int(act_b.sum())
     assert max(calls1) <= k and r1 < k * sims        # terminal leaves were skipped
     assert bool((v1[~act_b.cpu()] == 0).all())
+
+
+def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
+    """BASELINE config 3's search at full size: 4096 boards at assorted game
+    positions, 200 simulations, self-play settings (testing=False: the root
+    Dirichlet mix with eps 0.25, cpuct 2), stub evaluator, gathered leaf
+    batches on the device; every board's visit counts, tree sizes and next
+    MT word checked against the C oracle's search (run on the host cores)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+
+    class DeviceRows:  # the stub on the device-row protocol (no host read per simulation)
+        device_rows = True
+
+        def __call__(self, board, glob, rows, count):
+            return stub_evaluator(board, glob)
+
+    n, base, sims, cpuct, eps = 4096, 1300, 200, 2.0, 0.25
+    env = BatchedEnv(n, seed_base=base, device=DEV)
+    env.reset()
+    plies = torch.arange(n, device=DEV) % 63
+    for p in range(63):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+    st0, mt0, idx0 = env.export_state(with_mt=True)
+    st0, mt0, idx0 = st0.cpu().numpy(), mt0.cpu().numpy().view(np.uint32), idx0.cpu().numpy()
+    active = ~env.done()
+    torch.manual_seed(4)
+    noise = torch.distributions.Dirichlet(torch.full((69,), 0.4)).sample((n,)).double()
+    mcts = BatchedMCTS(env, sims)
+    visits = mcts.search(DeviceRows(), cpuct, active=active, noise=noise, eps=eps, testing=False,
+                         max_rows=int(active.sum())).cpu().numpy()
+    counts = mcts.stats().cpu().numpy()
+    _, mt1, idx1 = env.export_state(with_mt=True)
+    mt1, idx1 = mt1.cpu().numpy().view(np.uint32), idx1.cpu().numpy()
+    act_np = active.cpu().numpy()
+    nz = noise.numpy()
+
+    def one(b):
+        m = oracle.mt_from_words(mt0[b], idx0[b])
+        _, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, cpuct, eps=eps, testing=False,
+                                           noise=np.concatenate([nz[b], np.zeros(143 - 69)]))
+        return ov, nn, ne, oracle.mt_next32(m)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(one, [b for b in range(n) if act_np[b]]))
+    k = 0
+    for b in range(n):
+        if not act_np[b]:
+            assert visits[b].sum() == 0
+            continue
+        ov, nn, ne, nxt = res[k]
+        k += 1
+        assert (visits[b] == ov).all(), b
+        assert (counts[b, 0], counts[b, 1]) == (nn, ne), b
+        assert oracle.mt_next32(oracle.mt_from_words(mt1[b], idx1[b])) == nxt, b
+    assert k > 3000
+    mcts.close()
+    env.close()
