@@ -494,6 +494,17 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
     const int a = cbase[rb] + d;
     return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
   };
+  // the stem's second chunk holds only slots 32-39 (channels 32-36, the
+  // phase channel's three pieces): its K-steps take 8 channels x 4 taps
+  // instead of 32 channels x 1 tap, lane group kg reading tap 4 s + kg
+  // (zero past tap 8): 3 K-steps instead of 9 (weights packed to match,
+  // hzamd/infer.py pack_stem_x6)
+  auto aoff_tp = [&](int rb, int st) -> int {
+    const int tap = 4 * st + kg, base = cbase[rb] - 16 * kg;
+    if (tap >= 9) return kZero + (base & 255);
+    const int a = base + ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
+    return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
+  };
 
   f32x4 acc[kRBT][2];
 #pragma unroll
@@ -529,7 +540,8 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
     for (int q = 0; q < NQ; q++) {
       const char *lb = lds + (q & 1) * kBufT;
       if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
-      for (int tap = 0; tap < 9; tap++) {
+      const bool packed = Stem && q == 1;  // tap-packed K-steps (above)
+      for (int tap = 0; tap < (packed ? 3 : 9); tap++) {
         const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
   #pragma unroll
         for (int p = 0; p < 3; p++) {
@@ -543,7 +555,7 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
           bf16x8 a[kRBT];
   #pragma unroll
           for (int rb = 0; rb < kRBT; rb++)
-            a[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
+            a[rb] = *(const bf16x8 *)(lb + (packed ? aoff_tp(rb, tap) : aoff(rb, tap)) + 64 * pa);
   #pragma unroll
           for (int pb = 0; pb < 3 - pa; pb++) {
             const bf16x8 b0 = b[pb][0], b1 = b[pb][1];

@@ -102,19 +102,31 @@ def _conv3x3_x6_act(x, wpack6, b, res=None, live=None):
 
 
 def pack_stem_x6(w):
-    """Stem weights [128][38][3][3] packed like pack_conv3x3_x6
-    (hz_stem3x3_x6_bias_act's layout) over 64 input slots: channels 0-37,
-    then channel 37's weights again in slots 38 and 39, where the kernel
-    stages the phase channel's bf16 pieces m and l; slot 38 keeps the planes
-    (h, m), slot 39 only h, so each piece meets the weight pieces of the
-    six-product split; slots 40-63 are zero."""
-    w64 = torch.zeros(w.shape[0], 64, 3, 3, dtype=w.dtype, device=w.device)
+    """Stem weights [128][38][3][3] in hz_stem3x3_x6_bias_act's layout: bf16
+    planes [K-step][q][plane][co][32] over 64 input slots.  Slots 0-37 are
+    the channels, then channel 37's weights again in slots 38 and 39, where
+    the kernel stages the phase channel's bf16 pieces m and l: slot 38 keeps
+    the planes (h, m), slot 39 only h, so each piece meets the weight pieces
+    of the six-product split.  Chunk 0 (slots 0-31) is packed as
+    pack_conv3x3_x6 (K-step = tap); chunk 1 holds only slots 32-39, so its
+    K-steps are tap-packed: step s, k = 8 g + j is slot 32 + j at tap
+    4 s + g (zero past tap 8), in the entries of K-steps 0-2."""
+    co = w.shape[0]
+    w64 = torch.zeros(co, 64, 3, 3, dtype=w.dtype, device=w.device)
     w64[:, :w.shape[1]] = w
     w64[:, 38] = w64[:, 39] = w[:, 37]
-    p = pack_conv3x3_x6(w64)                             # [tap][q][plane][co][32]
-    p[:, 1, 2, :, 6] = 0                                 # slot 38: planes h, m
-    p[:, 1, 1:, :, 7] = 0                                # slot 39: plane h
-    return p
+    pl = split3_bf16(w64)                                # [3][co][64][3][3]
+    pl[2, :, 38] = 0                                     # slot 38: planes h, m
+    pl[1:, :, 39] = 0                                    # slot 39: plane h
+    pl = pl.reshape(3, co, 64, 9)                        # [plane][co][slot][tap]
+    p = torch.zeros(9, 2, 3, co, 32, dtype=pl.dtype, device=w.device)
+    p[:, 0] = pl[:, :, :32, :].permute(3, 0, 1, 2)       # [tap][plane][co][slot]
+    for st in range(3):
+        for g in range(4):
+            tap = 4 * st + g
+            if tap < 9:
+                p[st, 1, :, :, 8 * g:8 * g + 8] = pl[:, :, 32:40, tap]
+    return p.contiguous()
 
 
 def _stem_x6_act(board, wpack6, b, live=None):
