@@ -73,11 +73,13 @@ def parse():
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
-                    help="2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+                    help="1: one game at a time through the drop-in modules (profile_self_play.py); "
+                         "2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
                          "moves with the network; 4: whole self-play iterations + the RCCL all-gather into "
                          "every rank's replay buffer; 5: whole training iterations "
                          "(self-play -> buffer -> training -> arena)")
+    ap.add_argument("--games", type=int, default=4, help="config 1: timed games (seeds 0..games-1)")
     ap.add_argument("--no-selfplay", action="store_true", help="config 2: skip the selfplay sub-object")
     ap.add_argument("--sp-boards", type=int, default=4096, help="selfplay sub-object: boards per GPU")
     ap.add_argument("--sp-sims", type=int, default=200, help="selfplay sub-object: simulations per move")
@@ -141,6 +143,69 @@ def cpu_baseline(boards, seconds):
             "sample": f"{k} batches x {boards} rule-driven games ({steps} env steps) in {dt:.1f}s, "
                       f"C oracle with OpenMP, {nthreads} threads; 1 core: {k1} batches x {boards // 4} games "
                       f"in {dt1:.1f}s"}
+
+
+def bench_single_game(args, dev):
+    """BASELINE config 1: profile_self_play.py:17-77's loop, one game at a
+    time through the drop-in modules (harmonies_engine.HarmoniesGameState,
+    process_game_state.create_state_tensors, MCTS.get_best_action_and_pi)
+    with hzamd.manager.ModelManager as the model manager (predict: the folded
+    HIP network at batch 1), 32 simulations per move, mcts_config_default
+    otherwise, default network random-initialised with torch.manual_seed(0);
+    game g seeded random.seed(g), np.random.seed(g) as in BASELINE.md.  One
+    host round trip per simulation, as the reference's evaluator contract
+    has it.  Reports games/s over `games` games after one warm-up game."""
+    import random
+
+    import numpy as np
+    from harmonies_engine import HarmoniesGameState
+    from MCTS import get_best_action_and_pi
+    from process_game_state import create_state_tensors
+
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    from hzamd.selfplay import MCTS_DEFAULT
+    sims = args.sims or 32
+    cfg = dict(MCTS_DEFAULT, num_simulations=sims)
+    torch.manual_seed(0)
+    mm = ModelManager(dict(DEFAULT), {"device": str(dev), "optimizer_type": "Adam", "learning_rate": 0.001,
+                                      "weight_decay": 0.0001, "value_loss_weight": 1.0,
+                                      "policy_loss_weight": 1.0})
+
+    def one(g):
+        random.seed(g)
+        np.random.seed(g)
+        game, turn = HarmoniesGameState(), 0
+        while not game.is_game_over():
+            create_state_tensors(game)  # the reference loop builds the inputs every ply
+            action, _ = get_best_action_and_pi(game.clone(), mm, cfg, turn)
+            if action is None:
+                raise RuntimeError(f"config 1: no move for seed {g} at ply {turn}")
+            game = game.apply_move(action)
+            turn += 1
+        return turn
+
+    one(1000)  # warm-up: kernels, allocator, the folded network
+    torch.cuda.synchronize(dev)
+    times, plies = [], []
+    for g in range(args.games):
+        t0 = time.perf_counter()
+        plies.append(one(g))
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    total = sum(times)
+    line = {"metric": "config 1: one self-play game at a time through the drop-in modules (games/s)",
+            "value": len(times) / total, "unit": "games/s", "n_gpus": 1, "steps": len(times), "warmup": 1,
+            "ms_per_step": total / len(times) * 1e3, "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic: random-init network, seeded games",
+            "config": {"workload": f"config1: 1 game at a time, {sims} sims/move, mcts_config_default, "
+                                   "default 128fx8 net", "games": len(times), "sims": sims},
+            "s_per_game": [round(t, 3) for t in times], "plies": plies,
+            "plies_per_s": sum(plies) / total, "sims_per_s": sum(plies) * sims / total,
+            "reference_cpu": {"s_per_game": 13.80, "games_per_s": 0.0725, "plies_per_s": 4.35,
+                              "source": "BASELINE.md: the reference on 8 CPU cores, seeds 0-3, measured in the "
+                                        "survey container (not published)"}}
+    print(json.dumps(line), flush=True)
 
 
 def bench_loop(args, dev, rank, world):
@@ -615,6 +680,11 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    if args.config == 1:
+        if world > 1:
+            raise SystemExit("config 1 is one game at a time on one GPU")
+        bench_single_game(args, dev)
+        return
     if args.config == 5:
         bench_loop(args, dev, rank, world)
         if world > 1:

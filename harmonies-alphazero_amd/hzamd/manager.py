@@ -57,18 +57,49 @@ class ModelManager:
         self.value_loss_fn = nn.MSELoss()
         self.value_loss_weight = training_config["value_loss_weight"]
         self.policy_loss_weight = training_config["policy_loss_weight"]
+        self._folded = None
+        self._folded_sig = None
 
     # -- inference -------------------------------------------------------------
+    def _fast(self):
+        """On the GPU: the folded network (hzamd.infer.FoldedNet: the HIP
+        stem / tower / head kernels, one state per workgroup at batch 1) of
+        the current weights, re-folded whenever any parameter or buffer was
+        modified since (PyTorch's per-tensor version counters: optimizer
+        steps, load_state_dict, any in-place write).  None on the CPU or for
+        shapes the kernels do not cover."""
+        if self.device.type != "cuda":
+            return None
+        tensors = list(self.model.parameters()) + list(self.model.buffers())
+        sig = tuple((t.data_ptr(), t._version) for t in tensors)
+        if self._folded is None or sig != self._folded_sig:
+            from .infer import FoldedNet
+            self.model.eval()
+            if self._folded is None:
+                self._folded = FoldedNet(self.model)
+            else:
+                self._folded.refresh()
+            self._folded_sig = sig
+        f = self._folded
+        return f if f.stem_packed is not None and f.packed is not None else None
+
     def predict(self, board_tensor, global_features_tensor):
+        """model.py:81-110: eval mode, softmax over all 143 logits."""
         if board_tensor.dim() == 3:
             board_tensor = board_tensor.unsqueeze(0)
         if global_features_tensor.dim() == 1:
             global_features_tensor = global_features_tensor.unsqueeze(0)
         self.model.eval()
+        fast = self._fast()
         with torch.no_grad():
-            logits, value = self.model(board_tensor.to(self.device), global_features_tensor.to(self.device))
-            probs = torch.softmax(logits, dim=1)
-        return probs.squeeze(0).detach().cpu().numpy(), value.squeeze(0).item()
+            board = board_tensor.to(self.device, torch.float32)
+            glob = global_features_tensor.to(self.device, torch.float32)
+            if fast is not None:
+                probs, value = fast.predict(board.contiguous(), glob.contiguous())
+            else:
+                logits, value = self.model(board, glob)
+                probs = torch.softmax(logits, dim=1)
+        return probs.squeeze(0).detach().cpu().numpy(), value.reshape(-1)[0].item()
 
     # -- training --------------------------------------------------------------
     def losses(self, board, glob, target_pi, target_z):

@@ -114,3 +114,41 @@ def test_graphed_training_phase_matches_eager(net):
             assert torch.allclose(v, w1[k], rtol=1e-3, atol=1e-5), k
         else:
             assert torch.equal(v, w1[k]), k
+
+
+def test_manager_predict_uses_folded_kernels_and_follows_weight_changes():
+    """ModelManager.predict on the GPU runs the folded HIP network at batch 1
+    (model.py:81-110 semantics: eval mode, softmax over all logits) and
+    re-folds after any weight change: an optimizer step, a load_state_dict."""
+    from hzamd.net import DEFAULT, HarmoniesNet
+    from test_infer_cpu import _randomise_bn
+    from test_manager_cpu import TRAIN_CFG
+    g = torch.Generator().manual_seed(12)
+    torch.manual_seed(0)
+    mm = ModelManager(dict(DEFAULT), dict(TRAIN_CFG, device="cuda:0"))
+    _randomise_bn(mm.model, g)
+    board = (torch.rand(38, 5, 7, generator=g) > 0.8).float()
+    glob = torch.rand(42, generator=g)
+
+    def want():
+        mm.model.eval()
+        with torch.no_grad():
+            lo, v = mm.model(board[None].cuda(), glob[None].cuda())
+        return torch.softmax(lo, 1)[0].cpu().numpy(), float(v.reshape(-1)[0])
+
+    def check():
+        p, v = mm.predict(board, glob)
+        wp, wv = want()
+        assert p.shape == (143,) and abs(float(p.sum()) - 1.0) < 1e-5
+        assert float(abs(p - wp).max()) <= 1e-5 and abs(v - wv) <= 1e-5, (float(abs(p - wp).max()), v, wv)
+        return p
+    p0 = check()
+    assert mm._folded is not None and mm._folded.packed is not None
+    B = 8
+    mm.train_step(board[None].repeat(B, 1, 1, 1), glob[None].repeat(B, 1), torch.full((B, 143), 1 / 143),
+                  torch.ones(B, 1))
+    p1 = check()
+    assert float(abs(p1 - p0).max()) > 0
+    other = HarmoniesNet().cuda()
+    mm.model.load_state_dict(other.state_dict())
+    check()
