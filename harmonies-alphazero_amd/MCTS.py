@@ -93,6 +93,27 @@ class _PredictAdapter:
         return p, v
 
 
+class _FoldedRows:
+    """hzamd.manager.ModelManager.predict's own computation (the folded HIP
+    network, softmax) on the device-row protocol: the leaf stays on the GPU,
+    no host round trip per simulation.  Used only for that ModelManager; any
+    other model manager goes through its predict()."""
+
+    device_rows = True
+
+    def __init__(self, folded):
+        self.f = folded
+
+    def __call__(self, board, glob, rows=None, count=None):
+        return self.f.predict(board, glob, live=count)
+
+
+def _evaluator(model_manager, device):
+    fast = getattr(model_manager, "_fast", None)
+    f = fast() if callable(fast) else None
+    return _FoldedRows(f) if f is not None else _PredictAdapter(model_manager, device)
+
+
 def get_best_action_and_pi(game_state, model_manager, mcts_config, game_move_number):
     br = bridge()
     sims = int(mcts_config["num_simulations"])
@@ -107,7 +128,7 @@ def get_best_action_and_pi(game_state, model_manager, mcts_config, game_move_num
         vec = np.random.dirichlet([mcts_config["dirichlet_alpha"]] * len(legal))  # MCTS.py:314-316
         noise = torch.zeros(1, 69, dtype=torch.float64)
         noise[0, :len(vec)] = torch.from_numpy(np.asarray(vec, dtype=np.float64))
-    visits = search.search(_PredictAdapter(model_manager, br.device), float(mcts_config["cpuct"]),
+    visits = search.search(_evaluator(model_manager, br.device), float(mcts_config["cpuct"]),
                            noise=noise, eps=float(mcts_config["dirichlet_epsilon"]), testing=testing)
     v = visits[0].cpu().numpy().astype(np.int64)
     br.store_rng()

@@ -103,3 +103,17 @@ def test_config4_exchange_two_ranks_equals_world1(tmp_path):
     want = torch.cat([torch.cat((own[0][i], own[1][i])) for i in range(2)])
     assert torch.equal(w2[0]["buffer"], want)
     assert d["exchange"]["records"] == want.shape[0] == d["examples_per_iteration"] * 2
+
+
+def test_config1_single_game_contract():
+    """bench.py --config 1: games played one at a time through the drop-in
+    modules (harmonies_engine / MCTS / process_game_state with ModelManager)
+    to the end; one JSON line with the contract keys and the reference's
+    CPU figure beside it."""
+    r = _single(["--config", "1", "--games", "1", "--sims", "2"])
+    d = _last_json(r.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "dtype",
+              "config", "plies", "reference_cpu"):
+        assert k in d, k
+    assert d["unit"] == "games/s" and d["value"] > 0 and d["steps"] == 1
+    assert 40 <= d["plies"][0] <= 100

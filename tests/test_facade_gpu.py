@@ -187,3 +187,35 @@ def test_get_best_action_and_pi_matches_golden(he):
         assert np.allclose(pi, f["pi"][k], rtol=0, atol=0), k
         assert pgs.get_action_index(mv) == f["action"][k], k
         assert nxt == f["next_word"][k], k
+
+
+def test_get_best_action_and_pi_with_model_manager_device_rows(he):
+    """With hzamd's ModelManager the drop-in search evaluates its leaves on
+    the device (the folded network that predict() runs, no host round trip
+    per simulation); any other manager goes through predict().  Both give
+    the same move, pi and Python RNG state on the same positions."""
+    import MCTS
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    from hzamd.state import apply_ref_to_object
+    from test_manager_cpu import TRAIN_CFG
+    torch.manual_seed(0)
+    mm = ModelManager(dict(DEFAULT), dict(TRAIN_CFG, device="cuda:0"))
+
+    class ViaPredict:  # no _fast: MCTS uses predict() per leaf
+        def predict(self, board, glob):
+            return mm.predict(board, glob)
+
+    f = load("mcts.npz")
+    cfg = {"num_simulations": 24, "cpuct": 2.0, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+           "turns_until_tau0": 15, "action_size": 143, "testing": True}
+    for k in range(0, 80, 10):
+        out = []
+        for manager in (mm, ViaPredict()):
+            obj = apply_ref_to_object(f["state"][k], he.HarmoniesGameState.__new__(he.HarmoniesGameState))
+            random.seed(int(f["mt_seed"][k]))
+            mv, pi = MCTS.get_best_action_and_pi(obj, manager, cfg, 20)
+            out.append((mv, pi, random.getrandbits(32)))
+        assert isinstance(MCTS._evaluator(mm, "cuda:0"), MCTS._FoldedRows)
+        (m0, p0, r0), (m1, p1, r1) = out
+        assert m0 == m1 and np.array_equal(p0, p1) and r0 == r1, k
