@@ -140,7 +140,8 @@ def test_manager_predict_uses_folded_kernels_and_follows_weight_changes():
         p, v = mm.predict(board, glob)
         wp, wv = want()
         assert p.shape == (143,) and abs(float(p.sum()) - 1.0) < 1e-5
-        assert float(abs(p - wp).max()) <= 1e-5 and abs(v - wv) <= 1e-5, (float(abs(p - wp).max()), v, wv)
+        # folded fp32-exact-product kernels vs MIOpen's fp32 convs: fp32 rounding
+        assert float(abs(p - wp).max()) <= 1e-4 and abs(v - wv) <= 1e-4, (float(abs(p - wp).max()), v, wv)
         return p
     p0 = check()
     assert mm._folded is not None and mm._folded.packed is not None
