@@ -329,6 +329,7 @@ constexpr int kX6Zero = 512;                          // bytes of zeros after th
 constexpr int kX6Buf = kCS * 35 * kX6Cell + kX6Zero;  // one chunk of 8 states + the zero region
 static_assert(kCS * 35 * kX6Cell % 256 == 0 && kX6Buf % 256 == 0, "zero region and buffers 256-B aligned");
 constexpr int kX6SmallMax = 768;                      // batches up to this run one state per workgroup
+constexpr int kX6TinyMax = 256;                       // ... and up to this, 8 waves of 16 channels each
 
 __device__ __forceinline__ uint32_t bf16_bits(float v) {
   return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)v);
@@ -359,22 +360,24 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
 // chain (8 states: ~175 k cycles, ~73 us, however few states are live), and
 // the arena's batches of a few dozen boards fill only a few CUs; one state
 // per group cuts each wave's chain to a third at 48/35 rows of waste.
-template <int NQ, bool Stem, int CS>
-__global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
+template <int NQ, bool Stem, int CS, int NCB>
+__global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
     k_conv3x3_x6(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                  const float *__restrict__ res, float *__restrict__ out, int32_t batch,
                  const int32_t *__restrict__ live) {
   static_assert(CS == 8 || CS == 1, "8 or 1 states per workgroup");
+  static_assert(NCB == 2 || NCB == 1, "column blocks of 16 output channels per wave");
   constexpr int kRowsT = CS * 35;                  // output rows of the group
   constexpr int kRBT = CS == 8 ? 9 : 3;            // row blocks of 16 per wave
-  constexpr int kThreads = (CS == 8 ? 2 : 1) * 256;
+  constexpr int kCG = 8 / NCB;                     // column groups (waves per row group)
+  constexpr int kThreads = (CS == 8 ? 2 : 1) * kCG * 64;
   constexpr int kStg = (kRowsT * 8 + kThreads - 1) / kThreads;  // float4 staged per thread per chunk
   constexpr int kZero = (CS * 35 * kX6Cell + 255) / 256 * 256;   // zero region: 256-B aligned (banks)
   constexpr int kBufT = kZero + kX6Zero;                          // one chunk's buffer + zero region
-  static_assert((kThreads / 256) * kRBT * 16 >= kRowsT, "row blocks cover the rows");
+  static_assert((CS == 8 ? 2 : 1) * kRBT * 16 >= kRowsT, "row blocks cover the rows");
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w / kCG, cg = w % kCG;
   const int s0 = blockIdx.x * CS;
   if (live) batch = *live < batch ? *live : batch;  // rows past the live count are not computed
   if (s0 >= batch) return;
@@ -439,15 +442,17 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
   }
   // the wait names the staged registers, so the split's arithmetic (which,
   // unlike an LDS store, could move above a plain asm statement) waits too
-  static_assert(kStg == 5 || kStg == 2, "HZ_X6_STORE ties five or two staging registers");
+  static_assert(kStg == 5 || kStg == 2 || kStg == 1, "HZ_X6_STORE ties five, two or one staging registers");
 #define HZ_X6_STORE(buf)                                                                  \
   if constexpr (kStg == 5)                                                                \
     asm volatile("s_waitcnt vmcnt(0)"                                                     \
                  : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4])    \
                  :                                                                        \
                  : "memory");                                                             \
-  else                                                                                    \
+  else if constexpr (kStg == 2)                                                           \
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[0]), "+v"(stg[1]) : : "memory");         \
+  else                                                                                    \
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[0]) : : "memory");                       \
   _Pragma("unroll") for (int it = 0; it < kStg; it++) {                                   \
     uint2 h_, m_, l_;                                                                     \
     split4(stg[it], h_, m_, l_);                                                          \
@@ -506,11 +511,13 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
     return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
   };
 
-  f32x4 acc[kRBT][2];
+  f32x4 acc[kRBT][NCB];
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) acc[rb][0] = acc[rb][1] = (f32x4){};
+  for (int rb = 0; rb < kRBT; rb++)
+#pragma unroll
+    for (int cb = 0; cb < NCB; cb++) acc[rb][cb] = (f32x4){};
 
-  const int co0 = 32 * (w & 3) + (lane & 15);
+  const int co0 = 16 * NCB * cg + (lane & 15);
   // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
   // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
   const bf16x8 *wl = wp + co0 * 4 + kg;
@@ -528,12 +535,11 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
   if constexpr (Stem) npa = npa ? 3 : 1;
   HZ_STAMP(2)
 
-  bf16x8 b[3][2], bn[3][2];  // this K-step's B fragments, the next step's (loaded a step ahead)
+  bf16x8 b[3][NCB], bn[3][NCB];  // this K-step's B fragments, the next step's (loaded a step ahead)
 #pragma unroll
-  for (int p = 0; p < 3; p++) {
-    b[p][0] = bload(0, p, 0);
-    b[p][1] = bload(0, p, 1);
-  }
+  for (int p = 0; p < 3; p++)
+#pragma unroll
+    for (int cb = 0; cb < NCB; cb++) b[p][cb] = bload(0, p, cb);
 
   {
 #pragma unroll
@@ -544,10 +550,9 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
       for (int tap = 0; tap < (packed ? 3 : 9); tap++) {
         const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
   #pragma unroll
-        for (int p = 0; p < 3; p++) {
-          bn[p][0] = bload(Ln, p, 0);
-          bn[p][1] = bload(Ln, p, 1);
-        }
+        for (int p = 0; p < 3; p++)
+  #pragma unroll
+          for (int cb = 0; cb < NCB; cb++) bn[p][cb] = bload(Ln, p, cb);
         // plane a of A against the planes b with a + b <= 2
   #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
@@ -558,19 +563,17 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
             a[rb] = *(const bf16x8 *)(lb + (packed ? aoff_tp(rb, tap) : aoff(rb, tap)) + 64 * pa);
   #pragma unroll
           for (int pb = 0; pb < 3 - pa; pb++) {
-            const bf16x8 b0 = b[pb][0], b1 = b[pb][1];
   #pragma unroll
-            for (int rb = 0; rb < kRBT; rb++) {
-              acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b0, acc[rb][0], 0, 0, 0);
-              acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b1, acc[rb][1], 0, 0, 0);
-            }
+            for (int rb = 0; rb < kRBT; rb++)
+  #pragma unroll
+              for (int cb = 0; cb < NCB; cb++)
+                acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
           }
         }
   #pragma unroll
-        for (int p = 0; p < 3; p++) {
-          b[p][0] = bn[p][0];
-          b[p][1] = bn[p][1];
-        }
+        for (int p = 0; p < 3; p++)
+  #pragma unroll
+          for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
       }
       if (q < NQ - 1) {
         HZ_X6_STORE((q + 1) & 1)
@@ -589,28 +592,32 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
   // in buffer 0, which no wave reads after the last chunk's barrier (the last
   // chunk is in buffer 1: NQ is even).
   static_assert(NQ % 2 == 0, "the last chunk is staged in buffer 1");
-  constexpr int kTS = 20;  // tile row stride (floats): 16-B aligned rows, conflict-free column writes
-  static_assert(kThreads / 64 * 16 * kTS * 4 <= kZero, "per-wave tiles fit in buffer 0");
+  // tile row stride (floats): 16-B aligned rows, conflict-free column writes
+  // (16 where 20 would not fit: one state, 8 waves)
+  constexpr int kTS = kThreads / 64 * 16 * 20 * 4 <= kZero ? 20 : 16;
+  static_assert(kThreads / 64 * 16 * kTS * 4 <= kBufT, "per-wave tiles fit in buffer 0");
   float *tile = (float *)lds + w * 16 * kTS;
   const int trow = lane >> 2, tcol = 4 * (lane & 3);
-  const int cow = 32 * (w & 3) + tcol;  // this lane's first output channel (column block 0)
+  const int cow = 16 * NCB * cg + tcol;  // this lane's first output channel (column block 0)
   const int nrow = ns * 35;
   const size_t gbase = (size_t)s0 * 35 * 128;
-  float4 rv[kRBT][2];
+  float4 rv[kRBT][NCB];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
     const int row = (rh * kRBT + rb) * 16 + trow;
 #pragma unroll
-    for (int cb = 0; cb < 2; cb++)
+    for (int cb = 0; cb < NCB; cb++)
       rv[rb][cb] = res && row < nrow ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  const float4 bv[2] = {*(const float4 *)(bias + cow), *(const float4 *)(bias + cow + 16)};
+  float4 bv[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(bias + cow + 16 * cb);
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
     const int row = (rh * kRBT + rb) * 16 + trow;
 #pragma unroll
-    for (int cb = 0; cb < 2; cb++) {
+    for (int cb = 0; cb < NCB; cb++) {
 #pragma unroll
       for (int j = 0; j < 4; j++) tile[(4 * kg + j) * kTS + (lane & 15)] = acc[rb][cb][j];
       __builtin_amdgcn_wave_barrier();
@@ -647,7 +654,7 @@ __global__ void __launch_bounds__(CS == 8 ? 512 : 256, 1)
 
 }  // namespace
 
-template <int NQ, bool Stem, int CS>
+template <int NQ, bool Stem, int CS, int NCB>
 static int launch_x6_cs(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                         int32_t batch, const int32_t *live, void *stream) {
   static std::atomic<uint64_t> init_mask{0};
@@ -655,13 +662,14 @@ static int launch_x6_cs(const float *x, const void *wpack6, const float *bias, c
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3_x6<NQ, Stem, CS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6<NQ, Stem, CS, NCB>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
-  hipLaunchKernelGGL((k_conv3x3_x6<NQ, Stem, CS>), dim3((batch + CS - 1) / CS), dim3(CS == 8 ? 512 : 256), lds,
-                     (hipStream_t)stream, x, (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  hipLaunchKernelGGL((k_conv3x3_x6<NQ, Stem, CS, NCB>), dim3((batch + CS - 1) / CS),
+                     dim3((CS == 8 ? 2 : 1) * (8 / NCB) * 64), lds, (hipStream_t)stream, x, (const bf16x8 *)wpack6,
+                     bias, res, out, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -675,11 +683,22 @@ static int32_t x6_small_max() {
   return v;
 }
 
+// ... and up to this many, one state per workgroup with 8 waves of 16
+// output channels (half of each wave's MFMA chain; HZ_X6_TINY_MAX overrides)
+static int32_t x6_tiny_max() {
+  static const int32_t v = [] {
+    const char *e = getenv("HZ_X6_TINY_MAX");
+    return e ? (int32_t)atoi(e) : (int32_t)kX6TinyMax;
+  }();
+  return v;
+}
+
 template <int NQ, bool Stem>
 static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                      int32_t batch, const int32_t *live, void *stream) {
-  return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1>(x, wpack6, bias, res, out, batch, live, stream)
-                                 : launch_x6_cs<NQ, Stem, 8>(x, wpack6, bias, res, out, batch, live, stream);
+  if (batch <= x6_tiny_max()) return launch_x6_cs<NQ, Stem, 1, 1>(x, wpack6, bias, res, out, batch, live, stream);
+  return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1, 2>(x, wpack6, bias, res, out, batch, live, stream)
+                                 : launch_x6_cs<NQ, Stem, 8, 2>(x, wpack6, bias, res, out, batch, live, stream);
 }
 
 extern "C" int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res,
