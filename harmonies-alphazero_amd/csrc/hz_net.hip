@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "../../include/hz_abi.h"
 
@@ -351,6 +352,49 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
   l = make_uint2(lb[0] | lb[1] << 16, lb[2] | lb[3] << 16);
 }
 
+// Tap classes (8-state tower conv).  On the 5x7 board with zero padding a
+// cell on the top row has no dh = -1 neighbours, one on the left column no
+// dw = -1 neighbours, and so on: of the 315 (cell, tap) pairs of a state only
+// 247 read the board.  The 280 rows of a workgroup are regrouped into 18
+// blocks of 16 rows whose cells share (a superset of) their valid taps, and
+// a block issues MFMAs only for its taps: 132 block-taps instead of 162
+// (-18.5 % MFMA work).  Blocks 0-8 are row half 0, 9-17 row half 1, each
+// 66 block-taps: 4 interior blocks (9 taps) and 5 edge blocks (6 taps; the
+// corner cells ride in edge blocks whose taps cover theirs).
+// kX6ClassRow: the block's rows as state * 35 + cell (-1: padding row, not
+// stored); kX6ClassTaps: each block's taps (bit t = tap t = (dh + 1) * 3 +
+// dw + 1).  Generated by the grouping in DESIGN.md §3 (k_conv3x3_x6 row).
+__constant__ int16_t kX6ClassRow[18][16] = {
+    {8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 22, 23, 24, 25, 26, 43},  // MM
+    {44, 45, 46, 47, 50, 51, 52, 53, 54, 57, 58, 59, 60, 61, 78, 79},  // MM
+    {80, 81, 82, 85, 86, 87, 88, 89, 92, 93, 94, 95, 96, 113, 114, 115},  // MM
+    {116, 117, 120, 121, 122, 123, 124, 127, 128, 129, 130, 131, 148, 149, 150, 151},  // MM
+    {1, 2, 3, 4, 5, 36, 37, 38, 39, 40, 71, 72, 73, 74, 75, 106},  // TM
+    {107, 108, 109, 110, 141, 142, 143, 144, 145, 176, 177, 178, 179, 180, 211, 212},  // TM
+    {29, 30, 31, 32, 33, 64, 65, 66, 67, 68, 99, 100, 101, 102, 103, 134},  // BM
+    {7, 14, 21, 42, 49, 56, 77, 84, 91, 112, 119, 126, 147, 154, 161, 182},  // ML
+    {13, 20, 27, 48, 55, 62, 83, 90, 97, 118, 125, 132, 153, 160, 167, 188},  // MR
+    {152, 155, 156, 157, 158, 159, 162, 163, 164, 165, 166, 183, 184, 185, 186, 187},  // MM
+    {190, 191, 192, 193, 194, 197, 198, 199, 200, 201, 218, 219, 220, 221, 222, 225},  // MM
+    {226, 227, 228, 229, 232, 233, 234, 235, 236, 253, 254, 255, 256, 257, 260, 261},  // MM
+    {262, 263, 264, 267, 268, 269, 270, 271, -1, -1, -1, -1, -1, -1, -1, -1},  // MM
+    {213, 214, 215, 246, 247, 248, 249, 250, 0, 35, 70, 105, 140, 175, 210, 245},  // TM
+    {135, 136, 137, 138, 169, 170, 171, 172, 173, 204, 205, 206, 207, 208, 239, 240},  // BM
+    {241, 242, 243, 274, 275, 276, 277, 278, 34, 69, 104, 139, 174, 209, 244, 279},  // BM
+    {189, 196, 217, 224, 231, 252, 259, 266, 28, 63, 98, 133, 168, 203, 238, 273},  // ML
+    {195, 202, 223, 230, 237, 258, 265, 272, 6, 41, 76, 111, 146, 181, 216, 251},  // MR
+};
+// kX6ClassSel: the block taps some of whose rows (the corner cells) read
+// off the board: only those need the zero-region redirect
+constexpr uint32_t kX6ClassSel[2][9] = {
+    {0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000},
+    {0x000, 0x000, 0x000, 0x000, 0x048, 0x000, 0x024, 0x180, 0x003},
+};
+constexpr uint32_t kX6ClassTaps[2][9] = {
+    {0x1ff, 0x1ff, 0x1ff, 0x1ff, 0x1f8, 0x1f8, 0x03f, 0x1b6, 0x0db},
+    {0x1ff, 0x1ff, 0x1ff, 0x1ff, 0x1f8, 0x03f, 0x03f, 0x1b6, 0x0db},
+};
+
 // NQ chunks of 32 input channels.  Stem: x is the encoder's NCHW board
 // [B][38][5][7] (channels >= 38 stage as zeros; NQ = 2), else an NHWC
 // [B][5][7][128] activation (NQ = 4).
@@ -478,11 +522,17 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   // or, off the board, the zero region at the same offset mod 256 (so the
   // lane keeps the LDS banks its row would use).
   // valid[rb] bit tap = the neighbour is on the board.
+  // the 8-state tower groups its rows by tap class (above)
+  constexpr bool kClassed = CS == 8 && !Stem && NCB == 2;
   int cbase[kRBT];
   uint32_t valid[kRBT];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
     int r = (rh * kRBT + rb) * 16 + (lane & 15);
+    if constexpr (kClassed) {
+      r = kX6ClassRow[rh * kRBT + rb][lane & 15];
+      r = r >= 0 ? r : kX6ClassRow[rh * kRBT + rb][0];  // padding rows read a real row (not stored)
+    }
     r = r < kRowsT ? r : kRowsT - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
     cbase[rb] = r * kX6Cell + 16 * kg;
@@ -493,6 +543,13 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
       v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
     }
     valid[rb] = v;
+  }
+  // classed: the epilogue's rows (transposed tiles: lane -> row lane >> 2),
+  // read from the table now so that their latency is long hidden
+  int erow[kClassed ? kRBT : 1];
+  if constexpr (kClassed) {
+#pragma unroll
+    for (int rb = 0; rb < kRBT; rb++) erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
   }
   auto aoff = [&](int rb, int tap) -> int {
     const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
@@ -540,6 +597,63 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   for (int p = 0; p < 3; p++)
 #pragma unroll
     for (int cb = 0; cb < NCB; cb++) b[p][cb] = bload(0, p, cb);
+
+  // classed main loop: the chunk loop rolled, the taps unrolled, one copy
+  // per row half (its blocks' tap sets are compile-time constants)
+  auto classed = [&](auto half) {
+    constexpr int H = decltype(half)::value;
+    for (int q = 0; q < NQ; q++) {
+      const char *lb = lds + (q & 1) * kBufT;
+      if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
+#pragma unroll
+      for (int tap = 0; tap < 9; tap++) {
+        const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+          for (int cb = 0; cb < NCB; cb++) bn[p][cb] = bload(Ln, p, cb);
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          bf16x8 a[kRBT];
+#pragma unroll
+          for (int rb = 0; rb < kRBT; rb++) {
+            if (!((kX6ClassTaps[H][rb] >> tap) & 1)) continue;
+            // a tap every row of the block reads on the board: base + a
+            // non-negative immediate (lbm is lb less the largest negative
+            // neighbour offset), no per-tap address register
+            constexpr int kNeg = 8 * kX6Cell;
+            const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell + kNeg + 64 * pa;
+            a[rb] = (kX6ClassSel[H][rb] >> tap) & 1 ? *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa)
+                                                    : *(const bf16x8 *)(lb - kNeg + cbase[rb] + d);
+          }
+#pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++)
+#pragma unroll
+            for (int rb = 0; rb < kRBT; rb++)
+              if ((kX6ClassTaps[H][rb] >> tap) & 1)
+#pragma unroll
+                for (int cb = 0; cb < NCB; cb++)
+                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+          for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
+        __builtin_amdgcn_sched_barrier(0);  // taps stay in order (registers: no hoisting across)
+      }
+      if (q < NQ - 1) {
+        HZ_X6_STORE((q + 1) & 1)
+        HZ_X6_SYNC(npa_next)
+      }
+      HZ_STAMP(3 + q)
+    }
+  };
+  if constexpr (kClassed) {
+    if (rh == 0)
+      classed(std::integral_constant<int, 0>{});
+    else
+      classed(std::integral_constant<int, 1>{});
+  } else
 
   {
 #pragma unroll
@@ -601,13 +715,19 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   const int cow = 16 * NCB * cg + tcol;  // this lane's first output channel (column block 0)
   const int nrow = ns * 35;
   const size_t gbase = (size_t)s0 * 35 * 128;
+  // the lane's output row (within the group) of block rb; -1: not stored
+  auto orow = [&](int rb) -> int {
+    int row = (rh * kRBT + rb) * 16 + trow;
+    if constexpr (kClassed) row = erow[rb];
+    return row >= 0 && row < nrow ? row : -1;
+  };
   float4 rv[kRBT][NCB];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    const int row = (rh * kRBT + rb) * 16 + trow;
+    const int row = orow(rb);
 #pragma unroll
     for (int cb = 0; cb < NCB; cb++)
-      rv[rb][cb] = res && row < nrow ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
+      rv[rb][cb] = res && row >= 0 ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float4 bv[NCB];
@@ -615,7 +735,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(bias + cow + 16 * cb);
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    const int row = (rh * kRBT + rb) * 16 + trow;
+    const int row = orow(rb);
 #pragma unroll
     for (int cb = 0; cb < NCB; cb++) {
 #pragma unroll
@@ -623,7 +743,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
       __builtin_amdgcn_wave_barrier();
       const float4 a4 = *(const float4 *)(tile + trow * kTS + tcol);
       __builtin_amdgcn_wave_barrier();
-      if (row < nrow) {
+      if (row >= 0) {
         float4 v;
         v.x = a4.x + bv[cb].x;
         v.y = a4.y + bv[cb].y;
