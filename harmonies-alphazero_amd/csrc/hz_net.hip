@@ -710,7 +710,9 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   // (16 where 20 would not fit: one state, 8 waves)
   constexpr int kTS = kThreads / 64 * 16 * 20 * 4 <= kZero ? 20 : 16;
   static_assert(kThreads / 64 * 16 * kTS * 4 <= kBufT, "per-wave tiles fit in buffer 0");
-  float *tile = (float *)lds + w * 16 * kTS;
+  // kT tiles per round (one wave barrier pair per round): 6 where they fit
+  constexpr int kT = kThreads / 64 * 6 * 16 * kTS * 4 <= kZero && (kRBT * NCB) % 6 == 0 ? 6 : 1;
+  float *tile = (float *)lds + w * 16 * kTS * kT;
   const int trow = lane >> 2, tcol = 4 * (lane & 3);
   const int cow = 16 * NCB * cg + tcol;  // this lane's first output channel (column block 0)
   const int nrow = ns * 35;
@@ -734,21 +736,28 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
 #pragma unroll
   for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(bias + cow + 16 * cb);
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) {
-    const int row = orow(rb);
+  for (int r0 = 0; r0 < kRBT * NCB; r0 += kT) {
 #pragma unroll
-    for (int cb = 0; cb < NCB; cb++) {
+    for (int k = 0; k < kT; k++) {
+      const int rb = (r0 + k) / NCB, cb = (r0 + k) % NCB;
 #pragma unroll
-      for (int j = 0; j < 4; j++) tile[(4 * kg + j) * kTS + (lane & 15)] = acc[rb][cb][j];
-      __builtin_amdgcn_wave_barrier();
-      const float4 a4 = *(const float4 *)(tile + trow * kTS + tcol);
-      __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < 4; j++) tile[k * 16 * kTS + (4 * kg + j) * kTS + (lane & 15)] = acc[rb][cb][j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    float4 a4[kT];
+#pragma unroll
+    for (int k = 0; k < kT; k++) a4[k] = *(const float4 *)(tile + k * 16 * kTS + trow * kTS + tcol);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < kT; k++) {
+      const int rb = (r0 + k) / NCB, cb = (r0 + k) % NCB;
+      const int row = orow(rb);
       if (row >= 0) {
         float4 v;
-        v.x = a4.x + bv[cb].x;
-        v.y = a4.y + bv[cb].y;
-        v.z = a4.z + bv[cb].z;
-        v.w = a4.w + bv[cb].w;
+        v.x = a4[k].x + bv[cb].x;
+        v.y = a4[k].y + bv[cb].y;
+        v.z = a4[k].z + bv[cb].z;
+        v.w = a4[k].w + bv[cb].w;
         if (res) {
           v.x = v.x + rv[rb][cb].x;
           v.y = v.y + rv[rb][cb].y;
