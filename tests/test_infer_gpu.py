@@ -378,3 +378,26 @@ def test_x6_small_batch_kernel_matches_large_batch_kernel():
         sub = _conv3x3_x6_act(x[:k].contiguous(memory_format=cl), w, b, r[:k].contiguous(memory_format=cl))
         assert torch.equal(sub, full[:k]), k
         assert torch.equal(_stem_x6_act(board[:k].contiguous(), ws, b), sfull[:k]), k
+
+
+def test_x6_eight_state_form_live_rows_and_accuracy():
+    """The eight-state tower conv (batches above 768 rows: rows grouped by
+    tap class, off-board taps skipped) against float64, and with a live-row
+    bound that ends inside a workgroup (517 = 64 x 8 + 5): the live rows are
+    the rows of the unbounded run, bit for bit."""
+    from hzamd.infer import _conv3x3_x6_act, pack_conv3x3_x6
+    n = 1000
+    g = torch.Generator().manual_seed(33)
+    x = torch.randn(n, 128, 5, 7, generator=g).relu()
+    w = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+    b = torch.randn(128, generator=g) * 0.1
+    r = torch.randn(n, 128, 5, 7, generator=g)
+    cl = torch.channels_last
+    xc, rc = x.cuda().contiguous(memory_format=cl), r.cuda().contiguous(memory_format=cl)
+    wp = pack_conv3x3_x6(w).cuda()
+    full = _conv3x3_x6_act(xc, wp, b.cuda(), rc)
+    want = _conv_ref(x[:64], w, b, r[:64])
+    assert (full[:64].cpu().double() - want).abs().max().item() <= 1e-5
+    lv = torch.tensor([517], dtype=torch.int32, device="cuda")
+    part = _conv3x3_x6_act(xc, wp, b.cuda(), rc, lv)
+    assert torch.equal(part[:517], full[:517])
