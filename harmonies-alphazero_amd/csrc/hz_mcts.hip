@@ -56,7 +56,8 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kMaxChildren = 69;  // measured max legal moves
-constexpr int kChildSlots = 128;  // two per lane
+constexpr int kChildSlots = 128;  // two per lane (loop bound: lanes c and c + 64)
+constexpr int kChildLds = 72;     // LDS rows per child array: every access has c < nl <= kMaxChildren
 
 inline int launch_err() {
   hipError_t e = hipGetLastError();
@@ -359,14 +360,16 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XSTAMP(k)
 #define HZ_XFLAG(k, v)
 #endif
+static_assert(kChildLds >= kMaxChildren, "child arrays hold every legal move");
+// 12.3 KB: three waves per SIMD (was 19.5 KB with 128-row arrays: two)
 struct ExpandLds {
   uint32_t mt[kMT];
-  uint64_t script[kChildSlots];
-  uint64_t state[kChildSlots][6];
-  uint64_t key[kChildSlots][8];
-  uint64_t hash[kChildSlots];
-  int32_t child[kChildSlots];
-  int32_t flag[kChildSlots];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
+  uint64_t script[kChildLds];
+  uint64_t state[kChildLds][6];
+  uint64_t key[kChildLds][8];
+  uint64_t hash[kChildLds];
+  int32_t child[kChildLds];
+  int32_t flag[kChildLds];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
 };
 
 // expand_leaf (MCTS.py:151-218) + back_fill (:220-266) + the root Dirichlet
