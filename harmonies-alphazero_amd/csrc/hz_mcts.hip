@@ -139,18 +139,22 @@ __global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__re
     int ne = m.node_ne[nb + node];
     if (ne <= 0) break;
     int e0 = m.node_e0[nb + node];
-    int n0 = 0, n1 = 0;
+    int n0 = 0, n1 = 0, c0 = 0, c1 = 0;
     double w0 = 0, w1 = 0;
     float p0 = 0, p1 = 0;
+    // each edge's child is read with its statistics (one memory round trip
+    // per level instead of a second, dependent one for the winner's child)
     if (lane < ne) {
       n0 = m.edge_n[eb + e0 + lane];
       w0 = m.edge_w[eb + e0 + lane];
       p0 = m.edge_p[eb + e0 + lane];
+      c0 = m.edge_child[eb + e0 + lane];
     }
     if (lane + kWave < ne) {
       n1 = m.edge_n[eb + e0 + lane + kWave];
       w1 = m.edge_w[eb + e0 + lane + kWave];
       p1 = m.edge_p[eb + e0 + lane + kWave];
+      c1 = m.edge_child[eb + e0 + lane + kWave];
     }
     int ns = n0 + n1;
 #pragma unroll
@@ -183,7 +187,7 @@ __global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__re
     }
     if (lane == 0) path[d] = sel;
     d++;
-    node = m.edge_child[eb + sel];
+    node = __shfl(bi < kWave ? c0 : c1, bi & (kWave - 1));  // edge_child[sel], from the winner's lane
   }
   if (lane == 0) {
     m.leaf[b] = node;
