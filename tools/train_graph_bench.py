@@ -27,9 +27,15 @@ src = TensorSource((torch.rand(M, 38, 5, 7, device="cuda", generator=g) > 0.8).f
                    torch.softmax(torch.rand(M, 143, device="cuda", generator=g), 1),
                    torch.randint(-1, 2, (M,), device="cuda", generator=g).float())
 out = {"examples": M, "batch": 64}
+CL = os.environ.get("HZ_TRAIN_CL") == "1"  # channels_last model and inputs (MIOpen NHWC kernels)
+if CL:
+    src = TensorSource(src.t[0].contiguous(memory_format=torch.channels_last), *src.t[1:])
+out["channels_last"] = CL
 for graph in (False, True, False, True):
     torch.manual_seed(0)
     mgr = ModelManager(dict(DEFAULT), tcfg)
+    if CL:
+        mgr.model.to(memory_format=torch.channels_last)
     training_phase(mgr, TensorSource(*(t[:640] for t in src.t)), 1, 64, graph=graph)  # warm the kernels
     torch.cuda.synchronize()
     t0 = time.perf_counter()
