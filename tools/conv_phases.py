@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "harmonies-alphazero_amd"))
 from hzamd.infer import pack_conv3x3, pack_conv3x3_x6  # noqa: E402
 
-lib = ctypes.CDLL(os.path.join(HERE, "libnet_diag.so"))
+lib = ctypes.CDLL(os.path.join(HERE, os.environ.get("HZ_NET_DIAG_LIB", "libnet_diag.so")))
 vp = ctypes.c_void_p
 lib.hz_conv3x3_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
 lib.hz_conv3x3_x6_bias_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
