@@ -846,6 +846,189 @@ extern "C" int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, co
   return launch_x6<2, true>(board, wpack6, bias, nullptr, out, batch, live, stream);
 }
 
+// Resident tower for small batches (config 1's one-board predict, the
+// arena's batches of a few dozen boards): one workgroup carries one state
+// through every conv of the tower (model.py:376-393, BN folded), its
+// activation never leaving LDS, the convs following each other after one
+// barrier.  A one-state conv's time is its workgroup streaming the conv's
+// 885 KB of weights into one CU (~20 us per conv layered: the B fragments
+// were loaded one K-step ahead, latency-bound); here the weight stream runs
+// kTRAhead K-steps ahead, across conv boundaries too.
+// Same arithmetic as k_conv3x3_x6<4, false, 1, 1> (8 waves of 16 output
+// channels, the state's 35 rows as 3 row blocks, the same K order and
+// epilogue), so the result is bit-identical to the layered tower.
+// LDS: two activation buffers (the conv's input, its output = the next
+// conv's input), each the state's four 32-channel chunks as bf16 planes in
+// k_conv3x3_x6's cell layout, every chunk followed by its own zero region
+// (chunk stride a multiple of 256 B: an off-board tap's offset within the
+// chunk does not depend on the chunk); the block input in fp32 for the skip
+// (35 x 128 floats).  85,504 B.
+namespace {
+constexpr int kTRZero = 31 * 256;                          // zero region of a chunk (after 35 cells)
+constexpr int kTRChunk = kTRZero + 256 + 256;              // chunk stride
+constexpr int kTRBuf = 4 * kTRChunk;                       // one activation buffer
+constexpr int kTRLds = 2 * kTRBuf + 35 * 128 * 4;          // + the fp32 skip (+ the biases)
+constexpr int kTRMaxConv = 64;
+constexpr int kTRConvW = 9 * 4 * 3 * 128 * 4;              // one conv's packed weights (bf16x8 units)
+constexpr int kTRAhead = 4;                                // K-steps of B fragments in flight
+static_assert(35 * kX6Cell <= kTRZero && kTRZero + 255 + 128 + 16 <= kTRChunk, "cells and zero region fit");
+static_assert(36 % kTRAhead == 0, "the B ring's slots repeat every conv");
+
+__global__ void __launch_bounds__(512, 1)
+    k_tower_x6_resident(const float *__restrict__ x0, const bf16x8 *__restrict__ wp,
+                        const float *__restrict__ bias, float *__restrict__ out, int32_t nconv, int32_t batch,
+                        const int32_t *__restrict__ live) {
+  extern __shared__ float4 lds4[];
+  char *lds = (char *)lds4;
+  float *skip = (float *)(lds + 2 * kTRBuf);
+  float *biasl = skip + 35 * 128;  // every conv's bias (no plain global load in the conv loop: see bissue)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4;
+  const int s = blockIdx.x;
+  if (live) batch = *live < batch ? *live : batch;
+  if (s >= batch) return;
+  for (int i = t; i < nconv * 128; i += 512) biasl[i] = bias[i];
+
+  if (t < 2 * 4 * 32) {  // every chunk's zero region (512 B = 32 float4)
+    const int c = t >> 5, k = t & 31;
+    *(float4 *)(lds + c * kTRChunk + kTRZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // the stem's output x0 (NHWC [35][128]) into buffer 0 and the skip:
+  // float4 f = cell f >> 5, channels 4 (f & 31) ..
+  const float *xs = x0 + (size_t)s * 35 * 128;
+  for (int f = t; f < 35 * 32; f += 512) {
+    const f32x4 v = *(const f32x4 *)(xs + 4 * f);
+    const int cell = f >> 5, part = f & 31;
+    uint2 h, m, l;
+    split4(v, h, m, l);
+    char *d = lds + (part >> 3) * kTRChunk + cell * kX6Cell + 8 * (part & 7);
+    *(uint2 *)d = h;
+    *(uint2 *)(d + 64) = m;
+    *(uint2 *)(d + 128) = l;
+    *(f32x4 *)(skip + 4 * f) = v;
+  }
+
+  // A fragment of row block rb, tap, chunk q: chunk base + aoff[rb][tap]
+  // (+ 64 pa), the lane's row 16 rb + (lane & 15) (clamped) as in
+  // k_conv3x3_x6; off the board the chunk's zero region at the same offset
+  // mod 256 (the chunk stride is a multiple of 256: the LDS banks the row
+  // would use)
+  int aoff[3][9];
+#pragma unroll
+  for (int rb = 0; rb < 3; rb++) {
+    int r = 16 * rb + (lane & 15);
+    r = r < 35 ? r : 34;
+    const int ch = r / 7, cw = r - 7 * ch;
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+      const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
+      const int a = r * kX6Cell + 16 * kg + ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
+      aoff[rb][tap] = hh >= 0 && hh < 5 && ww >= 0 && ww < 7 ? a : kTRZero + (a & 255);
+    }
+  }
+  const int co = 16 * w + (lane & 15);
+  const bf16x8 *wl = wp + co * 4 + kg;
+  // B fragments of conv l (clamped: the stream runs past the last conv),
+  // K-step L = q * 9 + tap, planes 0-2 (pack_conv3x3_x6 layout), requested
+  // by asm loads: the compiler would sink plain loads to their use and wait
+  // for all of them (one step in flight); program order and the explicit
+  // waits below keep kTRAhead - 1 steps in flight
+  auto bissue = [&](bf16x8(&dst)[3], int l, int L) {
+    l = l < nconv ? l : nconv - 1;
+    const int q2 = L / 9, t2 = L - 9 * q2;
+    const bf16x8 *src = wl + (size_t)l * kTRConvW + (t2 * 4 + q2) * 3 * 512;
+#pragma unroll
+    for (int p = 0; p < 3; p++) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p]) : "v"(src + p * 512));
+  };
+  // the B ring: K-step L of any conv in slot L % kTRAhead
+  bf16x8 bq[kTRAhead][3];
+#pragma unroll
+  for (int L = 0; L < kTRAhead - 1; L++) bissue(bq[L], 0, L);
+  __syncthreads();
+
+  for (int l = 0; l < nconv; l++) {
+    const char *lb = lds + (l & 1) * kTRBuf;
+    char *ob = lds + ((l + 1) & 1) * kTRBuf;
+    const float bv = biasl[l * 128 + co];
+    f32x4 acc[3] = {};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+      for (int tap = 0; tap < 9; tap++) {
+        const int L = q * 9 + tap, Lf = L + kTRAhead - 1;  // Lf: the step whose B this step requests
+        if (Lf < 36)
+          bissue(bq[Lf % kTRAhead], l, Lf);
+        else
+          bissue(bq[Lf % kTRAhead], l + 1, Lf - 36);
+        // this step's fragments have landed: only the 3 (kTRAhead - 1)
+        // requested after them may be outstanding (vmcnt counts in order)
+        bf16x8 *b = bq[L % kTRAhead];
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (kTRAhead - 1)));
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          bf16x8 a[3];
+#pragma unroll
+          for (int rb = 0; rb < 3; rb++)
+            a[rb] = *(const bf16x8 *)(lb + q * kTRChunk + aoff[rb][tap] + 64 * pa);
+#pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++)
+#pragma unroll
+            for (int rb = 0; rb < 3; rb++)
+              acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb], acc[rb], 0, 0, 0);
+        }
+      }
+    }
+    // epilogue: relu((acc + bias) [+ skip]); conv 2 of a block adds the
+    // block input and its output becomes the next block input
+    const bool second = l & 1, last = l == nconv - 1;
+    char *od = ob + (co >> 5) * kTRChunk + 2 * (co & 31);
+#pragma unroll
+    for (int rb = 0; rb < 3; rb++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int r = 16 * rb + 4 * kg + j;
+        if (r >= 35) continue;
+        float v = acc[rb][j] + bv;
+        if (second) v = v + skip[r * 128 + co];
+        v = v > 0.f ? v : 0.f;
+        if (last) {
+          out[((size_t)s * 35 + r) * 128 + co] = v;
+          continue;
+        }
+        if (second) skip[r * 128 + co] = v;
+        const uint32_t hb = bf16_bits(v);
+        const float r1 = v - bf16_value(hb);
+        const uint32_t mb = bf16_bits(r1);
+        const uint32_t lo = bf16_bits(r1 - bf16_value(mb));
+        char *d = od + r * kX6Cell;
+        *(uint16_t *)d = (uint16_t)hb;
+        *(uint16_t *)(d + 64) = (uint16_t)mb;
+        *(uint16_t *)(d + 128) = (uint16_t)lo;
+      }
+    __syncthreads();  // the output buffer is the next conv's input
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's requests past the last conv
+}
+}  // namespace
+
+extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const float *bias, float *out,
+                                    int32_t nconv, int32_t batch, const int32_t *live, void *stream) {
+  if (!x0 || !wpack6 || !bias || !out || batch < 0 || nconv < 2 || nconv > kTRMaxConv || (nconv & 1)) return -1;
+  if (((uintptr_t)x0 | (uintptr_t)wpack6 | (uintptr_t)out) & 15) return -1;
+  if (batch == 0) return 0;
+  static std::atomic<uint64_t> init_mask{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_tower_x6_resident, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kTRLds + kTRMaxConv * 128 * 4) != hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL(k_tower_x6_resident, dim3(batch), dim3(512), kTRLds + nconv * 128 * 4, (hipStream_t)stream, x0,
+                     (const bf16x8 *)wpack6, bias, out, nconv, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 #ifdef HZ_NET_DIAG
 extern "C" int hz_net_diag_stamps(uint64_t *host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;

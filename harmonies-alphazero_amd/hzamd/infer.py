@@ -77,6 +77,23 @@ def _conv3x3_act(x, wpack, b, res=None, live=None):
     return out
 
 
+def _tower_resident(x, allw, allb, live=None):
+    """The whole x6 tower in one HIP launch (hz_tower_x6_resident): allw
+    [nconv] pack_conv3x3_x6 layouts, allb [nconv][128]; bit-identical to the
+    per-conv _conv3x3_x6_act chain."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_tower_x6_resident needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    if not (allw.is_contiguous() and allb.is_contiguous() and allb.shape == (allw.shape[0], 128)):
+        raise NativeError("hz_tower_x6_resident: weights/biases of the wrong layout")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    rc = lib().hz_tower_x6_resident(x.data_ptr(), allw.data_ptr(), allb.data_ptr(), out.data_ptr(), allw.shape[0],
+                                    x.shape[0], _live_ptr(live), torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_tower_x6_resident failed ({rc})")
+    return out
+
+
 def pack_stem(w):
     """Stem weights [128][38][3][3] with the input channels zero-padded to 48,
     packed like pack_conv3x3 (hz_stem3x3_bias_act's layout)."""
@@ -230,6 +247,12 @@ class FoldedNet(nn.Module):
     # (bf16x6 split: hz_stem3x3_x6_bias_act, hz_conv3x3_x6_bias_act), "f32" =
     # the f32 MFMA (hz_stem3x3_bias_act, hz_conv3x3_bias_act)
     TOWER_MFMA = ("x6", "f32")
+    # batches of at most this many boards run the x6 tower as one resident
+    # launch (hz_tower_x6_resident; 0 = always layered).  Measured per
+    # predict (tools/resident_bench.py): 262 vs 402 us at 1 board, 986 vs
+    # 1047 us at 1024; from 1536 the layered eight-state convs win (1066 vs
+    # 1488 us: weights shared by 8 states, off-board taps skipped)
+    resident_max = 1024
 
     def __init__(self, net, epilogue=None, native_conv=True, tower="x6", fused_head=True):
         super().__init__()
@@ -253,9 +276,18 @@ class FoldedNet(nn.Module):
         if self.native_conv and self.stem[0].shape == (128, 38, 3, 3):
             self.stem_packed = pack_stem_x6(self.stem[0]) if self.tower == "x6" else pack_stem(self.stem[0])
         self.packed = None
+        self.resident = None
         if self.native_conv and self.blocks and self.blocks[0][0][0].shape[:2] == (128, 128):
             pk = pack_conv3x3_x6 if self.tower == "x6" else pack_conv3x3
-            self.packed = [(pk(w1), pk(w2)) for (w1, _), (w2, _) in self.blocks]
+            if self.tower == "x6":
+                # all convs back to back (hz_tower_x6_resident); the per-conv
+                # packs are views of it
+                allw = torch.stack([pk(w) for blk in self.blocks for (w, _) in blk])
+                self.packed = [(allw[2 * i], allw[2 * i + 1]) for i in range(len(self.blocks))]
+                if allw.shape[0] <= 64:  # the kernel's bias table holds 64 convs
+                    self.resident = (allw, torch.stack([b for blk in self.blocks for (_, b) in blk]).contiguous())
+            else:
+                self.packed = [(pk(w1), pk(w2)) for (w1, _), (w2, _) in self.blocks]
         self.pconv = _fold(n.policy_conv, n.policy_bn)
         self.vconv = _fold(n.value_conv, n.value_bn)
         # snapshots like the folded convs: an optimizer step on the source
@@ -299,7 +331,9 @@ class FoldedNet(nn.Module):
             x = (_stem_x6_act if self.tower == "x6" else _stem_act)(board, self.stem_packed, b, live)
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
-        if self.packed is not None:
+        if self.resident is not None and board.shape[0] <= self.resident_max:
+            x = _tower_resident(x, *self.resident, live)
+        elif self.packed is not None:
             conv = _conv3x3_x6_act if self.tower == "x6" else _conv3x3_act
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
                 y = conv(x, p1, b1, None, live)

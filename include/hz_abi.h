@@ -233,6 +233,15 @@ int hz_stem3x3_bias_act(const float *board, const float *wpack, const float *bia
  * (hzamd/infer.py:pack_stem_x6). */
 int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *bias, float *out, int32_t batch,
                            const int32_t *live, void *stream);
+/* The whole residual tower (model.py:332-333 over ResidualBlock.forward,
+ * model.py:376-393, BN folded) in one launch for small batches: nconv
+ * (even) convs, conv 2i without and 2i+1 with the skip of block i's input;
+ * x0 = the stem's output, out = the tower's, both NHWC [batch][5][7][128]
+ * (distinct buffers).  wpack6 = the nconv convs' pack_conv3x3_x6 layouts
+ * back to back, bias [nconv][128].  One workgroup per state, activations
+ * resident in LDS; bit-identical to nconv hz_conv3x3_x6_bias_act calls. */
+int hz_tower_x6_resident(const float *x0, const void *wpack6, const float *bias, float *out, int32_t nconv,
+                         int32_t batch, const int32_t *live, void *stream);
 
 /* The heads of model.py:336-351 up to their linear layers, BN folded:
  * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)

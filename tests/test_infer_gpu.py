@@ -401,3 +401,46 @@ def test_x6_eight_state_form_live_rows_and_accuracy():
     lv = torch.tensor([517], dtype=torch.int32, device="cuda")
     part = _conv3x3_x6_act(xc, wp, b.cuda(), rc, lv)
     assert torch.equal(part[:517], full[:517])
+
+
+@pytest.mark.parametrize("batch", [1, 5, 64, 256, 1024])
+def test_resident_tower_matches_layered_tower(batch):
+    """hz_tower_x6_resident (small batches: the whole tower in one launch,
+    activations in LDS) issues each row's products, sums and epilogue in the
+    order of the layered one-state x6 convs: logits and values bit-identical,
+    with and without a live-row bound."""
+    g = torch.Generator().manual_seed(90 + batch)
+    torch.manual_seed(batch)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    board = (torch.rand(batch, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    board[:, 37] = 1.0 / 3.0
+    glob = torch.rand(batch, 42, generator=g).cuda()
+    fnet = FoldedNet(net.cuda())
+    assert fnet.resident is not None and batch <= fnet.resident_max
+    l0, v0 = fnet(board, glob)
+    p0, pv0 = fnet.predict(board, glob)
+    fnet.resident_max = 0  # layered
+    l1, v1 = fnet(board, glob)
+    p1, pv1 = fnet.predict(board, glob)
+    assert torch.equal(l0, l1) and torch.equal(v0, v1)
+    assert torch.equal(p0, p1) and torch.equal(pv0, pv1)
+    fnet.resident_max = 1024
+    k = (batch + 1) // 2
+    live = torch.tensor([k], dtype=torch.int32, device="cuda")
+    l2, v2 = fnet(board, glob, live=live)
+    assert torch.equal(l2[:k], l0[:k]) and torch.equal(v2[:k], v0[:k])
+
+
+def test_resident_tower_reads_nothing_past_its_input():
+    """The resident tower on the prefix of a buffer whose tail is NaN."""
+    from hzamd.infer import _tower_resident
+    batch = 3
+    g = torch.Generator().manual_seed(4)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    fnet = FoldedNet(net.cuda())
+    x = torch.full((batch + 2, 128, 5, 7), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
+    x[:batch] = torch.rand(batch, 128, 5, 7, device="cuda")
+    y = _tower_resident(x[:batch], *fnet.resident)
+    assert bool(torch.isfinite(y).all())
