@@ -1029,6 +1029,190 @@ extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const f
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// Split tower for the smallest batches (config 1's one-board predict): the
+// resident tower's workgroup is bound by one CU taking in the whole tower's
+// weights (14 MB at ~62 GB/s).  Here kTSG workgroups share a state, each
+// owning 16 output channels (3 waves: the state's 3 row blocks), so each
+// reads an eighth of the weights; workgroup g of every state runs on the
+// same XCD (blocks are dealt round-robin), whose L2 then holds only that
+// eighth.  After each conv the groups exchange the activation through HBM
+// (xch, double-buffered by conv parity) with the write-through hand-off of
+// the HIP guide's Guideline 16, table row 1: every payload store sc1, each
+// storing wave drains (vmcnt 0), a barrier, ONE lane's agent-scope atomic
+// add to the state's counter; ONE lane polls it relaxed (bounded spin),
+// a barrier, and every load of the payload is an sc1 load.  The counter
+// block (sync: one 128-B line per state, then the timeout word) is zeroed
+// by a memset node ahead of every launch.  All groups of a launch must be
+// resident together: the host caps the batch (kTSMaxBatch x kTSG groups,
+// at most one per CU).
+// Per (row block, 16 channels) tile the products, sums and epilogue are
+// issued in the layered convs' order: bit-identical to them.
+namespace {
+constexpr int kTSG = 8;                       // workgroups per state
+constexpr int kTSMaxBatch = 32;               // kTSMaxBatch * kTSG <= 256 CUs
+constexpr int kTSLds = kTRBuf + kTRMaxConv * 16 * 4;  // the input activation + the group's biases
+constexpr uint64_t kTSSpinTicks = 100000000;  // 1 s at the 100 MHz s_memrealtime clock: give up
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__global__ void __launch_bounds__(192, 1)
+    k_tower_x6_split(const float *__restrict__ x0, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
+                     float *__restrict__ out, float *xch, unsigned *sync, int32_t nconv, int32_t batch,
+                     const int32_t *__restrict__ live) {
+  extern __shared__ float4 lds4[];
+  char *lds = (char *)lds4;
+  float *biasl = (float *)(lds + kTRBuf);
+  const int t = threadIdx.x, lane = t & 63, rb = t >> 6, kg = lane >> 4;
+  const int s = blockIdx.x / kTSG, g = blockIdx.x - kTSG * (blockIdx.x / kTSG);
+  int nb = batch;
+  if (live) nb = *live < batch ? *live : batch;
+  if (s >= nb) return;  // every group of a state leaves together
+
+  for (int i = t; i < nconv * 16; i += 192) biasl[i] = bias[(i >> 4) * 128 + 16 * g + (i & 15)];
+  if (t < 4 * 32) {  // every chunk's zero region
+    const int c = t >> 5, k = t & 31;
+    *(float4 *)(lds + c * kTRChunk + kTRZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto put = [&](int f, const f32x4 v) {  // float4 f of a [35][128] activation into the LDS planes
+    const int cell = f >> 5, part = f & 31;
+    uint2 h, m, l;
+    split4(v, h, m, l);
+    char *d = lds + (part >> 3) * kTRChunk + cell * kX6Cell + 8 * (part & 7);
+    *(uint2 *)d = h;
+    *(uint2 *)(d + 64) = m;
+    *(uint2 *)(d + 128) = l;
+  };
+  const float *xs = x0 + (size_t)s * 35 * 128;
+  for (int f = t; f < 35 * 32; f += 192) put(f, *(const f32x4 *)(xs + 4 * f));
+  const int co = 16 * g + (lane & 15);
+  float sk[4];  // the block input (skip) of this lane's outputs
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int r = 16 * rb + 4 * kg + j;
+    sk[j] = r < 35 ? xs[r * 128 + co] : 0.f;
+  }
+
+  int aoff[9];
+  {
+    int r = 16 * rb + (lane & 15);
+    r = r < 35 ? r : 34;
+    const int ch = r / 7, cw = r - 7 * ch;
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+      const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
+      const int a = r * kX6Cell + 16 * kg + ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
+      aoff[tap] = hh >= 0 && hh < 5 && ww >= 0 && ww < 7 ? a : kTRZero + (a & 255);
+    }
+  }
+  const bf16x8 *wl = wp + co * 4 + kg;
+  auto bissue = [&](bf16x8(&dst)[3], int l, int L) {  // as k_tower_x6_resident
+    l = l < nconv ? l : nconv - 1;
+    const int q2 = L / 9, t2 = L - 9 * q2;
+    const bf16x8 *src = wl + (size_t)l * kTRConvW + (t2 * 4 + q2) * 3 * 512;
+#pragma unroll
+    for (int p = 0; p < 3; p++) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p]) : "v"(src + p * 512));
+  };
+  bf16x8 bq[kTRAhead][3];
+#pragma unroll
+  for (int L = 0; L < kTRAhead - 1; L++) bissue(bq[L], 0, L);
+  __syncthreads();
+
+  gu32 *cnt = (gu32 *)(sync + 32 * s);
+  for (int l = 0; l < nconv; l++) {
+    const float bv = biasl[l * 16 + (lane & 15)];
+    f32x4 acc = {};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+      for (int tap = 0; tap < 9; tap++) {
+        const int L = q * 9 + tap, Lf = L + kTRAhead - 1;
+        if (Lf < 36)
+          bissue(bq[Lf % kTRAhead], l, Lf);
+        else
+          bissue(bq[Lf % kTRAhead], l + 1, Lf - 36);
+        bf16x8 *b = bq[L % kTRAhead];
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (kTRAhead - 1)));
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          const bf16x8 a = *(const bf16x8 *)(lds + q * kTRChunk + aoff[tap] + 64 * pa);
+#pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[pb], acc, 0, 0, 0);
+        }
+      }
+    }
+    const bool second = l & 1, last = l == nconv - 1;
+    float *xo = xch + ((size_t)(l & 1) * batch + s) * 35 * 128;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int r = 16 * rb + 4 * kg + j;
+      if (r >= 35) continue;
+      float v = acc[j] + bv;
+      if (second) v = v + sk[j];
+      v = v > 0.f ? v : 0.f;
+      if (second) sk[j] = v;
+      if (last)
+        out[((size_t)s * 35 + r) * 128 + co] = v;
+      else  // payload: write-through (sc1)
+        __hip_atomic_store((gu32 *)(xo + r * 128 + co), __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (last) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its payload stores
+    __syncthreads();                                    // ... and every wave is done reading the LDS planes
+    if (t == 0) {
+      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned want = kTSG * (l + 1);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kTSSpinTicks) {  // give up: flag it, finish
+          __hip_atomic_store((gu32 *)(sync + 32 * batch), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    // the whole activation (every group's channels), every load sc1
+    const float *xi = xo;
+    f32x4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      int f = t + 192 * k;
+      f = f < 35 * 32 ? f : 35 * 32 - 1;
+      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[k]) : "v"(xi + 4 * f));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]));
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+      if (t + 192 * k < 35 * 32) put(t + 192 * k, v[k]);
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's requests past the last conv
+}
+}  // namespace
+
+extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const float *bias, float *out, float *xch,
+                                 uint32_t *sync, int32_t nconv, int32_t batch, const int32_t *live, void *stream) {
+  if (!x0 || !wpack6 || !bias || !out || !xch || !sync || batch < 0 || batch > kTSMaxBatch || nconv < 2 ||
+      nconv > kTRMaxConv || (nconv & 1))
+    return -1;
+  if (((uintptr_t)x0 | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)xch | (uintptr_t)sync) & 15) return -1;
+  if (batch == 0) return 0;
+  static std::atomic<uint64_t> init_mask{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_tower_x6_split, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) !=
+        hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  // the counters and the timeout word: zeroed ahead of every launch (a memset node under capture)
+  if (hipMemsetAsync(sync, 0, (size_t)(batch + 1) * 128, (hipStream_t)stream) != hipSuccess) return 1;
+  hipLaunchKernelGGL(k_tower_x6_split, dim3(batch * kTSG), dim3(192), kTRBuf + nconv * 16 * 4, (hipStream_t)stream,
+                     x0, (const bf16x8 *)wpack6, bias, out, xch, (unsigned *)sync, nconv, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 #ifdef HZ_NET_DIAG
 extern "C" int hz_net_diag_stamps(uint64_t *host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;

@@ -94,6 +94,29 @@ def _tower_resident(x, allw, allb, live=None):
     return out
 
 
+def _tower_split(x, allw, allb, live=None, sync_out=None):
+    """_tower_resident with 8 workgroups per state (hz_tower_x6_split, batch
+    <= 32): bit-identical, the weights streamed by 8 CUs per state.
+    sync_out (list, tests): receives the counter/timeout block."""
+    B = x.shape[0]
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_tower_x6_split needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    if not (allw.is_contiguous() and allb.is_contiguous() and allb.shape == (allw.shape[0], 128)):
+        raise NativeError("hz_tower_x6_split: weights/biases of the wrong layout")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    xch = torch.empty(2 * B * 35 * 128, dtype=torch.float32, device=x.device)
+    sync = torch.empty((B + 1) * 32, dtype=torch.int32, device=x.device)
+    rc = lib().hz_tower_x6_split(x.data_ptr(), allw.data_ptr(), allb.data_ptr(), out.data_ptr(), xch.data_ptr(),
+                                 sync.data_ptr(), allw.shape[0], B, _live_ptr(live),
+                                 torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_tower_x6_split failed ({rc})")
+    if sync_out is not None:
+        sync_out.append(sync)
+    return out
+
+
 def pack_stem(w):
     """Stem weights [128][38][3][3] with the input channels zero-padded to 48,
     packed like pack_conv3x3 (hz_stem3x3_bias_act's layout)."""
@@ -253,6 +276,8 @@ class FoldedNet(nn.Module):
     # 1047 us at 1024; from 1536 the layered eight-state convs win (1066 vs
     # 1488 us: weights shared by 8 states, off-board taps skipped)
     resident_max = 1024
+    # ... and at most this many with 8 workgroups per state (hz_tower_x6_split)
+    split_max = 32
 
     def __init__(self, net, epilogue=None, native_conv=True, tower="x6", fused_head=True):
         super().__init__()
@@ -331,7 +356,9 @@ class FoldedNet(nn.Module):
             x = (_stem_x6_act if self.tower == "x6" else _stem_act)(board, self.stem_packed, b, live)
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
-        if self.resident is not None and board.shape[0] <= self.resident_max:
+        if self.resident is not None and board.shape[0] <= min(self.split_max, 32):
+            x = _tower_split(x, *self.resident, live)
+        elif self.resident is not None and board.shape[0] <= self.resident_max:
             x = _tower_resident(x, *self.resident, live)
         elif self.packed is not None:
             conv = _conv3x3_x6_act if self.tower == "x6" else _conv3x3_act

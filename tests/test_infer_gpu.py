@@ -420,12 +420,13 @@ def test_resident_tower_matches_layered_tower(batch):
     assert fnet.resident is not None and batch <= fnet.resident_max
     l0, v0 = fnet(board, glob)
     p0, pv0 = fnet.predict(board, glob)
-    fnet.resident_max = 0  # layered
+    split_max = fnet.split_max
+    fnet.resident_max = fnet.split_max = 0  # layered
     l1, v1 = fnet(board, glob)
     p1, pv1 = fnet.predict(board, glob)
     assert torch.equal(l0, l1) and torch.equal(v0, v1)
     assert torch.equal(p0, p1) and torch.equal(pv0, pv1)
-    fnet.resident_max = 1024
+    fnet.resident_max, fnet.split_max = 1024, split_max
     k = (batch + 1) // 2
     live = torch.tensor([k], dtype=torch.int32, device="cuda")
     l2, v2 = fnet(board, glob, live=live)
@@ -444,3 +445,27 @@ def test_resident_tower_reads_nothing_past_its_input():
     x[:batch] = torch.rand(batch, 128, 5, 7, device="cuda")
     y = _tower_resident(x[:batch], *fnet.resident)
     assert bool(torch.isfinite(y).all())
+
+
+@pytest.mark.parametrize("batch", [1, 3, 32])
+def test_split_tower_matches_resident_tower(batch):
+    """hz_tower_x6_split (8 workgroups per state, in-launch hand-off of each
+    conv's output) == hz_tower_x6_resident bit for bit, no workgroup timed
+    out, with a live bound too; repeated launches reuse nothing stale."""
+    from hzamd.infer import _tower_resident, _tower_split
+    g = torch.Generator().manual_seed(300 + batch)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    fnet = FoldedNet(net.cuda())
+    for rep in range(3):
+        x = torch.rand(batch, 128, 5, 7, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+        want = _tower_resident(x, *fnet.resident)
+        sync = []
+        got = _tower_split(x, *fnet.resident, sync_out=sync)
+        torch.cuda.synchronize()
+        assert int(sync[0][32 * batch]) == 0
+        assert torch.equal(got, want), rep
+    k = (batch + 1) // 2
+    live = torch.tensor([k], dtype=torch.int32, device="cuda")
+    got = _tower_split(x, *fnet.resident, live)
+    assert torch.equal(got[:k], want[:k])

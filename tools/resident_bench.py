@@ -21,8 +21,10 @@ for batch in [int(b) for b in sys.argv[1:]] or (1, 16, 64, 256, 384, 512, 768, 1
     board = (torch.rand(batch, 38, 5, 7, device="cuda") > 0.8).float()
     glob = torch.rand(batch, 42, device="cuda")
     row = {}
-    for name, rmax in (("resident", 1 << 30), ("layered", 0)):
-        fnet.resident_max = rmax
+    for name, rmax, smax in (("split", 1 << 30, 32), ("resident", 1 << 30, 0), ("layered", 0, 0)):
+        if name == "split" and batch > 32:
+            continue
+        fnet.resident_max, fnet.split_max = rmax, smax
         for _ in range(5):
             fnet.predict(board, glob)
         torch.cuda.synchronize()
