@@ -1037,7 +1037,7 @@ extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const f
 // same XCD (blocks are dealt round-robin), whose L2 then holds only that
 // eighth.  After each conv the groups exchange the activation through HBM
 // (xch, double-buffered by conv parity) with the write-through hand-off of
-// the HIP guide's Guideline 16, table row 1: every payload store sc1, each
+// the HIP guide's Guideline 16, table row 1: every payload store sc1 (16 B), each
 // storing wave drains (vmcnt 0), a barrier, ONE lane's agent-scope atomic
 // add to the state's counter; ONE lane polls it relaxed (bounded spin),
 // a barrier, and every load of the payload is an sc1 load.  The counter
@@ -1050,7 +1050,7 @@ extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const f
 namespace {
 constexpr int kTSG = 8;                       // workgroups per state
 constexpr int kTSMaxBatch = 32;               // kTSMaxBatch * kTSG <= 256 CUs
-constexpr int kTSLds = kTRBuf + kTRMaxConv * 16 * 4;  // the input activation + the group's biases
+constexpr int kTSLds = kTRBuf + kTRMaxConv * 16 * 4 + 3 * 16 * 20 * 4;  // input, biases, tiles
 constexpr uint64_t kTSSpinTicks = 100000000;  // 1 s at the 100 MHz s_memrealtime clock: give up
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -1062,6 +1062,7 @@ __global__ void __launch_bounds__(192, 1)
   char *lds = (char *)lds4;
   float *biasl = (float *)(lds + kTRBuf);
   const int t = threadIdx.x, lane = t & 63, rb = t >> 6, kg = lane >> 4;
+  float *tile = (float *)(lds + kTRBuf + kTRMaxConv * 16 * 4) + rb * 16 * 20;  // the wave's transpose tile
   const int s = blockIdx.x / kTSG, g = blockIdx.x - kTSG * (blockIdx.x / kTSG);
   int nb = batch;
   if (live) nb = *live < batch ? *live : batch;
@@ -1151,11 +1152,23 @@ __global__ void __launch_bounds__(192, 1)
       if (second) sk[j] = v;
       if (last)
         out[((size_t)s * 35 + r) * 128 + co] = v;
-      else  // payload: write-through (sc1)
-        __hip_atomic_store((gu32 *)(xo + r * 128 + co), __float_as_uint(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        tile[(4 * kg + j) * 20 + (lane & 15)] = v;
     }
     if (last) break;
+    // payload: the wave's 16 x 16 tile transposed through LDS, then one
+    // 16-B write-through (sc1) store per lane (narrow sc1 stores are one
+    // fabric write each)
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int r = 16 * rb + (lane >> 2);
+      const f32x4 v4 = *(const f32x4 *)(tile + (lane >> 2) * 20 + 4 * (lane & 3));
+      if (r < 35)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
+                     :
+                     : "v"(xo + r * 128 + 16 * g + 4 * (lane & 3)), "v"(v4)
+                     : "memory");
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its payload stores
     __syncthreads();                                    // ... and every wave is done reading the LDS planes
     if (t == 0) {
@@ -1208,7 +1221,7 @@ extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const floa
   }
   // the counters and the timeout word: zeroed ahead of every launch (a memset node under capture)
   if (hipMemsetAsync(sync, 0, (size_t)(batch + 1) * 128, (hipStream_t)stream) != hipSuccess) return 1;
-  hipLaunchKernelGGL(k_tower_x6_split, dim3(batch * kTSG), dim3(192), kTRBuf + nconv * 16 * 4, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_tower_x6_split, dim3(batch * kTSG), dim3(192), kTSLds, (hipStream_t)stream,
                      x0, (const bf16x8 *)wpack6, bias, out, xch, (unsigned *)sync, nconv, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
