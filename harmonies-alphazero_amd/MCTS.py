@@ -14,6 +14,7 @@ Moves are expanded in ascending action-index order; the reference uses
 set iteration order (PYTHONHASHSEED-dependent), see DESIGN.md.  For
 thousands of concurrent games use hzamd.mcts.BatchedMCTS / hzamd.selfplay.
 """
+import os
 import random
 
 import numpy as np
@@ -68,6 +69,11 @@ class MCTS:
 
 
 _SEARCH = {}
+# simulations 2.. of a search replay one captured HIP graph, kept across moves
+# while the network's weights do not change (hzamd.mcts.BatchedMCTS.search);
+# taken only with hzamd's ModelManager (the device-row evaluator);
+# HZ_DROPIN_GRAPH=0 runs every simulation eagerly (A/B measurements)
+GRAPH = os.environ.get("HZ_DROPIN_GRAPH", "1") != "0"
 
 
 def _search_for(sims):
@@ -100,9 +106,14 @@ class _FoldedRows:
     other model manager goes through its predict()."""
 
     device_rows = True
+    capturable = True  # HIP kernels + PyTorch ops only: one simulation is replayed as a HIP graph
 
     def __init__(self, folded):
         self.f = folded
+
+    @property
+    def graph_key(self):  # the captured simulation stays valid for this network generation
+        return self.f, self.f.generation
 
     def __call__(self, board, glob, rows=None, count=None):
         return self.f.predict(board, glob, live=count)
@@ -129,7 +140,8 @@ def get_best_action_and_pi(game_state, model_manager, mcts_config, game_move_num
         noise = torch.zeros(1, 69, dtype=torch.float64)
         noise[0, :len(vec)] = torch.from_numpy(np.asarray(vec, dtype=np.float64))
     visits = search.search(_evaluator(model_manager, br.device), float(mcts_config["cpuct"]),
-                           noise=noise, eps=float(mcts_config["dirichlet_epsilon"]), testing=testing)
+                           noise=noise, eps=float(mcts_config["dirichlet_epsilon"]), testing=testing,
+                           graph=GRAPH)
     v = visits[0].cpu().numpy().astype(np.int64)
     br.store_rng()
 

@@ -1050,7 +1050,8 @@ extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const f
 namespace {
 constexpr int kTSG = 8;                       // workgroups per state
 constexpr int kTSMaxBatch = 32;               // kTSMaxBatch * kTSG <= 256 CUs
-constexpr int kTSLds = kTRBuf + kTRMaxConv * 16 * 4 + 3 * 16 * 20 * 4;  // input, biases, tiles
+constexpr int kTSFlag = kTRBuf + kTRMaxConv * 16 * 4 + 3 * 16 * 20 * 4;  // input, biases, tiles, then
+constexpr int kTSLds = kTSFlag + 16;                                       // the timeout flag
 constexpr uint64_t kTSSpinTicks = 100000000;  // 1 s at the 100 MHz s_memrealtime clock: give up
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -1084,6 +1085,9 @@ __global__ void __launch_bounds__(192, 1)
   };
   const float *xs = x0 + (size_t)s * 35 * 128;
   for (int f = t; f < 35 * 32; f += 192) put(f, *(const f32x4 *)(xs + 4 * f));
+  int *flagl = (int *)(lds + kTSFlag);  // set by thread 0 when a hand-off wait gave up
+  if (t == 0) *flagl = 0;
+  bool failed = false;
   const int co = 16 * g + (lane & 15);
   float sk[4];  // the block input (skip) of this lane's outputs
 #pragma unroll
@@ -1150,8 +1154,8 @@ __global__ void __launch_bounds__(192, 1)
       if (second) v = v + sk[j];
       v = v > 0.f ? v : 0.f;
       if (second) sk[j] = v;
-      if (last)
-        out[((size_t)s * 35 + r) * 128 + co] = v;
+      if (last)  // a state whose hand-off timed out comes out as NaN (loud, never silently wrong)
+        out[((size_t)s * 35 + r) * 128 + co] = failed ? __builtin_nanf("") : v;
       else
         tile[(4 * kg + j) * 20 + (lane & 15)] = v;
     }
@@ -1178,12 +1182,14 @@ __global__ void __launch_bounds__(192, 1)
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTSSpinTicks) {  // give up: flag it, finish
           __hip_atomic_store((gu32 *)(sync + 32 * batch), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flagl = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
     }
     __syncthreads();
+    failed = failed || *flagl != 0;
     // the whole activation (every group's channels), every load sc1
     const float *xi = xo;
     f32x4 v[6];

@@ -293,6 +293,9 @@ class FoldedNet(nn.Module):
     @torch.no_grad()
     def refresh(self):
         n = self.src
+        # bumped on every re-fold: a captured HIP graph of this network's
+        # kernels (BatchedMCTS's cached simulation) is valid for one generation
+        self.generation = getattr(self, "generation", -1) + 1
         self.stem = _fold(n.conv, n.bn)
         self.blocks = [(_fold(b.conv1, b.bn1), _fold(b.conv2, b.bn2)) for b in n.residual_blocks]
         # the tower's 128-channel convs run as one fused HIP kernel each

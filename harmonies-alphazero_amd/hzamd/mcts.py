@@ -33,6 +33,7 @@ class BatchedMCTS:
         self.n = env.n
         self.device = env.device
         self.num_simulations = int(num_simulations)
+        self._graph_cache = None  # (key, captured simulation, network) kept by search(graph=True)
         self.max_nodes = int(max_nodes or 1 + MAX_CHILDREN * self.num_simulations)
         L = nat.lib()
         self._h = L.hz_mcts_create(self.n, self.max_nodes, int(max_depth), int(bool(exact_keys)),
@@ -160,7 +161,21 @@ class BatchedMCTS:
         total = self.num_simulations if sims is None else int(sims)
         if graph and gather and device_rows and getattr(evaluator, "capturable", False) and total > 1:
             self._device_step(evaluator, cpuct, active, noise, eps, testing, max_rows)
-            g = self._capture_step(evaluator, cpuct, active, eps, testing, max_rows)
+            # an evaluator with a graph_key (the network object and its weight
+            # generation) lets the captured simulation be kept for the next
+            # search with the same settings (the drop-in's one search per move);
+            # only without an `active` mask, whose tensor the graph would bake in
+            gk = getattr(evaluator, "graph_key", None)
+            key = None if gk is None or active is not None else (
+                id(gk[0]), gk[1], float(cpuct), float(eps), bool(testing), max_rows)
+            cached = self._graph_cache
+            if key is not None and cached is not None and cached[0] == key:
+                g = cached[1]
+            else:
+                self._graph_cache = None
+                g = self._capture_step(evaluator, cpuct, active, eps, testing, max_rows)
+                if key is not None:
+                    self._graph_cache = (key, g, gk[0])  # holds the network: its id stays unique
             for _ in range(total - 1):
                 g.replay()
             return self.result()

@@ -219,3 +219,41 @@ def test_get_best_action_and_pi_with_model_manager_device_rows(he):
         assert isinstance(MCTS._evaluator(mm, "cuda:0"), MCTS._FoldedRows)
         (m0, p0, r0), (m1, p1, r1) = out
         assert m0 == m1 and np.array_equal(p0, p1) and r0 == r1, k
+
+
+def test_get_best_action_and_pi_graph_cache(he):
+    """The drop-in search replays one captured simulation (HIP graph) kept
+    across moves; the result equals the eager search on the same positions,
+    with noise and sampling (testing=False), and after a weight change (the
+    network's generation changes: the kept graph is not reused)."""
+    import MCTS
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    from hzamd.state import apply_ref_to_object
+    from test_manager_cpu import TRAIN_CFG
+    torch.manual_seed(1)
+    mm = ModelManager(dict(DEFAULT), dict(TRAIN_CFG, device="cuda:0"))
+    f = load("mcts.npz")
+    cfg = {"num_simulations": 16, "cpuct": 2.0, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
+           "turns_until_tau0": 15, "action_size": 143, "testing": False}
+
+    def run(k, graph):
+        MCTS.GRAPH = graph
+        try:
+            obj = apply_ref_to_object(f["state"][k], he.HarmoniesGameState.__new__(he.HarmoniesGameState))
+            random.seed(int(f["mt_seed"][k]))
+            np.random.seed(k)
+            mv, pi = MCTS.get_best_action_and_pi(obj, mm, cfg, 3)
+            return mv, pi, random.getrandbits(32)
+        finally:
+            MCTS.GRAPH = True
+
+    for phase in range(2):
+        for k in range(0, 80, 16):
+            (m0, p0, r0), (m1, p1, r1) = run(k, True), run(k, False)
+            assert m0 == m1 and np.array_equal(p0, p1) and r0 == r1, (phase, k)
+        gen = mm._fast().generation
+        with torch.no_grad():
+            for prm in mm.model.parameters():
+                prm.mul_(1.5)
+        assert mm._fast().generation == gen + 1
