@@ -1052,13 +1052,16 @@ constexpr int kTSG = 8;                       // workgroups per state
 constexpr int kTSMaxBatch = 32;               // kTSMaxBatch * kTSG <= 256 CUs
 constexpr int kTSFlag = kTRBuf + kTRMaxConv * 16 * 4 + 3 * 16 * 20 * 4;  // input, biases, tiles, then
 constexpr int kTSLds = kTSFlag + 16;                                       // the timeout flag
+constexpr int kTSAhead = 4;                  // K-steps of B fragments in flight (4-18 measured alike)
 constexpr uint64_t kTSSpinTicks = 100000000;  // 1 s at the 100 MHz s_memrealtime clock: give up
 typedef __attribute__((address_space(1))) unsigned gu32;
 
+template <int Ahead>
 __global__ void __launch_bounds__(192, 1)
     k_tower_x6_split(const float *__restrict__ x0, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                      float *__restrict__ out, float *xch, unsigned *sync, int32_t nconv, int32_t batch,
                      const int32_t *__restrict__ live) {
+  static_assert(36 % Ahead == 0 && 3 * (Ahead - 1) <= 63, "the B ring's slots repeat every conv; vmcnt range");
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   float *biasl = (float *)(lds + kTRBuf);
@@ -1116,9 +1119,9 @@ __global__ void __launch_bounds__(192, 1)
 #pragma unroll
     for (int p = 0; p < 3; p++) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p]) : "v"(src + p * 512));
   };
-  bf16x8 bq[kTRAhead][3];
+  bf16x8 bq[Ahead][3];
 #pragma unroll
-  for (int L = 0; L < kTRAhead - 1; L++) bissue(bq[L], 0, L);
+  for (int L = 0; L < Ahead - 1; L++) bissue(bq[L], 0, L);
   __syncthreads();
 
   gu32 *cnt = (gu32 *)(sync + 32 * s);
@@ -1129,13 +1132,13 @@ __global__ void __launch_bounds__(192, 1)
     for (int q = 0; q < 4; q++) {
 #pragma unroll
       for (int tap = 0; tap < 9; tap++) {
-        const int L = q * 9 + tap, Lf = L + kTRAhead - 1;
+        const int L = q * 9 + tap, Lf = L + Ahead - 1;
         if (Lf < 36)
-          bissue(bq[Lf % kTRAhead], l, Lf);
+          bissue(bq[Lf % Ahead], l, Lf);
         else
-          bissue(bq[Lf % kTRAhead], l + 1, Lf - 36);
-        bf16x8 *b = bq[L % kTRAhead];
-        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (kTRAhead - 1)));
+          bissue(bq[Lf % Ahead], l + 1, Lf - 36);
+        bf16x8 *b = bq[L % Ahead];
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (Ahead - 1)));
 #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
           const bf16x8 a = *(const bf16x8 *)(lds + q * kTRChunk + aoff[tap] + 64 * pa);
@@ -1216,19 +1219,38 @@ extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const floa
     return -1;
   if (((uintptr_t)x0 | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)xch | (uintptr_t)sync) & 15) return -1;
   if (batch == 0) return 0;
+  // K-steps of B fragments in flight (HZ_TS_AHEAD: 4, 6, 9, 12 or 18 for
+  // measurements; at one state per 8 CUs the weight stream is latency-bound)
+  static const int ahead = [] {
+    const char *e = getenv("HZ_TS_AHEAD");
+    const int v = e ? atoi(e) : kTSAhead;
+    return v == 4 || v == 6 || v == 9 || v == 12 || v == 18 ? v : kTSAhead;
+  }();
+  const void *fn = ahead == 4    ? (const void *)k_tower_x6_split<4>
+                   : ahead == 6  ? (const void *)k_tower_x6_split<6>
+                   : ahead == 9  ? (const void *)k_tower_x6_split<9>
+                   : ahead == 18 ? (const void *)k_tower_x6_split<18>
+                                 : (const void *)k_tower_x6_split<12>;
   static std::atomic<uint64_t> init_mask{0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_tower_x6_split, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) !=
-        hipSuccess)
-      return 1;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) != hipSuccess) return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
   // the counters and the timeout word: zeroed ahead of every launch (a memset node under capture)
   if (hipMemsetAsync(sync, 0, (size_t)(batch + 1) * 128, (hipStream_t)stream) != hipSuccess) return 1;
-  hipLaunchKernelGGL(k_tower_x6_split, dim3(batch * kTSG), dim3(192), kTSLds, (hipStream_t)stream,
-                     x0, (const bf16x8 *)wpack6, bias, out, xch, (unsigned *)sync, nconv, batch, live);
+  const bf16x8 *wp = (const bf16x8 *)wpack6;
+  unsigned *sy = (unsigned *)sync;
+  const dim3 grid(batch * kTSG), block(192);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (ahead) {
+    case 4: hipLaunchKernelGGL(k_tower_x6_split<4>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+    case 6: hipLaunchKernelGGL(k_tower_x6_split<6>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+    case 9: hipLaunchKernelGGL(k_tower_x6_split<9>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+    case 18: hipLaunchKernelGGL(k_tower_x6_split<18>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+    default: hipLaunchKernelGGL(k_tower_x6_split<12>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -1502,6 +1524,121 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
 #undef HZ_HSTAMP
 #undef HZ_HSTAMP_RT
 
+// The same head for the smallest batches (config 1's one-board predict, the
+// arena's few dozen rows): one state per 1024-thread workgroup, every layer
+// split over the inputs so that each thread has at most 20 weight loads,
+// all in flight at once (k_heads_fc's 8-state workgroup walks its weight
+// rows in 8 + 7 dependent blocks: ~24 us at any batch up to 8).  Partial
+// sums are added in a fixed order; results agree with k_heads_fc to fp32
+// rounding (different summation order).
+constexpr int kH1Max = 64;  // batches up to this take k_heads_fc1 (HZ_HEADS1_MAX overrides)
+__global__ void __launch_bounds__(1024) k_heads_fc1(const float *__restrict__ x, const float *__restrict__ glob,
+                                                    const float *__restrict__ hw, const float *__restrict__ hb,
+                                                    const float *__restrict__ wpT, const float *__restrict__ bp,
+                                                    const float *__restrict__ w1T, const float *__restrict__ b1,
+                                                    const float *__restrict__ w2, const float *__restrict__ b2,
+                                                    float *__restrict__ logits, float *__restrict__ probs,
+                                                    float *__restrict__ value, int32_t batch,
+                                                    const int32_t *__restrict__ live) {
+  __shared__ float c1p[105][9];  // 1x1 convs: (head channel, cell) x 8 channel chunks (+1 pad)
+  __shared__ float pin[kPIn], vin[kVIn];
+  __shared__ float p2[7][kAct];  // policy: 7 chunks of 16 inputs
+  __shared__ float p3[4][kHid];  // value: 4 chunks of 20 (the last 17) inputs
+  __shared__ float lg[kAct + 1];
+  __shared__ float vpart[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (live) batch = *live < batch ? *live : batch;
+  const int s = blockIdx.x;
+  if (s >= batch) return;
+  // 1. the heads' 1x1 convs: output o = head channel * 35 + cell, 16 input channels per thread
+  if (t < 105 * 8) {
+    const int o = t >> 3, part = t & 7, hc = o / 35, cell = o - 35 * hc;
+    const float4 *xv = (const float4 *)(x + ((size_t)s * 35 + cell) * 128 + 16 * part);
+    const float4 *wv = (const float4 *)(hw + hc * 128 + 16 * part);
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const float4 u = xv[k], q = wv[k];
+      a += u.x * q.x + u.y * q.y + u.z * q.z + u.w * q.w;
+    }
+    c1p[o][part] = a;
+  } else if (t < 105 * 8 + kGlob) {
+    const float v = glob[(size_t)s * kGlob + t - 105 * 8];
+    pin[70 + t - 105 * 8] = v;
+    vin[35 + t - 105 * 8] = v;
+  }
+  __syncthreads();
+  if (t < 105) {
+    const int hc = t / 35, cell = t - 35 * hc;
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) a += c1p[t][k];
+    a += hb[hc];
+    a = a > 0.f ? a : 0.f;
+    if (hc < 2)
+      pin[t] = a;
+    else
+      vin[cell] = a;
+  }
+  __syncthreads();
+  // 2. policy partials (t < 1001: chunk t / 143 of 16 inputs, column t % 143)
+  //    and value partials (all threads: chunk t / 256, hidden unit t % 256)
+  float pp = 0.f, vp = 0.f;
+  const int pc = t / kAct, pcol = t - kAct * pc;
+  if (pc < 7) {
+    float wr[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) wr[j] = wpT[(size_t)(16 * pc + j) * kAct + pcol];
+#pragma unroll
+    for (int j = 0; j < 16; j++) pp += wr[j] * pin[16 * pc + j];
+  }
+  {
+    const int vc = t >> 8, u = t & 255, j0 = 20 * vc, nj = vc < 3 ? 20 : kVIn - 60;
+    float wr[20];
+#pragma unroll
+    for (int j = 0; j < 20; j++) wr[j] = j < nj ? w1T[(size_t)(j0 + j) * kHid + u] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 20; j++)
+      if (j < nj) vp += wr[j] * vin[j0 + j];
+    p3[vc][u] = vp;
+  }
+  if (pc < 7) p2[pc][pcol] = pp;
+  __syncthreads();
+  if (t < kAct) {
+    float a = p2[0][t];
+#pragma unroll
+    for (int c = 1; c < 7; c++) a += p2[c][t];
+    lg[t] = a + bp[t];
+  } else if (t >= 256 && t < 512) {
+    const int u = t - 256;
+    float h = ((p3[0][u] + p3[1][u]) + (p3[2][u] + p3[3][u])) + b1[u];
+    h = h > 0.f ? h : 0.f;
+    const float c = wave_sum(h * w2[u]);
+    if (lane == 0) vpart[w - 4] = c;
+  }
+  __syncthreads();
+  // 3. value (tanh) and the softmax over all 143 logits (model.py:104)
+  if (w == 1 && lane == 0) value[s] = tanhf(((vpart[0] + vpart[1]) + (vpart[2] + vpart[3])) + b2[0]);
+  if (w == 0) {
+    const bool has2 = lane + 128 < kAct;
+    const float l0 = lg[lane], l1 = lg[lane + 64], l2 = has2 ? lg[lane + 128] : -INFINITY;
+    const size_t o = (size_t)s * kAct;
+    if (logits) {
+      logits[o + lane] = l0;
+      logits[o + lane + 64] = l1;
+      if (has2) logits[o + lane + 128] = l2;
+    }
+    if (probs) {
+      const float m = wave_max(fmaxf(fmaxf(l0, l1), l2));
+      const float e0 = expf(l0 - m), e1 = expf(l1 - m), e2 = has2 ? expf(l2 - m) : 0.f;
+      const float inv = 1.f / wave_sum((e0 + e1) + e2);
+      probs[o + lane] = e0 * inv;
+      probs[o + lane + 64] = e1 * inv;
+      if (has2) probs[o + lane + 128] = e2 * inv;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int hz_heads_fc(const float *x, const float *glob, const float *hw, const float *hb, const float *wpT,
@@ -1511,8 +1648,16 @@ extern "C" int hz_heads_fc(const float *x, const float *glob, const float *hw, c
   if (!x || !glob || !hw || !hb || !wpT || !bp || !w1T || !b1 || !w2 || !b2 || !value || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)hw) & 15) return -1;
   if (batch == 0) return 0;
-  hipLaunchKernelGGL(k_heads_fc, dim3((batch + kHS - 1) / kHS), dim3(256), 0, (hipStream_t)stream, x, glob, hw,
-                     hb, wpT, bp, w1T, b1, w2, b2, logits, probs, value, batch, live);
+  static const int32_t h1max = [] {
+    const char *e = getenv("HZ_HEADS1_MAX");
+    return e ? (int32_t)atoi(e) : (int32_t)kH1Max;
+  }();
+  if (batch <= h1max)
+    hipLaunchKernelGGL(k_heads_fc1, dim3(batch), dim3(1024), 0, (hipStream_t)stream, x, glob, hw, hb, wpT, bp, w1T,
+                       b1, w2, b2, logits, probs, value, batch, live);
+  else
+    hipLaunchKernelGGL(k_heads_fc, dim3((batch + kHS - 1) / kHS), dim3(256), 0, (hipStream_t)stream, x, glob, hw,
+                       hb, wpT, bp, w1T, b1, w2, b2, logits, probs, value, batch, live);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
