@@ -50,6 +50,7 @@ struct hz_mcts {
   int32_t *leaf_gidx;    // [n]  b*max_nodes + leaf for the encoder, -1 = no eval
   int32_t *slot;         // [n]  row of board b in the gathered leaf batch, -1 = not evaluated
   int32_t *gidx_c;       // [n]  leaf_gidx of the gathered rows, in board order
+  int64_t *eval_ctr;     // optional (hz_mcts_set_eval_counter): k_gather adds each simulation's row count
 };
 
 namespace {
@@ -232,7 +233,10 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
       m.slot[b] = -1;
     }
   }
-  if (t == kGatherThreads - 1) count[0] = part[t];
+  if (t == kGatherThreads - 1) {
+    count[0] = part[t];
+    if (m.eval_ctr) m.eval_ctr[0] += part[t];  // one workgroup, stream-ordered: no atomic needed
+  }
 }
 
 // ------------------------------------------------ turn-end chance, in parallel
@@ -695,6 +699,12 @@ void hz_mcts_destroy(hz_mcts *m) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   free(m);
+}
+
+int hz_mcts_set_eval_counter(hz_mcts *m, int64_t *counter) {
+  if (!m) return -1;
+  m->eval_ctr = counter;
+  return 0;
 }
 
 int hz_mcts_set_stream(hz_mcts *m, void *stream) {

@@ -48,6 +48,8 @@ class BatchedMCTS:
         self.rows = torch.zeros(self.n, dtype=torch.int32, device=d)
         self.count = torch.zeros(1, dtype=torch.int32, device=d)
         self.eval_rows = torch.zeros(1, dtype=torch.int64, device=d)  # leaves evaluated, last search
+        # k_gather adds each simulation's gathered row count to it (no extra kernel)
+        nat.check(L.hz_mcts_set_eval_counter(self._h, nat.ptr(self.eval_rows)), "hz_mcts_set_eval_counter")
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
         self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
 
@@ -111,8 +113,7 @@ class BatchedMCTS:
     def _device_step(self, evaluator, cpuct, active, noise, eps, testing, max_rows=None):
         """One simulation with a device-row evaluator: no host round trip."""
         self.select(cpuct, active)
-        board, glob, rows, count = self.gather_leaves()
-        self.eval_rows += count
+        board, glob, rows, count = self.gather_leaves()  # (adds count to eval_rows)
         if max_rows is not None:  # the live rows are a prefix of at most max_rows
             board, glob = board[:max_rows], glob[:max_rows]
         policy, value = evaluator(board, glob, rows, count)
@@ -187,8 +188,7 @@ class BatchedMCTS:
                 self.eval_rows += self.n
                 self.expand_backup(policy, value, noise, eps, testing)
                 continue
-            board, glob, rows, count = self.gather_leaves()
-            self.eval_rows += count
+            board, glob, rows, count = self.gather_leaves()  # (adds count to eval_rows)
             if device_rows:
                 if max_rows is not None:
                     board, glob = board[:max_rows], glob[:max_rows]

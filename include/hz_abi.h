@@ -176,6 +176,10 @@ int hz_mcts_encode_leaves(hz_mcts *mcts, float *board, float *glob);
  * leaf-eval kernels below take `count` as their live-row bound.  Pair with
  * hz_mcts_expand_backup_gathered. */
 int hz_mcts_gather_leaves(hz_mcts *mcts, float *board, float *glob, int32_t *rows, int32_t *count);
+/* counter (device int64, may be NULL to detach): every later
+ * hz_mcts_gather_leaves adds its row count k to counter[0] on the device
+ * (the number of leaf evaluations of a search without a separate kernel). */
+int hz_mcts_set_eval_counter(hz_mcts *mcts, int64_t *counter);
 /* expand_leaf (MCTS.py:151-218) with policy[n][143] (probabilities, as
  * ModelManager.predict returns them, model.py:81-110), root Dirichlet mix
  * (MCTS.py:308-327) when !testing using noise[n][69] (i-th legal move), then
