@@ -18,6 +18,8 @@ fp32; the results differ from the unfolded graph only by fp32 rounding
 (tests/test_infer_gpu.py states the tolerance).  Rebuild (or call refresh())
 after the weights change.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -275,9 +277,9 @@ class FoldedNet(nn.Module):
     # predict (tools/resident_bench.py): 262 vs 402 us at 1 board, 986 vs
     # 1047 us at 1024; from 1536 the layered eight-state convs win (1066 vs
     # 1488 us: weights shared by 8 states, off-board taps skipped)
-    resident_max = 1024
+    resident_max = int(os.environ.get("HZ_RESIDENT_MAX", "1024"))  # (A/B measurements)
     # ... and at most this many with 8 workgroups per state (hz_tower_x6_split)
-    split_max = 32
+    split_max = int(os.environ.get("HZ_SPLIT_MAX", "32"))
 
     def __init__(self, net, epilogue=None, native_conv=True, tower="x6", fused_head=True):
         super().__init__()
