@@ -1052,22 +1052,40 @@ constexpr int kTSG = 8;                       // workgroups per state
 constexpr int kTSMaxBatch = 32;               // kTSMaxBatch * kTSG <= 256 CUs
 constexpr int kTSFlag = kTRBuf + kTRMaxConv * 16 * 4 + 3 * 16 * 20 * 4;  // input, biases, tiles, then
 constexpr int kTSLds = kTSFlag + 16;                                       // the timeout flag
+constexpr int kTSAAhead = 2;                 // K-steps of A fragments read ahead from LDS
+constexpr int kTSRb1Max = 10;                // batches up to this: one row block per workgroup
 constexpr int kTSAhead = 4;                  // K-steps of B fragments in flight (4-18 measured alike)
 constexpr uint64_t kTSSpinTicks = 100000000;  // 1 s at the 100 MHz s_memrealtime clock: give up
 typedef __attribute__((address_space(1))) unsigned gu32;
+#ifdef HZ_NET_DIAG  // per conv phase stamps of state 0's groups (tools/split_phases.py)
+__device__ uint64_t g_split_stamps[8][64][6];
+#define HZ_SSTAMP(k) \
+  if (t == 0 && s == 0 && l < 64) g_split_stamps[g][l][k] = __builtin_amdgcn_s_memtime();
+#else
+#define HZ_SSTAMP(k)
+#endif
 
-template <int Ahead>
+template <int Ahead, int RBG>
 __global__ void __launch_bounds__(192, 1)
     k_tower_x6_split(const float *__restrict__ x0, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                      float *__restrict__ out, float *xch, unsigned *sync, int32_t nconv, int32_t batch,
                      const int32_t *__restrict__ live) {
   static_assert(36 % Ahead == 0 && 3 * (Ahead - 1) <= 63, "the B ring's slots repeat every conv; vmcnt range");
+  // RBG = row blocks per workgroup: 3 (wave w computes row block w; kTSG groups
+  // per state) or 1 (the group owns one row block, computed by wave 0; 3 *
+  // kTSG groups per state, so a CU streams its B fragments once instead of
+  // three times; the other waves only share the staging)
+  static_assert(RBG == 3 || RBG == 1, "3 or 1 row blocks per workgroup");
+  constexpr int G = kTSG * 3 / RBG;  // workgroups per state
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   float *biasl = (float *)(lds + kTRBuf);
-  const int t = threadIdx.x, lane = t & 63, rb = t >> 6, kg = lane >> 4;
-  float *tile = (float *)(lds + kTRBuf + kTRMaxConv * 16 * 4) + rb * 16 * 20;  // the wave's transpose tile
-  const int s = blockIdx.x / kTSG, g = blockIdx.x - kTSG * (blockIdx.x / kTSG);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4;
+  // group g of every state on XCD g (blocks are dealt round-robin)
+  const int s = blockIdx.x / G, g = blockIdx.x % kTSG;
+  const int rb = RBG == 3 ? w : (blockIdx.x / kTSG) % 3;
+  const bool compute = RBG == 3 || w == 0;  // wave-uniform
+  float *tile = (float *)(lds + kTRBuf + kTRMaxConv * 16 * 4) + (RBG == 3 ? w : 0) * 16 * 20;  // transpose tile
   int nb = batch;
   if (live) nb = *live < batch ? *live : batch;
   if (s >= nb) return;  // every group of a state leaves together
@@ -1120,35 +1138,48 @@ __global__ void __launch_bounds__(192, 1)
     for (int p = 0; p < 3; p++) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p]) : "v"(src + p * 512));
   };
   bf16x8 bq[Ahead][3];
+  if (compute) {
 #pragma unroll
-  for (int L = 0; L < Ahead - 1; L++) bissue(bq[L], 0, L);
+    for (int L = 0; L < Ahead - 1; L++) bissue(bq[L], 0, L);
+  }
   __syncthreads();
 
   gu32 *cnt = (gu32 *)(sync + 32 * s);
   for (int l = 0; l < nconv; l++) {
-    const float bv = biasl[l * 16 + (lane & 15)];
-    f32x4 acc = {};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-#pragma unroll
-      for (int tap = 0; tap < 9; tap++) {
-        const int L = q * 9 + tap, Lf = L + Ahead - 1;
-        if (Lf < 36)
-          bissue(bq[Lf % Ahead], l, Lf);
-        else
-          bissue(bq[Lf % Ahead], l + 1, Lf - 36);
-        bf16x8 *b = bq[L % Ahead];
-        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (Ahead - 1)));
-#pragma unroll
-        for (int pa = 0; pa < 3; pa++) {
-          const bf16x8 a = *(const bf16x8 *)(lds + q * kTRChunk + aoff[tap] + 64 * pa);
-#pragma unroll
-          for (int pb = 0; pb < 3 - pa; pb++) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[pb], acc, 0, 0, 0);
-        }
-      }
-    }
+    HZ_SSTAMP(0)
     const bool second = l & 1, last = l == nconv - 1;
     float *xo = xch + ((size_t)(l & 1) * batch + s) * 35 * 128;
+    if (compute) {
+    const float bv = biasl[l * 16 + (lane & 15)];
+    f32x4 acc = {};
+    // A fragments kTSAAhead K-steps ahead (a ring of kTSAAhead + 1 slots):
+    // with the reads issued just before their MFMAs, every K-step paid the
+    // LDS latency (~275 cycles per K-step against 96 of MFMA issue)
+    bf16x8 af[kTSAAhead + 1][3];
+    auto aread = [&](bf16x8(&dst)[3], int L) {
+      const int q2 = L / 9, t2 = L - 9 * q2;
+#pragma unroll
+      for (int pa = 0; pa < 3; pa++) dst[pa] = *(const bf16x8 *)(lds + q2 * kTRChunk + aoff[t2] + 64 * pa);
+    };
+#pragma unroll
+    for (int L = 0; L < kTSAAhead; L++) aread(af[L], L);
+#pragma unroll
+    for (int L = 0; L < 36; L++) {
+      const int Lf = L + Ahead - 1;
+      if (Lf < 36)
+        bissue(bq[Lf % Ahead], l, Lf);
+      else
+        bissue(bq[Lf % Ahead], l + 1, Lf - 36);
+      if (L + kTSAAhead < 36) aread(af[(L + kTSAAhead) % (kTSAAhead + 1)], L + kTSAAhead);
+      bf16x8 *b = bq[L % Ahead];
+      asm volatile("s_waitcnt vmcnt(%3)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]) : "n"(3 * (Ahead - 1)));
+      const bf16x8 *a = af[L % (kTSAAhead + 1)];
+#pragma unroll
+      for (int pa = 0; pa < 3; pa++)
+#pragma unroll
+        for (int pb = 0; pb < 3 - pa; pb++) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[pa], b[pb], acc, 0, 0, 0);
+    }
+    HZ_SSTAMP(1)
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int r = 16 * rb + 4 * kg + j;
@@ -1162,12 +1193,11 @@ __global__ void __launch_bounds__(192, 1)
       else
         tile[(4 * kg + j) * 20 + (lane & 15)] = v;
     }
-    if (last) break;
     // payload: the wave's 16 x 16 tile transposed through LDS, then one
     // 16-B write-through (sc1) store per lane (narrow sc1 stores are one
     // fabric write each)
-    __builtin_amdgcn_wave_barrier();
-    {
+    if (!last) {
+      __builtin_amdgcn_wave_barrier();
       const int r = 16 * rb + (lane >> 2);
       const f32x4 v4 = *(const f32x4 *)(tile + (lane >> 2) * 20 + 4 * (lane & 3));
       if (r < 35)
@@ -1176,11 +1206,14 @@ __global__ void __launch_bounds__(192, 1)
                      : "v"(xo + r * 128 + 16 * g + 4 * (lane & 3)), "v"(v4)
                      : "memory");
     }
+    }  // compute
+    if (last) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its payload stores
+    HZ_SSTAMP(2)
     __syncthreads();                                    // ... and every wave is done reading the LDS planes
     if (t == 0) {
       __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned want = kTSG * (l + 1);
+      const unsigned want = G * (l + 1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTSSpinTicks) {  // give up: flag it, finish
@@ -1191,6 +1224,7 @@ __global__ void __launch_bounds__(192, 1)
         __builtin_amdgcn_s_sleep(1);
       }
     }
+    HZ_SSTAMP(3)
     __syncthreads();
     failed = failed || *flagl != 0;
     // the whole activation (every group's channels), every load sc1
@@ -1206,7 +1240,9 @@ __global__ void __launch_bounds__(192, 1)
 #pragma unroll
     for (int k = 0; k < 6; k++)
       if (t + 192 * k < 35 * 32) put(t + 192 * k, v[k]);
+    HZ_SSTAMP(4)
     __syncthreads();
+    HZ_SSTAMP(5)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's requests past the last conv
 }
@@ -1219,42 +1255,54 @@ extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const floa
     return -1;
   if (((uintptr_t)x0 | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)xch | (uintptr_t)sync) & 15) return -1;
   if (batch == 0) return 0;
-  // K-steps of B fragments in flight (HZ_TS_AHEAD: 4, 6, 9, 12 or 18 for
-  // measurements; at one state per 8 CUs the weight stream is latency-bound)
+  // K-steps of B fragments in flight (HZ_TS_AHEAD=12 for measurements; 4,
+  // 6, 9, 12 and 18 measured alike with three row blocks per workgroup)
   static const int ahead = [] {
     const char *e = getenv("HZ_TS_AHEAD");
-    const int v = e ? atoi(e) : kTSAhead;
-    return v == 4 || v == 6 || v == 9 || v == 12 || v == 18 ? v : kTSAhead;
+    return e && atoi(e) == 12 ? 12 : kTSAhead;
   }();
-  const void *fn = ahead == 4    ? (const void *)k_tower_x6_split<4>
-                   : ahead == 6  ? (const void *)k_tower_x6_split<6>
-                   : ahead == 9  ? (const void *)k_tower_x6_split<9>
-                   : ahead == 18 ? (const void *)k_tower_x6_split<18>
-                                 : (const void *)k_tower_x6_split<12>;
+  // one row block per workgroup (3 x kTSG groups per state) up to this batch
+  // (HZ_TS_RB1_MAX; at most 256 / (3 x kTSG) so that every group is resident)
+  static const int rb1max = [] {
+    const char *e = getenv("HZ_TS_RB1_MAX");
+    const int v = e ? atoi(e) : kTSRb1Max;
+    return v < 0 ? 0 : v > 256 / (3 * kTSG) ? 256 / (3 * kTSG) : v;
+  }();
+  const bool rb1 = batch <= rb1max;
   static std::atomic<uint64_t> init_mask{0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) != hipSuccess) return 1;
+    for (const void *f : {(const void *)k_tower_x6_split<4, 1>, (const void *)k_tower_x6_split<12, 1>,
+                          (const void *)k_tower_x6_split<4, 3>, (const void *)k_tower_x6_split<12, 3>})
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) != hipSuccess) return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
   // the counters and the timeout word: zeroed ahead of every launch (a memset node under capture)
   if (hipMemsetAsync(sync, 0, (size_t)(batch + 1) * 128, (hipStream_t)stream) != hipSuccess) return 1;
   const bf16x8 *wp = (const bf16x8 *)wpack6;
   unsigned *sy = (unsigned *)sync;
-  const dim3 grid(batch * kTSG), block(192);
+  const dim3 grid(batch * kTSG * (rb1 ? 3 : 1)), block(192);
   const hipStream_t st = (hipStream_t)stream;
-  switch (ahead) {
-    case 4: hipLaunchKernelGGL(k_tower_x6_split<4>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
-    case 6: hipLaunchKernelGGL(k_tower_x6_split<6>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
-    case 9: hipLaunchKernelGGL(k_tower_x6_split<9>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
-    case 18: hipLaunchKernelGGL(k_tower_x6_split<18>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
-    default: hipLaunchKernelGGL(k_tower_x6_split<12>, grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live); break;
+  if (rb1) {
+    if (ahead == 4)
+      hipLaunchKernelGGL((k_tower_x6_split<4, 1>), grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live);
+    else
+      hipLaunchKernelGGL((k_tower_x6_split<12, 1>), grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live);
+  } else {
+    if (ahead == 4)
+      hipLaunchKernelGGL((k_tower_x6_split<4, 3>), grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live);
+    else
+      hipLaunchKernelGGL((k_tower_x6_split<12, 3>), grid, block, kTSLds, st, x0, wp, bias, out, xch, sy, nconv, batch, live);
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 #ifdef HZ_NET_DIAG
+extern "C" int hz_net_diag_split_stamps(uint64_t *host) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_split_stamps), sizeof(g_split_stamps)) == hipSuccess ? 0 : 1;
+}
 extern "C" int hz_net_diag_stamps(uint64_t *host) {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), sizeof(g_conv_stamps)) == hipSuccess ? 0 : 1;

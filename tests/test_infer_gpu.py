@@ -447,9 +447,10 @@ def test_resident_tower_reads_nothing_past_its_input():
     assert bool(torch.isfinite(y).all())
 
 
-@pytest.mark.parametrize("batch", [1, 3, 32])
+@pytest.mark.parametrize("batch", [1, 3, 10, 11, 32])
 def test_split_tower_matches_resident_tower(batch):
-    """hz_tower_x6_split (8 workgroups per state, in-launch hand-off of each
+    """hz_tower_x6_split (24 one-row-block workgroups per state up to 10
+    states, else 8 three-row-block ones; in-launch hand-off of each
     conv's output) == hz_tower_x6_resident bit for bit, no workgroup timed
     out, with a live bound too; repeated launches reuse nothing stale."""
     from hzamd.infer import _tower_resident, _tower_split
