@@ -1041,8 +1041,10 @@ extern "C" int hz_tower_x6_resident(const float *x0, const void *wpack6, const f
 // storing wave drains (vmcnt 0), a barrier, ONE lane's agent-scope atomic
 // add to the state's counter; ONE lane polls it relaxed (bounded spin),
 // a barrier, and every load of the payload is an sc1 load.  The counter
-// block (sync: one 128-B line per state, then the timeout word) is zeroed
-// by a memset node ahead of every launch.  All groups of a launch must be
+// block (sync: one 128-B line per state holding its hand-off counter and
+// its done counter; the timeout word at line kTSMaxBatch) is zeroed once by
+// the caller, and the last group of a state to finish zeroes the state's
+// counters again (no memset ahead of each launch).  All groups of a launch must be
 // resident together: the host caps the batch (kTSMaxBatch x kTSG groups,
 // at most one per CU).
 // Per (row block, 16 channels) tile the products, sums and epilogue are
@@ -1207,7 +1209,15 @@ __global__ void __launch_bounds__(192, 1)
                      : "memory");
     }
     }  // compute
-    if (last) break;
+    if (last) {
+      // the state's last group to get here (every group is past its last
+      // wait) zeroes the state's counters for the next launch
+      if (t == 0 && __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its payload stores
     HZ_SSTAMP(2)
     __syncthreads();                                    // ... and every wave is done reading the LDS planes
@@ -1217,7 +1227,7 @@ __global__ void __launch_bounds__(192, 1)
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTSSpinTicks) {  // give up: flag it, finish
-          __hip_atomic_store((gu32 *)(sync + 32 * batch), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gu32 *)(sync + 32 * kTSMaxBatch), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           *flagl = 1;
           break;
         }
@@ -1278,8 +1288,6 @@ extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const floa
       if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kTSLds) != hipSuccess) return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
-  // the counters and the timeout word: zeroed ahead of every launch (a memset node under capture)
-  if (hipMemsetAsync(sync, 0, (size_t)(batch + 1) * 128, (hipStream_t)stream) != hipSuccess) return 1;
   const bf16x8 *wp = (const bf16x8 *)wpack6;
   unsigned *sy = (unsigned *)sync;
   const dim3 grid(batch * kTSG * (rb1 ? 3 : 1)), block(192);

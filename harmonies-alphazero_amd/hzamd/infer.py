@@ -96,9 +96,20 @@ def _tower_resident(x, allw, allb, live=None):
     return out
 
 
+_SPLIT_SYNC = {}  # device -> the hand-off counter block (zeroed once; every launch leaves it zeroed)
+
+
+def _split_sync(device):
+    t = _SPLIT_SYNC.get(device)
+    if t is None:
+        t = _SPLIT_SYNC[device] = torch.zeros(33 * 32, dtype=torch.int32, device=device)
+    return t
+
+
 def _tower_split(x, allw, allb, live=None, sync_out=None):
-    """_tower_resident with 8 workgroups per state (hz_tower_x6_split, batch
-    <= 32): bit-identical, the weights streamed by 8 CUs per state.
+    """_tower_resident with 24 or 8 workgroups per state (hz_tower_x6_split,
+    batch <= 32): bit-identical, the weights streamed by 8 CUs per state.
+    The counter block is shared per device: calls run in stream order.
     sync_out (list, tests): receives the counter/timeout block."""
     B = x.shape[0]
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
@@ -108,7 +119,7 @@ def _tower_split(x, allw, allb, live=None, sync_out=None):
         raise NativeError("hz_tower_x6_split: weights/biases of the wrong layout")
     out = torch.empty_like(x, memory_format=torch.channels_last)
     xch = torch.empty(2 * B * 35 * 128, dtype=torch.float32, device=x.device)
-    sync = torch.empty((B + 1) * 32, dtype=torch.int32, device=x.device)
+    sync = _split_sync(x.device)
     rc = lib().hz_tower_x6_split(x.data_ptr(), allw.data_ptr(), allb.data_ptr(), out.data_ptr(), xch.data_ptr(),
                                  sync.data_ptr(), allw.shape[0], B, _live_ptr(live),
                                  torch.cuda.current_stream(x.device).cuda_stream)

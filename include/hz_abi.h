@@ -246,11 +246,13 @@ int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *
  * resident in LDS; bit-identical to nconv hz_conv3x3_x6_bias_act calls. */
 int hz_tower_x6_resident(const float *x0, const void *wpack6, const float *bias, float *out, int32_t nconv,
                          int32_t batch, const int32_t *live, void *stream);
-/* hz_tower_x6_resident for batch <= 32 with 8 workgroups per state (16
- * output channels each) exchanging each conv's output through HBM in-launch:
- * xch = scratch of 2 * batch * 35 * 128 floats, sync = (batch + 1) * 32
- * words (zeroed by the call; after it, sync[32 * batch] != 0 means a
- * workgroup gave up waiting, 1 s, and the output is invalid).  Bit-identical
+/* hz_tower_x6_resident for batch <= 32 with 24 (batch <= 10) or 8
+ * workgroups per state (16 output channels each) exchanging each conv's
+ * output through HBM in-launch: xch = scratch of 2 * batch * 35 * 128
+ * floats, sync = 33 * 32 words, zero-initialised ONCE by the caller and left
+ * zeroed by every launch (calls sharing one sync block must be ordered on
+ * one stream); sync[32 * 32] != 0 means a workgroup gave up waiting (1 s)
+ * since the block was zeroed, and that state's output is NaN.  Bit-identical
  * to hz_tower_x6_resident. */
 int hz_tower_x6_split(const float *x0, const void *wpack6, const float *bias, float *out, float *xch, uint32_t *sync,
                       int32_t nconv, int32_t batch, const int32_t *live, void *stream);

@@ -26,13 +26,13 @@ nconv = allw.shape[0]
 x = torch.randn(B, 128, 5, 7, device="cuda").relu().contiguous(memory_format=torch.channels_last)
 out = torch.empty_like(x)
 xch = torch.empty(2 * B * 35 * 128, device="cuda")
-sync = torch.zeros((B + 1) * 32, dtype=torch.int32, device="cuda")
+sync = torch.zeros(33 * 32, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for _ in range(300):
     assert lib.hz_tower_x6_split(x.data_ptr(), allw.data_ptr(), allb.data_ptr(), out.data_ptr(), xch.data_ptr(),
                                  sync.data_ptr(), nconv, B, None, st) == 0
 torch.cuda.synchronize()
-assert int(sync[B * 32].item()) == 0, "hand-off timed out"
+assert int(sync[32 * 32].item()) == 0 and not sync.any().item(), "hand-off timed out or counters left set"
 s = np.zeros((8, 64, 6), dtype=np.uint64)
 assert lib.hz_net_diag_split_stamps(s.ctypes.data) == 0
 s = s[:, :nconv].astype(np.int64)
