@@ -7,4 +7,4 @@ REPO=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/$OUT" -o run -- \
-  python3 "$REPO/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$REPO/$OUT/bench_under_prof.json"
+  python3 "$REPO/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-off-compare > "$REPO/$OUT/bench_under_prof.json"
