@@ -1587,7 +1587,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
 // rows in 8 + 7 dependent blocks: ~24 us at any batch up to 8).  Partial
 // sums are added in a fixed order; results agree with k_heads_fc to fp32
 // rounding (different summation order).
-constexpr int kH1Max = 64;  // batches up to this take k_heads_fc1 (HZ_HEADS1_MAX overrides)
+constexpr int kH1Max = 2048;  // batches up to this take k_heads_fc1 (HZ_HEADS1_MAX overrides; equal at 2048, 0.8 % slower at 4096)
 __global__ void __launch_bounds__(1024) k_heads_fc1(const float *__restrict__ x, const float *__restrict__ glob,
                                                     const float *__restrict__ hw, const float *__restrict__ hb,
                                                     const float *__restrict__ wpT, const float *__restrict__ bp,
