@@ -57,9 +57,40 @@ __host__ __device__ constexpr uint64_t code_sets(int from, int cnt) {
 constexpr uint64_t kCodeSetLo = code_sets(0, 4), kCodeSetMid = code_sets(4, 4), kCodeSetHi = code_sets(8, 4),
                    kCodeSetTop = code_sets(12, 4), kCodeSetEnd = code_sets(16, 2);
 
+// feature f of item j's global vector (process_game_state.py:98-137)
+__device__ __forceinline__ float glob_value(const uint64_t *__restrict__ st, long word_stride, long item_stride,
+                                            const int32_t *__restrict__ idx, long j, int f) {
+  long b = idx ? (long)idx[j] : j;
+  float val = 0.f;
+  if (b >= 0) {
+    const uint64_t *sb = st + b * item_stride;
+    uint64_t misc = sb[5 * word_stride];
+    if (f < 30) {
+      uint64_t piles = sb[4 * word_stride];
+      int pi = f / 6, t = f - pi * 6;
+      if (pi < npiles_of(piles)) {
+        int cnt = (pile_tile(piles, pi, 0) == t) + (pile_tile(piles, pi, 1) == t) + (pile_tile(piles, pi, 2) == t);
+        val = (float)((double)cnt / 3.0);
+      }
+    } else if (f < 36) {
+      int t = f - 30, nh = hand_n(misc), cnt = 0;
+      for (int q = 0; q < nh; q++) cnt += hand_tile(misc, q) == t;
+      val = (float)((double)cnt / 3.0);
+    } else {
+      int t = f - 36;
+      val = (float)((double)bag_n(misc, t) / (double)initial_count(t));
+    }
+  }
+  return val;
+}
+
+// Glob: the wave also writes its pair's global features (small batches: one
+// launch instead of two; at 4096 items two launches measured faster)
+template <bool Glob>
 __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
                                                       long item_stride, const int32_t *__restrict__ idx, int m,
-                                                      const int32_t *__restrict__ mcount, float *__restrict__ board) {
+                                                      const int32_t *__restrict__ mcount, float *__restrict__ board,
+                                                      float *__restrict__ glob) {
   __shared__ uint64_t smask[kEncWaves][76];
   __shared__ float sval[kEncWaves][76];
   int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -143,6 +174,14 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
     int el = 1328 + lane, ch = el / 35, yx = el - 35 * ch;
     out[el] = ((smask[w][ch] >> yx) & 1) ? sval[w][ch] : 0.f;
   }
+  if constexpr (Glob) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int i = lane + 64 * r;
+      const long j = j0 + (i >= 42 ? 1 : 0);
+      if (i < 84 && j < m) glob[j * 42 + i - 42 * (i >= 42 ? 1 : 0)] = glob_value(st, word_stride, item_stride, idx, j, i % 42);
+    }
+  }
 }
 
 __global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict__ st, long word_stride,
@@ -152,38 +191,25 @@ __global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict_
   if (mcount) m = *mcount < m ? *mcount : m;
   if (i >= m * 42) return;
   int j = i / 42, f = i - j * 42;
-  long b = idx ? (long)idx[j] : (long)j;
-  float val = 0.f;
-  if (b >= 0) {
-    const uint64_t *sb = st + b * item_stride;
-    uint64_t misc = sb[5 * word_stride];
-    if (f < 30) {
-      uint64_t piles = sb[4 * word_stride];
-      int pi = f / 6, t = f - pi * 6;
-      if (pi < npiles_of(piles)) {
-        int cnt = (pile_tile(piles, pi, 0) == t) + (pile_tile(piles, pi, 1) == t) + (pile_tile(piles, pi, 2) == t);
-        val = (float)((double)cnt / 3.0);
-      }
-    } else if (f < 36) {
-      int t = f - 30, nh = hand_n(misc), cnt = 0;
-      for (int q = 0; q < nh; q++) cnt += hand_tile(misc, q) == t;
-      val = (float)((double)cnt / 3.0);
-    } else {
-      int t = f - 36;
-      val = (float)((double)bag_n(misc, t) / (double)initial_count(t));
-    }
-  }
-  glob[i] = val;
+  glob[i] = glob_value(st, word_stride, item_stride, idx, j, f);
 }
 
 // mcount (device pointer, may be NULL): only items [0, min(m, *mcount)) are
 // written; the grid is sized for m.
+constexpr int kEncFuseMax = 512;  // items up to this: board and glob in one launch
+
 inline void launch_encode(const uint64_t *st, long word_stride, long item_stride, const int32_t *idx, int m,
                           float *board, float *glob, hipStream_t stream, const int32_t *mcount = nullptr) {
   if (board) {
     long pairs = ((long)m + 1) / 2;
-    hipLaunchKernelGGL(k_encode_board, dim3((unsigned)((pairs + kEncWaves - 1) / kEncWaves)), dim3(256), 0, stream,
-                       st, word_stride, item_stride, idx, m, mcount, board);
+    const dim3 grid((unsigned)((pairs + kEncWaves - 1) / kEncWaves));
+    if (glob && m <= kEncFuseMax) {  // one launch for both tensors
+      hipLaunchKernelGGL(k_encode_board<true>, grid, dim3(256), 0, stream, st, word_stride, item_stride, idx, m,
+                         mcount, board, glob);
+      return;
+    }
+    hipLaunchKernelGGL(k_encode_board<false>, grid, dim3(256), 0, stream, st, word_stride, item_stride, idx, m,
+                       mcount, board, nullptr);
   }
   if (glob) {
     hipLaunchKernelGGL(k_encode_glob, dim3((unsigned)((m * 42 + 255) / 256)), dim3(256), 0, stream, st,
