@@ -86,7 +86,10 @@ def parse():
     ap.add_argument("--sp-warmup", type=int, default=2, help="selfplay sub-object: untimed moves")
     ap.add_argument("--sp-moves", type=int, default=3, help="selfplay sub-object: timed moves")
     ap.add_argument("--sp-cpu-seconds", type=float, default=8.0,
-                    help="selfplay sub-object: C-twin MCTS baseline sample (host cores)")
+                    help="selfplay sub-object: bound of the one-thread C-twin sample (seconds x 4)")
+    ap.add_argument("--sp-games", type=int, default=1,
+                    help="selfplay sub-object: complete games timed on every board (0: estimate games/s from "
+                         "the per-move leg)")
     ap.add_argument("--iterations", type=int, default=5,
                     help="config 5: training iterations timed (one evaluation cycle at eval-every 5); "
                          "config 4: self-play iterations timed")
@@ -97,6 +100,11 @@ def parse():
                     help="MCTS simulations per move (config 3/4: 200; config 5: 400 = mcts_config_default)")
     ap.add_argument("--records-out", default=None,
                     help="config 4: write this rank's replay buffer and own records (torch.save) for tests")
+    ap.add_argument("--checkpoint", default=None,
+                    help="self-play network: a model.py-format checkpoint (default: synthesize best_model.pth.tar "
+                         "from the torch.manual_seed(0) default net and load it through load_checkpoint)")
+    ap.add_argument("--stub", action="store_true",
+                    help="config 4: the deterministic stub evaluator instead of the network (oracle-replay tests)")
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     ap.add_argument("--full-game", action="store_true",
                     help="config 3: time one complete game on every board (games/s measured, not estimated)")
@@ -330,17 +338,55 @@ class TimedEvaluator:
         return sum(a.elapsed_time(b) for a, b in self.events)
 
 
+REF_TRAIN_CFG = {"optimizer_type": "Adam", "learning_rate": 0.001, "weight_decay": 0.0001,
+                 "value_loss_weight": 1.0, "policy_loss_weight": 1.0, "batch_size": 64, "momentum": 0.9,
+                 "use_scheduler": True, "scheduler_type": "StepLR", "scheduler_step_size": 30,
+                 "scheduler_gamma": 0.5, "force_lr_reset_on_load": False, "new_forced_lr": 0.000125}
+
+
+def load_selfplay_model(args, dev):
+    """BASELINE config 3's network: best_model.pth.tar through
+    ModelManager.load_checkpoint (model.py:184-256).  The reference's file is
+    absent offline, so unless --checkpoint names one, a
+    checkpoint is synthesized first: the default network initialised with
+    torch.manual_seed(0), written by save_checkpoint in the model.py:161-182
+    dict.  Returns (model in eval mode, description)."""
+    import tempfile
+    from hzamd.manager import ModelManager
+    from hzamd.net import DEFAULT
+    cfg = dict(REF_TRAIN_CFG, device=str(dev))
+    path = args.checkpoint
+    if path is None:
+        folder = tempfile.mkdtemp(prefix="hz_ckpt_")
+        torch.manual_seed(0)
+        ModelManager(dict(DEFAULT, board_size=(5, 7)), cfg).save_checkpoint(folder=folder,
+                                                                            filename="best_model.pth.tar")
+        path, what = os.path.join(folder, "best_model.pth.tar"), "synthesized best_model.pth.tar " \
+            "(torch.manual_seed(0) default net, model.py:161-182 format)"
+    else:
+        what = f"checkpoint {path}"
+    mm = ModelManager(dict(DEFAULT, board_size=(5, 7)), cfg)
+    ok, _ = mm.load_checkpoint(folder=os.path.dirname(os.path.abspath(path)), filename=os.path.basename(path))
+    if not ok:
+        raise SystemExit(f"could not load {path} with ModelManager.load_checkpoint")
+    return mm.model.eval(), what + " loaded by ModelManager.load_checkpoint"
+
+
 def _selfplay_setup(args, dev, rank, sims, n):
     from hzamd.mcts import BatchedPredictor
-    from hzamd.net import HarmoniesNet
     from hzamd.selfplay import SelfPlay
-    torch.manual_seed(0)
     torch.backends.cudnn.benchmark = True
-    net = HarmoniesNet().to(dev).eval()
-    dtype = torch.bfloat16 if args.nn_dtype == "bf16" else None
-    ev = TimedEvaluator(BatchedPredictor(net, dtype=dtype), dev)
     cfg = {"num_simulations": sims, "cpuct": 2, "dirichlet_alpha": 0.4, "dirichlet_epsilon": 0.25,
            "turns_until_tau0": 15, "testing": False}
+    if getattr(args, "stub", False):
+        # the deterministic integer evaluator of the parity fixtures (tests
+        # replay such runs with the C twin's search, board by board)
+        from hzamd.mcts import stub_evaluator
+        return SelfPlay(n, stub_evaluator, cfg, seed_base=args.seed_base + rank * n, device=dev), None
+    net, what = load_selfplay_model(args, dev)
+    dtype = torch.bfloat16 if args.nn_dtype == "bf16" else None
+    ev = TimedEvaluator(BatchedPredictor(net, dtype=dtype), dev)
+    ev.network = what
     sp = SelfPlay(n, ev, cfg, seed_base=args.seed_base + rank * n, device=dev)
     return sp, ev
 
@@ -384,7 +430,8 @@ def bench_selfplay(args, dev, rank, world):
             "metric": "self-play MCTS simulations/sec @4096 boards x 200 sims",
             "value": sims_all / elapsed, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": per_move * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
+            "vs_baseline": None, "dtype": args.nn_dtype,
+            "data": "synthetic: seeded games; network = synthesized best_model.pth.tar (seed-0 random init)",
             "config": {"workload": f"config3: {n} boards x {sims} sims/move, default 128fx8 net",
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
             "games_per_s_est": world * n / (per_move * MEAN_SELFPLAY_PLIES),
@@ -434,7 +481,8 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
             "metric": "self-play games/sec @4096 boards x 200 MCTS sims (complete games, measured)",
             "value": world * n / elapsed, "unit": "games/s", "n_gpus": world, "steps": 1, "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.nn_dtype, "data": "synthetic: random-init network, seeded games",
+            "dtype": args.nn_dtype,
+            "data": "synthetic: seeded games; network = synthesized best_model.pth.tar (seed-0 random init)",
             "config": {"workload": f"config3: {n} boards x {sims} sims/move, one whole game per board",
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
             "plies": rec["plies"], "moves": moves, "sims_per_s": world * moves * sims / elapsed,
@@ -444,22 +492,38 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
 
 
 def selfplay_probe(args, dev, rank, world):
-    """The `selfplay` sub-object of the default line: config 3 per move
-    (profile_self_play.py:17-77's loop, batched) and, at N > 1, config 4's
-    RCCL all-gather of the timed moves' records.  Returns a dict on rank 0."""
+    """The `selfplay` sub-object of the default line (config 3,
+    profile_self_play.py:17-77's loop batched; at N > 1 also config 4's
+    exchange).  Three legs on every rank:
+      1. per move: `sp_moves` timed moves at the full leaf batch (sims/s and
+         the network's roofline at batch 4096);
+      2. complete games: `sp_games` whole self-play games on every board, timed
+         end to end (games_per_s is measured, not extrapolated); at N > 1 the
+         games' (s, pi, z) records are all-gathered over RCCL into every
+         rank's replay buffer and the exchange is timed (config 4);
+      3. parity guard: the first timed move's roots, chance streams and root
+         noise searched again on the GPU with the deterministic stub
+         evaluator, and by the C twin (or_mcts_search, MCTS.py:272-441
+         restated) on the host: root visit counts, tree sizes and the next
+         word of every board's CPython stream must agree, board by board,
+         on every rank (the count of mismatches is all-reduced).
+    Returns the sub-object on rank 0."""
     from hzamd import distributed as hd
     from hzamd.net import flops_per_eval
     n, sims = args.sp_boards, args.sp_sims
     sp, ev = _selfplay_setup(args, dev, rank, sims, n)
+    fl = flops_per_eval()
     sp.env.reset()
     for w in range(args.sp_warmup):
         sp.move(w)
     torch.cuda.synchronize(dev)
-    # root states + streams of the first timed move: the CPU twin's sample
-    cpu_roots = sp.env.export_state(with_mt=True) if rank == 0 and world == 1 else None
+    # the first timed move's roots + streams (device copies): the guard's input
+    roots = tuple(t.clone() for t in sp.env.export_state(with_mt=True))
+    active0 = ~sp.env.done()
     sp.keep_noise = True
     sp.noise_log.clear()
     ev.reset()
+    # -- leg 1: per move at the full leaf batch
     recs = []
     if world > 1:
         dist.barrier()
@@ -474,105 +538,202 @@ def selfplay_probe(args, dev, rank, world):
     nn_ms = ev.ms()
     rows = int(ev.rows.item())
     board_moves = int(sum(int(a.sum().item()) for _, _, a in recs))
+    noise0 = sp.noise_log[0][0].clone()
+    sp.keep_noise = False
+    sp.noise_log.clear()
     sims_done = board_moves * sims
-    exchange = None
     if world > 1:
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
         sims_all, rows_all = (int(x) for x in all_reduce([sims_done, rows], dist.ReduceOp.SUM))
-        # config 4's exchange on the records of the timed moves (z pending:
-        # the games are not over; the bytes and the collective are the same)
-        st = torch.cat([s.t()[a] for s, _, a in recs])
-        vis = torch.cat([v[a] for _, v, a in recs])
-        player = ((st[:, 5] >> 41) & 1).to(torch.int8)
-        packed = hd.pack_records(st, vis, torch.zeros(st.shape[0], dtype=torch.int8, device=dev), player)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        x0 = time.perf_counter()
-        gathered = hd.all_gather_records(packed)
-        torch.cuda.synchronize(dev)
-        xdt = time.perf_counter() - x0
-        xdt = all_reduce([xdt], dist.ReduceOp.MAX)[0]
-        nbytes = gathered.numel() * 8
-        exchange = {"collective": "all_gather (counts) + all_gather_into_tensor (records)",
-                    "records": int(gathered.shape[0]), "bytes_per_rank_received": nbytes,
-                    "ms": xdt * 1e3, "GBps": nbytes / xdt / 1e9,
-                    "records_per_move_per_rank": int(packed.shape[0]) / args.sp_moves,
-                    "est_ms_per_iteration": xdt * 1e3 / args.sp_moves * MEAN_SELFPLAY_PLIES,
-                    "note": "records of the timed moves (336 B each); a self-play iteration exchanges "
-                            "~62 plies' worth once"}
     else:
         sims_all, rows_all = sims_done, rows
     per_move = elapsed / args.sp_moves
-    fl = flops_per_eval()
     nn_tf = fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None
+    # -- leg 2: complete games (+ config 4's exchange at N > 1)
+    game = selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl) if args.sp_games > 0 else None
+    # -- leg 3: the parity guard (every rank), with the CPU twin's timing
+    guard = selfplay_guard(roots, active0, noise0, sims, dev, rank, world,
+                           cpu_sample=rank == 0 and world == 1 and args.sp_cpu_seconds > 0,
+                           one_core_s=min(2.0, args.sp_cpu_seconds / 4))
     out = None
     if rank == 0:
-        out = {"workload": f"config3: {n} boards/GPU x {sims} sims/move, default 128fx8 net, fp32 "
-                           f"({args.sp_warmup} warm-up + {args.sp_moves} timed moves from the game start)",
+        emu_peak = BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS
+        out = {"workload": f"config3: {n} boards/GPU x {sims} sims/move, default 128fx8 net, fp32; "
+                           f"per move: {args.sp_warmup} warm-up + {args.sp_moves} timed moves from the game start; "
+                           f"complete games: {args.sp_games} whole game(s) on every board",
                "sims_per_s": sims_all / elapsed, "nn_evals_per_s": rows_all / elapsed,
-               "games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
-               "games_per_s_basis": f"ms per move x mean game length {MEAN_SELFPLAY_PLIES} plies; "
-                                    "complete games: bench.py --config 3 --full-game",
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
                "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
                "nn_rows_evaluated": rows, "sims": sims_done,
-               "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS,
-                               "unit": "TFLOP/s",
-                               "frac": nn_tf / (BF16_MFMA_PEAK_TFLOPS / X6_PRODUCTS) if nn_tf else None,
+               "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": emu_peak, "unit": "TFLOP/s",
+                               "frac": nn_tf / emu_peak if nn_tf else None,
+                               "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
+                               "fp32_mfma_frac": nn_tf / FP32_MFMA_PEAK_TFLOPS if nn_tf else None,
                                "flop_per_eval": fl,
-                               "basis": "fp32 FLOP of the whole leaf-eval forward (HIP events around each call, incl. "
-                                        "the linear layers) against the bf16 MFMA's dense peak / 6 (the stem and "
-                                        "tower convs issue six bf16 MFMAs per fp32 product block); the f32 MFMA "
-                                        f"peak is {FP32_MFMA_PEAK_TFLOPS} TFLOP/s"},
-               "exchange": exchange, "dtype": "fp32", "n_gpus": world}
-        if cpu_roots is not None and args.sp_cpu_seconds > 0:
-            out["cpu_baseline"] = selfplay_cpu_baseline(cpu_roots, sp.noise_log[0][0], sims, args.sp_cpu_seconds)
+                               "basis": "fp32 FLOP of the whole leaf-eval forward at the 4096-row batch (HIP events "
+                                        "around each call, incl. the heads) over the emulated-fp32 roof: the stem "
+                                        "and tower convs compute fp32-exact products as six bf16 MFMAs per fp32 "
+                                        "product block, so their ceiling is the bf16 dense peak / 6 = "
+                                        f"{emu_peak:.1f} TFLOP/s; fp32_mfma_frac is the same figure against the "
+                                        f"f32 MFMA's dense peak ({FP32_MFMA_PEAK_TFLOPS} TFLOP/s), which this path "
+                                        "does not use"},
+               "dtype": "fp32", "n_gpus": world, "network": ev.network, "parity": guard["parity"]}
+        if game is not None:
+            out.update({"games_per_s": game["games_per_s"], "games_per_s_basis": game["basis"],
+                        "game": game})
+            out["exchange"] = game.get("exchange")
+        else:
+            out.update({"games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
+                        "games_per_s_basis": f"estimate: ms per move x mean game length {MEAN_SELFPLAY_PLIES} "
+                                             "plies (--sp-games 0)", "exchange": None})
+        if guard.get("cpu_baseline") is not None:
+            out["cpu_baseline"] = guard["cpu_baseline"]
     sp.mcts.close()
     sp.env.close()
     return out
 
 
-def selfplay_cpu_baseline(roots, noise, sims, seconds):
-    """The C twin's MCTS (oracle/hz_oracle.c or_mcts_search, the reference's
-    get_best_action_and_pi restated) on the box's host cores: the first timed
-    move's root states and streams, same sims / cpuct / noise, the stub
-    evaluator in place of the network (tree work only), boards spread over
-    threads (ctypes releases the GIL); plus the reference network's batch-1
-    CPU forward (ModelManager.predict's shape) timed separately."""
+def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
+    """Leg 2 of the selfplay sub-object: `sp_games` complete games on every
+    board (SelfPlay.play: search + choice + env step per ply, records kept on
+    the device), timed end to end with barriers; at N > 1 the compacted
+    records (z from each recorded player's side) are all-gathered into every
+    rank's replay buffer over RCCL, timed separately (config 4's exchange,
+    trainer.py:104-127)."""
+    from hzamd import distributed as hd
+    n = sp.n
+    orig_move = sp.move
+
+    def move(ply, done=None):  # progress on stderr: a long run must not look hung
+        out = orig_move(ply, done)
+        if ply % 16 == 0:
+            print(f"[selfplay game] rank {rank} ply {ply}", file=sys.stderr, flush=True)
+        return out
+
+    sp.move = move
+    ev.reset()
+    plies, moves, t_play, packed = [], 0, 0.0, []
+    try:
+        for _ in range(args.sp_games):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            rec = sp.play(reset=True)
+            torch.cuda.synchronize(dev)
+            t_play += time.perf_counter() - t0
+            plies.append(rec["plies"])
+            moves += int(rec["valid"].sum().item())
+            if world > 1:
+                comp = sp.compact(rec)
+                packed.append(hd.pack_records(comp["states"], comp["visits"], comp["z"], comp["player"]))
+            del rec
+    finally:
+        sp.move = orig_move
+    nn_ms, rows = ev.ms(), int(ev.rows.item())
+    exchange = None
+    if world > 1:
+        t_play = all_reduce([t_play], dist.ReduceOp.MAX)[0]
+        moves_all, rows_all = (int(x) for x in all_reduce([moves, rows], dist.ReduceOp.SUM))
+        own = torch.cat(packed)
+        buf = hd.ReplayBuffer(max(1, own.shape[0]) * world, dev)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        x0 = time.perf_counter()
+        gathered = hd.all_gather_records(own)
+        buf.extend(gathered)
+        torch.cuda.synchronize(dev)
+        xdt = all_reduce([time.perf_counter() - x0], dist.ReduceOp.MAX)[0]
+        nbytes = gathered.numel() * 8
+        exchange = {"collective": "all_gather (counts) + all_gather_into_tensor (records), into every rank's "
+                                  "device replay buffer",
+                    "records": int(gathered.shape[0]), "records_own": int(own.shape[0]),
+                    "bytes_per_rank_received": nbytes, "ms": xdt * 1e3, "GBps": nbytes / xdt / 1e9,
+                    "note": "the complete games' (s, pi, z) records, 336 B each (config 4's exchange)"}
+    else:
+        moves_all, rows_all = moves, rows
+    if rank != 0:
+        return None
+    games = world * n * args.sp_games
+    return {"games_per_s": games / t_play,
+            "basis": f"complete games: {args.sp_games} whole game(s) on each of the {world} x {n} boards, timed "
+                     "end to end (slowest rank)",
+            "seconds": t_play, "games": games, "plies_per_game_batch": plies, "moves": moves_all,
+            "sims_per_s": moves_all * sims / t_play, "nn_rows_evaluated": rows_all,
+            "nn_rows_skipped": moves_all * sims - rows_all, "nn_s_rank0": nn_ms * 1e-3,
+            "nn_tflops_rank0": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
+            "exchange": exchange}
+
+
+def selfplay_guard(roots, active, noise, sims, dev, rank, world, cpu_sample=False, one_core_s=2.0):
+    """Leg 3: the first timed move's roots (states, CPython streams, root
+    noise) searched on the GPU (BatchedMCTS with the stub evaluator, the
+    timed move's settings: cpuct 2, eps 0.25, testing False) and on the host
+    by the C twin's or_mcts_search, all boards spread over threads (ctypes
+    releases the GIL).  Root visit counts, node and edge counts and the next
+    CPython word of every board must be equal; mismatches are summed over
+    ranks.  The CPU run's rate doubles as the selfplay cpu_baseline (rank 0,
+    N = 1), with a one-thread sample and the reference network's batch-1 CPU
+    forward beside it."""
     from concurrent.futures import ThreadPoolExecutor
     import numpy as np
-    import oracle
-    from hzamd.net import HarmoniesNet
+    import oracle  # test infrastructure: the checker and the CPU baseline only
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
     from hzamd.state import unpack_ref
-    st, mt, idx = (t.cpu().numpy() for t in roots)
-    mt = mt.view(np.uint32)
-    nz = noise.cpu().numpy()
+    st_d, mt_d, idx_d = roots
+    n = st_d.shape[1]
+    env = BatchedEnv(n, device=dev)
+    env.import_state(st_d, mt_d, idx_d)
+    mcts = BatchedMCTS(env, sims)
+    visits = mcts.search(stub_evaluator, 2.0, active=active, noise=noise, eps=0.25, testing=False)
+    counts = mcts.stats()
+    _, mt1, idx1 = env.export_state(with_mt=True)
+    torch.cuda.synchronize(dev)
+    visits, counts = visits.cpu().numpy(), counts.cpu().numpy()
+    mt1, idx1 = mt1.cpu().numpy().view(np.uint32), idx1.cpu().numpy()
+    st, mt, idx = st_d.cpu().numpy(), mt_d.cpu().numpy().view(np.uint32), idx_d.cpu().numpy()
+    nz = np.zeros((n, 143), np.float64)
+    nz[:, :noise.shape[1]] = noise.cpu().numpy()
+    act = active.cpu().numpy()
+    mcts.close()
+    env.close()
     nthreads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-    nb = st.shape[1]
 
-    def one(b):
+    def search(b):
         m = oracle.mt_from_words(mt[b], idx[b])
-        ref = unpack_ref(st[:, b])
-        if oracle.is_game_over(ref):
-            return 0
-        oracle.mcts_search(ref, m, sims, 2.0, eps=0.25, testing=False, tau0=15, ply=0, noise=nz[b])
-        return sims
+        _, ov, nn, ne = oracle.mcts_search(unpack_ref(st[:, b]), m, sims, 2.0, eps=0.25, testing=False, tau0=15,
+                                           ply=0, noise=nz[b])
+        return ov, nn, ne, m
 
-    done, b0 = 0, 0
+    def check(b):
+        ov, nn, ne, m = search(b)
+        ok = ((visits[b] == ov).all() and counts[b, 0] == nn and counts[b, 1] == ne
+              and oracle.mt_next32(m) == oracle.mt_next32(oracle.mt_from_words(mt1[b], idx1[b])))
+        return int(not ok)
+
+    boards = [b for b in range(n) if act[b]]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(nthreads) as pool:
-        while time.perf_counter() - t0 < seconds and b0 < nb:
-            chunk = list(range(b0, min(nb, b0 + 4 * nthreads)))
-            done += sum(pool.map(one, chunk))
-            b0 += len(chunk)
-    dt = time.perf_counter() - t0
-    # one search on one thread, for the per-core figure
-    t1 = time.perf_counter()
-    k1, s1 = 0, 0
-    while time.perf_counter() - t1 < min(2.0, seconds / 4):
-        s1 += one(k1 % nb)
+        bad = sum(pool.map(check, boards, chunksize=8))
+    cpu_dt = time.perf_counter() - t0
+    checked = len(boards)
+    if world > 1:
+        bad, checked = (int(x) for x in all_reduce([bad, checked], dist.ReduceOp.SUM))
+    assert bad == 0, f"selfplay parity: {bad} of {checked} boards' searches differ from the C twin"
+    out = {"parity": f"{checked}/{checked} boards bit-exact vs C twin (first timed move's roots, streams and root "
+                     f"noise, {sims} sims, stub evaluator: root visits, tree sizes, next MT word"
+                     + (f"; {world} ranks, each its own boards)" if world > 1 else ")")}
+    if not cpu_sample:
+        return out
+    # one thread, bounded, for the per-core figure
+    t1, k1, s1 = time.perf_counter(), 0, 0
+    while time.perf_counter() - t1 < one_core_s and k1 < len(boards):
+        search(boards[k1])
+        s1 += sims
         k1 += 1
     dt1 = time.perf_counter() - t1
+    from hzamd.net import HarmoniesNet
     net = HarmoniesNet().eval()
     prev = torch.get_num_threads()
     torch.set_num_threads(nthreads)
@@ -586,14 +747,17 @@ def selfplay_cpu_baseline(roots, noise, sims, seconds):
         nn_s = (time.perf_counter() - t2) / 40
     torch.set_num_threads(prev)
     tree_1 = s1 / dt1
-    return {"value": done / dt, "unit": "sims/s", "cores": nthreads, "kind": "port",
-            "value_1core": tree_1, "nn_cpu_ms_per_eval": nn_s * 1e3,
-            "est_sims_per_s_one_process": 1.0 / (1.0 / tree_1 + nn_s),
-            "sample": f"{b0} boards' first timed move searched ({done} sims, {sims} per board) in {dt:.1f}s by the "
-                      f"C twin's or_mcts_search on {nthreads} threads with the stub evaluator (tree work only); "
-                      f"1 thread: {k1} searches in {dt1:.1f}s; the reference net's batch-1 CPU forward "
-                      f"({nthreads} intra-op threads) timed separately; est_sims_per_s_one_process = one "
-                      f"reference-shaped process (one tree, one predict per leaf)"}
+    done = len(boards) * sims
+    out["cpu_baseline"] = {
+        "value": done / cpu_dt, "unit": "sims/s", "cores": nthreads, "kind": "port",
+        "value_1core": tree_1, "nn_cpu_ms_per_eval": nn_s * 1e3,
+        "est_sims_per_s_one_process": 1.0 / (1.0 / tree_1 + nn_s),
+        "sample": f"the first timed move's {len(boards)} roots searched ({done} sims, {sims} per board) in "
+                  f"{cpu_dt:.1f}s by the C twin's or_mcts_search on {nthreads} threads with the stub evaluator "
+                  f"(tree work only; the same run is the parity guard); 1 thread: {k1} searches in {dt1:.1f}s; "
+                  f"the reference net's batch-1 CPU forward ({nthreads} intra-op threads) timed separately; "
+                  "est_sims_per_s_one_process = one reference-shaped process (one tree, one predict per leaf)"}
+    return out
 
 
 def bench_exchange(args, dev, rank, world):
@@ -614,15 +778,21 @@ def bench_exchange(args, dev, rank, world):
     if world > 1:
         hd.all_gather_records(torch.zeros(1, hd.RECORD_WORDS, dtype=torch.int64, device=dev))
     torch.cuda.synchronize(dev)
-    own = []
+    own, plies = [], []
     t_play = t_x = 0.0
     games = examples = 0
+    # --records-out: keep each move's root noise, uniforms and choices, so a
+    # test can replay the records with the C twin (tests/test_bench_gpu.py)
+    sp.keep_noise = bool(args.records_out)
+    sp.noise_log.clear()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for it in range(args.iterations):
         tm = {}
-        gathered, _ = sp.iteration(buf, timings=tm)
+        gathered, rec = sp.iteration(buf, timings=tm)
+        plies.append(rec["plies"])
+        del rec
         t_play += tm["play_s"]
         t_x += tm["exchange_s"]
         games += n * world
@@ -637,8 +807,12 @@ def bench_exchange(args, dev, rank, world):
     if world > 1:
         elapsed, t_play, t_x = all_reduce([elapsed, t_play, t_x], dist.ReduceOp.MAX)
     if args.records_out:
+        log = sp.noise_log
         torch.save({"buffer": buf.records().cpu(), "own": torch.cat(own).cpu(),
-                    "own_counts": torch.tensor([o.shape[0] for o in own]), "rank": rank, "world": world},
+                    "own_counts": torch.tensor([o.shape[0] for o in own]), "rank": rank, "world": world,
+                    "seed_base": args.seed_base + rank * n, "plies": torch.tensor(plies),
+                    "noise": torch.stack([x[0] for x in log]).cpu(), "u": torch.stack([x[1] for x in log]).cpu(),
+                    "act": torch.stack([x[2] for x in log]).cpu(), "sims": sims, "stub": bool(args.stub)},
                    f"{args.records_out}.rank{rank}.pt")
     nbytes = examples * hd.RECORD_WORDS * 8
     if rank == 0:
@@ -647,7 +821,9 @@ def bench_exchange(args, dev, rank, world):
             "value": games / elapsed, "unit": "games/s", "n_gpus": world, "steps": args.iterations,
             "warmup": 1, "ms_per_step": elapsed * 1e3 / args.iterations, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.nn_dtype,
-            "data": "synthetic: random-init network, seeded games",
+            "data": ("synthetic: stub evaluator (parity runs), seeded games" if args.stub else
+                     "synthetic: seeded games; network = synthesized best_model.pth.tar (seed-0 random init) "
+                     "loaded through ModelManager.load_checkpoint"),
             "config": {"workload": f"config4: {n} boards/GPU x {sims} sims/move, whole games, records "
                                    f"all-gathered into every rank's replay buffer",
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
@@ -798,20 +974,28 @@ def main():
         api = api_mode(env, dev, stream)
     enc = encoder_roofline(dev, n, args.seed_base) if rank == 0 else None
 
-    parity = None
-    if rank == 0:
-        import oracle  # test infrastructure: parity guard + cpu_baseline only
-        ref_total = oracle.play_rule_games(n, args.seed_base, nthreads=8)[0]
-        assert ref_total == first_steps, (ref_total, first_steps)
-        checked = []
-        for ep, stt in ((first_ep, first_state), (last_ep, last_state)):
-            got = stt.cpu().numpy()
-            _, finals, _, _ = oracle.play_rule_games(n, args.seed_base, nthreads=8, episode=ep)
-            bad = [b for b in range(n) if not (unpack_ref(got[:, b]) == finals[b]).all()]
-            assert not bad, f"episode {ep}: boards {bad[:8]} differ from the C oracle"
-            checked.append(ep)
-        parity = (f"first batch: {first_steps} env steps == C oracle ({ref_total}); final states of the first and "
-                  f"last timed batches (episodes {checked[0]}, {checked[1]}): {n}/{n} boards bit-exact vs C oracle")
+    # parity guard on every rank, over its own boards (global ids
+    # seed_base + rank * n + b): the first batch's env-step count and the
+    # final states of the first and the last timed batches against the C
+    # oracle; the mismatch counts are summed over ranks
+    import oracle  # test infrastructure: parity guard + cpu_baseline only
+    my_base = args.seed_base + rank * n
+    ref_total = oracle.play_rule_games(n, my_base, nthreads=8)[0]
+    bad_steps = int(ref_total != first_steps)
+    bad_boards = 0
+    for ep, stt in ((first_ep, first_state), (last_ep, last_state)):
+        got = stt.cpu().numpy()
+        _, finals, _, _ = oracle.play_rule_games(n, my_base, nthreads=8, episode=ep)
+        bad = [b for b in range(n) if not (unpack_ref(got[:, b]) == finals[b]).all()]
+        if bad:
+            print(f"[parity] rank {rank} episode {ep}: boards {bad[:8]} differ from the C oracle", file=sys.stderr)
+        bad_boards += len(bad)
+    if world > 1:
+        bad_steps, bad_boards = (int(x) for x in all_reduce([bad_steps, bad_boards], dist.ReduceOp.SUM))
+    assert bad_steps == 0 and bad_boards == 0, (bad_steps, bad_boards)
+    parity = (f"first batch: {first_steps} env steps == C oracle ({ref_total}); final states of the first and "
+              f"last timed batches (episodes {first_ep}, {last_ep}): {world * n}/{world * n} boards bit-exact vs "
+              "C oracle" + (f" ({world} ranks, each its own boards)" if world > 1 else ""))
     sp = None
     if not args.no_selfplay:
         env.close()
@@ -838,10 +1022,13 @@ def main():
                                    f"launches of 4096 boards",
                        "boards_per_gpu": n, "launches_per_step": L, "env_steps_per_step": timed_steps / args.steps,
                        "games_per_step": timed_games / args.steps, "parallelism": f"shard{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "latency (per-lane chains)", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rollout", "kernel_ms": kern_ms, "kernel_ms_launches": K,
-                         "alg_bytes_per_launch": alg_bytes, "issue_bound": issue},
+                         "alg_bytes_per_launch": alg_bytes, "issue_bound": issue,
+                         "bound_note": "priced against HBM (peak 8 TB/s), but the launch is bound by its serial "
+                                       "per-lane chains (a board's whole game, a stream's seeding): counter "
+                                       "traffic is below the algorithmic bytes, see issue_bound and DESIGN.md §3"},
             "chance_ahead": {"on": True, "note": "each hz_play also prepares every board's next three episodes "
                                                  "as a pipeline on the other CUs (stream seeding, pile draws and "
                                                  "rule hashes, none of which depends on moves); steady state: one "

@@ -634,6 +634,76 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
   HZ_XFLAG(11, d)
 }
 
+// ------------------------------------------------------------- root noise
+// The self-play root noise of get_best_action_and_pi (MCTS.py:314-316:
+// np.random.dirichlet([alpha] * L) over the L legal moves) and the tau = 1
+// uniform of its move choice (MCTS.py:411, np.random.choice), drawn from a
+// counter-based generator keyed by (seed, global board id, move) instead of
+// the process-global np.random: every board's draws are the same whatever
+// the batch it sits in or the number of GPUs.  One wave per
+// board; lane c draws child c's Gamma(alpha) (and c + 64's): Marsaglia-Tsang
+// for alpha + 1 with a standard normal from Box-Muller, times U^(1/alpha)
+// for alpha < 1.  The live children's sum is a fixed butterfly over the
+// wave, so the result does not depend on anything but the key.
+struct NoiseStream {
+  uint64_t key, ctr;
+  __device__ double uniform() {  // (0, 1], 53 bits
+    uint64_t z = mix64(key + 0x9E3779B97F4A7C15ULL * ++ctr);
+    return ((double)(z >> 11) + 1.0) * 0x1.0p-53;
+  }
+};
+
+__device__ double gamma_draw(NoiseStream &s, double alpha) {
+  const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+  const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+  double g;
+  for (;;) {
+    double x, v;
+    do {
+      double u1 = s.uniform(), u2 = s.uniform();
+      x = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+      v = 1.0 + c * x;
+    } while (v <= 0.0);
+    v = v * v * v;
+    double u = s.uniform();
+    if (u < 1.0 - 0.0331 * x * x * x * x || log(u) < 0.5 * x * x + d * (1.0 - v + log(v))) {
+      g = d * v;
+      break;
+    }
+  }
+  if (alpha < 1.0) g *= pow(s.uniform(), 1.0 / alpha);
+  return g;
+}
+
+__global__ void __launch_bounds__(kWave) k_root_noise(const int32_t *__restrict__ count, int n, uint64_t seed,
+                                                      uint64_t board_base, uint64_t move, double alpha,
+                                                      double *__restrict__ noise, double *__restrict__ u) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const uint64_t key = mix64(mix64(mix64(seed ^ 0x6A09E667F3BCC908ULL) ^ (board_base + (uint64_t)b)) ^ move);
+  const int nl = count ? min(max(count[b], 0), kMaxChildren) : 0;
+  double g[2];
+  double sum = 0.0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int c = lane + kWave * k;
+    NoiseStream s{mix64(key ^ (0xD1B54A32D192ED03ULL * (uint64_t)(c + 1))), 0};
+    g[k] = c < nl ? gamma_draw(s, alpha) : 0.0;
+    sum += g[k];
+  }
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) sum += __shfl_xor(sum, off);
+  const double inv = sum > 0.0 ? 1.0 / sum : 0.0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int c = lane + kWave * k;
+    if (c < kMaxChildren) noise[(size_t)b * kMaxChildren + c] = g[k] * inv;
+  }
+  if (lane == 0 && u) {
+    NoiseStream s{mix64(key ^ 0x5851F42D4C957F2DULL), 0};
+    u[b] = s.uniform() - 0x1.0p-53;  // [0, 1)
+  }
+}
+
 // root visit counts by action (MCTS.py:355-376)
 __global__ void __launch_bounds__(kWave) k_result(hz_mcts m, int32_t *__restrict__ visits) {
   int b = blockIdx.x;
@@ -756,6 +826,15 @@ int hz_mcts_expand_backup(hz_mcts *m, hz_env *env, const float *policy, const fl
 int hz_mcts_expand_backup_gathered(hz_mcts *m, hz_env *env, const float *policy, const float *value,
                                    const double *noise, double eps, int32_t testing) {
   return m ? expand_backup(m, env, policy, value, noise, eps, testing, m->slot) : -1;
+}
+
+int hz_root_noise(const int32_t *count, int32_t n, uint64_t seed, uint64_t board_base, uint64_t move, double alpha,
+                  double *noise, double *u, void *stream) {
+  if (n < 0 || !count || !noise || !(alpha > 0.0)) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_root_noise, dim3(n), dim3(kWave), 0, (hipStream_t)stream, count, n, seed, board_base, move,
+                     alpha, noise, u);
+  return launch_err();
 }
 
 int hz_mcts_result(hz_mcts *m, int32_t *visits) {

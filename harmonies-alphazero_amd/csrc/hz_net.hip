@@ -1424,16 +1424,20 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // out[s] = sum_j w[j * ld + col] * in[j][s] over the kHS states, as NB blocks
-// of J / NB rows.  A workgroup visits the blocks starting from block
-// blockIdx % NB: the workgroups, which all run at once, then read different
-// weight rows at a time rather than all queueing on the same L2 lines (all
-// starting at row 0 made the policy layer 57 k cycles).  The block partials
-// are added in block order, so the result does not depend on the workgroup.
-template <int J, int NB>
+// of JB rows (the last one cut at J).  A workgroup visits the blocks starting
+// from block blockIdx % NB: the workgroups, which all run at once, then read
+// different weight rows at a time rather than all queueing on the same L2
+// lines (all starting at row 0 made the policy layer 57 k cycles).  The
+// block partials are added in block order, so the result does not depend on
+// the workgroup.  The blocks are k_heads_fc1's input chunks (policy 7 x 16,
+// value 4 x 20 with the last cut at 17) and every sum runs in its order, so
+// the two head kernels give bit-identical rows: a board's priors do not
+// depend on the size of the batch it was evaluated in.
+template <int J, int NB, int JB = J / NB>
 __device__ __forceinline__ void fcn(const float *__restrict__ w, int ld, int col, const float4 (*in)[kHS / 4],
                                     float (&out)[kHS]) {
-  static_assert(J % NB == 0, "whole blocks");
-  constexpr int JB = J / NB;
+  static_assert(NB * JB >= J && (NB - 1) * JB < J, "NB blocks of JB rows cover J");
+  constexpr bool ragged = NB * JB != J;
   float part[NB][kHS];
   const int r0 = blockIdx.x % NB;
   for (int bi = 0; bi < NB; bi++) {
@@ -1444,6 +1448,7 @@ __device__ __forceinline__ void fcn(const float *__restrict__ w, int ld, int col
     float p[kHS] = {};
 #pragma unroll
     for (int j = 0; j < JB; j++) {  // the block's weight loads all in flight
+      if (ragged && blk * JB + j >= J) break;
       const float wv = wb[j * ld];
 #pragma unroll
       for (int q = 0; q < kHS / 4; q++) {
@@ -1502,16 +1507,23 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
     const int sa = w + 8 * pr, sb = sa + 4;
     const float4 *xa = (const float4 *)(x + ((size_t)(s0 + (sa < ns ? sa : ns - 1)) * 35 + lane) * 128);
     const float4 *xb = (const float4 *)(x + ((size_t)(s0 + (sb < ns ? sb : ns - 1)) * 35 + lane) * 128);
+    // eight partial sums of 16 channels added in order (k_heads_fc1's split)
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < 32; k++) {
-      const float4 u = xa[k], v = xb[k], p = w4[0][k], q = w4[1][k], r = w4[2][k];
-      a0 += u.x * p.x + u.y * p.y + u.z * p.z + u.w * p.w;
-      a1 += u.x * q.x + u.y * q.y + u.z * q.z + u.w * q.w;
-      a2 += u.x * r.x + u.y * r.y + u.z * r.z + u.w * r.w;
-      c0 += v.x * p.x + v.y * p.y + v.z * p.z + v.w * p.w;
-      c1 += v.x * q.x + v.y * q.y + v.z * q.z + v.w * q.w;
-      c2 += v.x * r.x + v.y * r.y + v.z * r.z + v.w * r.w;
+#pragma unroll 2
+    for (int kk = 0; kk < 8; kk++) {
+      float e0 = 0.f, e1 = 0.f, e2 = 0.f, f0 = 0.f, f1 = 0.f, f2 = 0.f;
+#pragma unroll
+      for (int k4 = 0; k4 < 4; k4++) {
+        const int k = 4 * kk + k4;
+        const float4 u = xa[k], v = xb[k], p = w4[0][k], q = w4[1][k], r = w4[2][k];
+        e0 += u.x * p.x + u.y * p.y + u.z * p.z + u.w * p.w;
+        e1 += u.x * q.x + u.y * q.y + u.z * q.z + u.w * q.w;
+        e2 += u.x * r.x + u.y * r.y + u.z * r.z + u.w * r.w;
+        f0 += v.x * p.x + v.y * p.y + v.z * p.z + v.w * p.w;
+        f1 += v.x * q.x + v.y * q.y + v.z * q.z + v.w * q.w;
+        f2 += v.x * r.x + v.y * r.y + v.z * r.z + v.w * r.w;
+      }
+      a0 += e0, a1 += e1, a2 += e2, c0 += f0, c1 += f1, c2 += f2;
     }
     const float h0 = hb[0], h1 = hb[1], h2 = hb[2];
     a0 += h0, a1 += h1, a2 += h2, c0 += h0, c1 += h1, c2 += h2;
@@ -1528,7 +1540,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   // 2. policy logits
   if (t < kAct) {
     float acc[kHS];
-    fcn<kPIn, 8>(wpT, kAct, t, pin, acc);
+    fcn<kPIn, 7>(wpT, kAct, t, pin, acc);
     const float bb = bp[t];
 #pragma unroll
     for (int s = 0; s < kHS; s++) lg[s][t] = acc[s] + bb;
@@ -1538,7 +1550,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   // 3. value: hidden unit t, relu, times w2[t], summed over the units
   {
     float acc[kHS];
-    fcn<kVIn, 7>(w1T, kHid, t, vin, acc);
+    fcn<kVIn, 4, 20>(w1T, kHid, t, vin, acc);
     const float bb = b1[t], wo = w2[t];
 #pragma unroll
     for (int s = 0; s < kHS; s++) {
@@ -1584,9 +1596,9 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
 // arena's few dozen rows): one state per 1024-thread workgroup, every layer
 // split over the inputs so that each thread has at most 20 weight loads,
 // all in flight at once (k_heads_fc's 8-state workgroup walks its weight
-// rows in 8 + 7 dependent blocks: ~24 us at any batch up to 8).  Partial
-// sums are added in a fixed order; results agree with k_heads_fc to fp32
-// rounding (different summation order).
+// rows in 7 + 4 dependent blocks: ~24 us at any batch up to 8).  Partial
+// sums are added in k_heads_fc's order, so rows are bit-identical between
+// the two kernels.
 constexpr int kH1Max = 2048;  // batches up to this take k_heads_fc1 (HZ_HEADS1_MAX overrides; equal at 2048, 0.8 % slower at 4096)
 __global__ void __launch_bounds__(1024) k_heads_fc1(const float *__restrict__ x, const float *__restrict__ glob,
                                                     const float *__restrict__ hw, const float *__restrict__ hb,
@@ -1667,7 +1679,7 @@ __global__ void __launch_bounds__(1024) k_heads_fc1(const float *__restrict__ x,
     lg[t] = a + bp[t];
   } else if (t >= 256 && t < 512) {
     const int u = t - 256;
-    float h = ((p3[0][u] + p3[1][u]) + (p3[2][u] + p3[3][u])) + b1[u];
+    float h = (((p3[0][u] + p3[1][u]) + p3[2][u]) + p3[3][u]) + b1[u];  // k_heads_fc's order
     h = h > 0.f ? h : 0.f;
     const float c = wave_sum(h * w2[u]);
     if (lane == 0) vpart[w - 4] = c;

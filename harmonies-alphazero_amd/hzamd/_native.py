@@ -53,6 +53,8 @@ _SIGS = {
     "hz_mcts_set_eval_counter": ([_vp, _vp], _c.c_int),
     "hz_mcts_expand_backup_gathered": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
     "hz_mcts_result": ([_vp, _vp], _c.c_int),
+    "hz_root_noise": ([_vp, _c.c_int32, _c.c_uint64, _c.c_uint64, _c.c_uint64, _c.c_double, _vp, _vp, _vp],
+                      _c.c_int),
     "hz_mcts_stats": ([_vp, _vp], _c.c_int),
     "hz_mcts_leaf_ptrs": ([_vp, _vp, _vp], _c.c_int),
     "hz_bias_act": ([_vp, _vp, _vp, _c.c_int64, _c.c_int32, _vp], _c.c_int),

@@ -71,6 +71,7 @@ class ModelManager:
         if self.device.type != "cuda":
             return None
         tensors = list(self.model.parameters()) + list(self.model.buffers())
+        # (invalidate_fold() clears _folded_sig for writes that bump no counter)
         sig = tuple((t.data_ptr(), t._version) for t in tensors)
         if self._folded is None or sig != self._folded_sig:
             from .infer import FoldedNet
@@ -124,13 +125,43 @@ class ModelManager:
         t, p, v = self.train_step_async(board_tensor, global_features_tensor, target_policies, target_values)
         return t.item(), p.item(), v.item()
 
+    def invalidate_fold(self):
+        """Weights changed behind PyTorch's version counters (a replayed HIP
+        graph's optimizer step does not bump them): re-fold on the next predict."""
+        self._folded_sig = None
+
     # -- checkpoints -----------------------------------------------------------
+    def _portable_optimizer_state(self):
+        """optimizer.state_dict() in the reference's form: a capturable GPU
+        Adam keeps its step counters on the device and saves capturable=True,
+        which a CPU Adam (model.py:199) cannot step after loading; the file
+        gets capturable=False and host step counters."""
+        sd = self.optimizer.state_dict()
+        groups = [dict(g, capturable=False) if "capturable" in g else dict(g) for g in sd["param_groups"]]
+        state = {k: {kk: (vv.detach().to("cpu", torch.float32) if kk == "step" and torch.is_tensor(vv) else vv)
+                     for kk, vv in st.items()} for k, st in sd["state"].items()}
+        return {"state": state, "param_groups": groups}
+
+    def _adopt_optimizer_device(self):
+        """After optimizer.load_state_dict: the groups' capturable flag comes
+        from the file; set it for this device (capturable on the GPU, so that
+        training can be graphed; plain on the CPU, as the reference) and move
+        the step counters where that mode keeps them."""
+        cap = self.device.type == "cuda"
+        for g in self.optimizer.param_groups:
+            if "capturable" in g:
+                g["capturable"] = cap
+                for p in g["params"]:
+                    st = self.optimizer.state.get(p)
+                    if st and torch.is_tensor(st.get("step")):
+                        st["step"] = st["step"].to(p.device if cap else "cpu", torch.float32)
+
     def save_checkpoint(self, folder="checkpoints", filename="checkpoint.pth.tar", iteration=None):
         path = Path(folder)
         path.mkdir(parents=True, exist_ok=True)
         state = {"model_config": self.model_config, "training_config": self.training_config,
                  "model_state_dict": self.model.state_dict(),
-                 "optimizer_state_dict": self.optimizer.state_dict()}
+                 "optimizer_state_dict": self._portable_optimizer_state()}
         if self.scheduler:
             state["scheduler_state_dict"] = self.scheduler.state_dict()
         if iteration is not None:
@@ -147,6 +178,8 @@ class ModelManager:
             ck = torch.load(path, map_location=self.device, weights_only=True)
             self.model.load_state_dict(ck["model_state_dict"])
             self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+            self._adopt_optimizer_device()
+            self.invalidate_fold()
             if self.scheduler and "scheduler_state_dict" in ck:
                 self.scheduler.load_state_dict(ck["scheduler_state_dict"])
             it = ck.get("iteration", 0)

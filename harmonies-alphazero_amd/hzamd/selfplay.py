@@ -28,23 +28,24 @@ MCTS_DEFAULT = {  # config.py:53-65 (the self-play config)
 
 class NoiseSource:
     """Root Dirichlet noise (MCTS.py:314-316) and the tau=1 uniforms, drawn on
-    the device from a generator seeded by (seed, first global board id, move
-    counter): a rank's 4096 boards get the same draws whatever the GPU count."""
+    the device by hz_root_noise from a counter-based generator keyed by
+    (seed, global board id = board_base + b, move counter): a board's draws
+    are the same whatever batch it sits in and whatever the GPU count."""
 
-    def __init__(self, seed, device):
+    def __init__(self, board_base, device, seed=0):
+        self.board_base = int(board_base)
         self.seed = int(seed)
-        self.device = device
-        self.gen = torch.Generator(device=device)
+        self.device = torch.device(device)
 
     def draw(self, step, counts, alpha):
-        self.gen.manual_seed((self.seed * 1000003 + step) & ((1 << 63) - 1))
         n = counts.numel()
-        conc = torch.full((n, MAX_CHILDREN), float(alpha), dtype=torch.float64, device=self.device)
-        g = torch._standard_gamma(conc, generator=self.gen)
-        live = torch.arange(MAX_CHILDREN, device=self.device).unsqueeze(0) < counts.unsqueeze(1)
-        g = torch.where(live, g, torch.zeros_like(g))
-        noise = g / g.sum(1, keepdim=True).clamp_min(1e-300)
-        u = torch.rand(n, dtype=torch.float64, device=self.device, generator=self.gen)
+        counts = counts.to(device=self.device, dtype=torch.int32).contiguous()
+        noise = torch.empty(n, MAX_CHILDREN, dtype=torch.float64, device=self.device)
+        u = torch.empty(n, dtype=torch.float64, device=self.device)
+        nat.check(nat.lib().hz_root_noise(nat.ptr(counts), n, self.seed & (2**64 - 1),
+                                          self.board_base & (2**64 - 1), int(step) & (2**64 - 1), float(alpha),
+                                          nat.ptr(noise), nat.ptr(u), nat.stream_ptr(self.device)),
+                  "hz_root_noise")
         return noise, u
 
 

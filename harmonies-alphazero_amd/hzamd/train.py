@@ -104,6 +104,10 @@ class GraphedStep:
             for dst, x in zip(self.static, (board, glob, pi, z)):
                 dst.copy_(x)
         self.graph.replay()
+        # the replayed optimizer step bumps no version counter: tell the
+        # manager its folded inference copy is stale
+        if hasattr(m, "invalidate_fold"):
+            m.invalidate_fold()
         return self.out
 
 

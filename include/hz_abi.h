@@ -192,6 +192,14 @@ int hz_mcts_expand_backup(hz_mcts *mcts, hz_env *env, const float *policy, const
  * hz_mcts_gather_leaves (board b reads row j where rows[j] = b) */
 int hz_mcts_expand_backup_gathered(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
                                    const double *noise, double eps, int32_t testing);
+/* Self-play root noise (MCTS.py:314-316, np.random.dirichlet([alpha] * L)
+ * over the L = count[b] legal moves, in legal-move order) into noise[n][69]
+ * (zeros past L) and the tau = 1 move-choice uniform (MCTS.py:411,
+ * np.random.choice) into u[n] (may be NULL), from a counter-based generator
+ * keyed by (seed, global board id = board_base + b, move): a board's draws do
+ * not depend on the batch or the GPU count.  Enqueued on `stream`. */
+int hz_root_noise(const int32_t *count, int32_t n, uint64_t seed, uint64_t board_base, uint64_t move, double alpha,
+                  double *noise, double *u, void *stream);
 /* root visit counts by action id: visits[n][143] (MCTS.py:355-376) */
 int hz_mcts_result(hz_mcts *mcts, int32_t *visits);
 /* per-board [nodes, edges, search generation, overflow flag] -> counts[n][4] */

@@ -51,8 +51,13 @@ def test_bench_two_ranks_rehearsal():
     sp = d["selfplay"]
     assert sp["n_gpus"] == 2 and sp["sims_per_s"] > 0
     x = sp["exchange"]
-    # two ranks x 256 boards x 2 timed moves of records, all-gathered
-    assert x["records"] == 2 * 256 * 2 and x["bytes_per_rank_received"] == x["records"] * 336
+    # the complete games' records of both ranks, all-gathered
+    assert x["records"] == sp["game"]["moves"] and x["bytes_per_rank_received"] == x["records"] * 336
+    assert 2 * 256 * 40 <= x["records"] <= 2 * 256 * 100
+    assert sp["games_per_s_basis"].startswith("complete games") and sp["game"]["games"] == 2 * 256
+    # every rank checked its own boards against the C twin and the oracle
+    assert sp["parity"].startswith("512/512 boards bit-exact vs C twin")
+    assert "8192/8192 boards bit-exact vs C oracle" in d["parity"]
 
 
 def test_bench_single_rank_contract():
@@ -74,7 +79,10 @@ def test_bench_single_rank_contract():
         assert k in sp, k
     assert sp["exchange"] is None
     assert sp["sims"] == 256 * 16 * 2 and 0 < sp["nn_rows_evaluated"] <= sp["sims"]
-    assert 0 < sp["nn_roofline"]["frac"] < 1
+    assert 0 < sp["nn_roofline"]["frac"] < 1 and sp["nn_roofline"]["fp32_mfma_frac"] > 0
+    assert sp["parity"].startswith("256/256 boards bit-exact vs C twin")
+    assert sp["games_per_s_basis"].startswith("complete games") and sp["game"]["games"] == 256
+    assert "load_checkpoint" in sp["network"]
     for k in ("value", "unit", "cores", "kind", "sample", "nn_cpu_ms_per_eval"):
         assert k in sp["cpu_baseline"], k
 
@@ -117,3 +125,59 @@ def test_config1_single_game_contract():
         assert k in d, k
     assert d["unit"] == "games/s" and d["value"] > 0 and d["steps"] == 1
     assert 40 <= d["plies"][0] <= 100
+
+
+def test_config4_stub_records_replayed_by_oracle(tmp_path):
+    """Config 4 at world 2 with the stub evaluator (--stub): each rank's own
+    records of both iterations (state, visit counts, z, player) are replayed
+    board by board by the C twin's search (oracle.mcts_search with the
+    logged root noise and uniforms, MCTS.py:272-441) and engine
+    (trainer.py:468-538's ply loop): states, visits, moves and z agree."""
+    import numpy as np
+    import oracle
+    from hzamd import distributed as hd
+    from hzamd.state import unpack_ref
+    n = 48
+    _torchrun(["--config", "4", "--boards", str(n), "--sims", "6", "--iterations", "2", "--warmup", "2", "--stub",
+               "--records-out", str(tmp_path / "s")], 29523)
+    checked = 0
+    for rank in (0, 1):
+        d = torch.load(tmp_path / f"s.rank{rank}.pt", weights_only=True)
+        assert d["stub"] and d["sims"] == 6
+        base = int(d["seed_base"])
+        states, visits, z, player = (t.numpy() for t in hd.unpack_records(d["own"]))
+        noise, u, act = d["noise"].numpy(), d["u"].numpy(), d["act"].numpy()
+        counts = d["own_counts"].tolist()
+        off = step = 0
+        for it in range(2):
+            # env.reset() before the warm-up moves started episode 0; iteration it plays episode it + 1
+            ms = [oracle.mt_seed(base + b + ((it + 1) << 32)) for b in range(n)]
+            ss = [oracle.reset(m) for m in ms]
+            start, ply, ends = off, 0, {}
+            while True:
+                live = [b for b in range(n) if not oracle.is_game_over(ss[b])]
+                if not live:
+                    break
+                for b in live:
+                    r = off
+                    assert (unpack_ref(states[r]) == ss[b]).all(), (rank, it, ply, b)
+                    assert player[r] == ss[b][72]
+                    a, ov, _, _ = oracle.mcts_search(ss[b], ms[b], 6, 2.0, eps=0.25, testing=False, tau0=15,
+                                                     ply=ply, u=float(u[step, b]),
+                                                     noise=np.concatenate([noise[step, b], np.zeros(143 - 69)]))
+                    assert (visits[r] == ov).all(), (rank, it, ply, b)
+                    assert a == act[step, b], (rank, it, ply, b)
+                    rc, ss[b] = oracle.step(ss[b], a, ms[b])
+                    assert rc == 0
+                    ends.setdefault(b, []).append(r)
+                    off += 1
+                    checked += 1
+                ply += 1
+                step += 1
+            assert ply == int(d["plies"][it]) and off - start == counts[it]
+            for b, rows in ends.items():
+                w = int(ss[b][75])
+                outcome = 1.0 if w == 0 else -1.0 if w == 1 else 0.0
+                for r in rows:
+                    assert z[r] == (outcome if player[r] == 0 else -outcome), (rank, it, b)
+    assert checked > 2 * 2 * n * 40

@@ -470,3 +470,36 @@ def test_split_tower_matches_resident_tower(batch):
     live = torch.tensor([k], dtype=torch.int32, device="cuda")
     got = _tower_split(x, *fnet.resident, live)
     assert torch.equal(got[:k], want[:k])
+
+
+def test_predict_rows_do_not_depend_on_batch_size():
+    """A board's priors and value are the same bits whatever batch it is
+    evaluated in: every kernel form the batch size selects (split tower <= 32
+    rows, resident tower <= 1,024, one-state and eight-state layered convs,
+    k_heads_fc1 <= 2,048 and k_heads_fc above) sums in the same order, so a
+    self-play board's search does not depend on how many boards share its
+    GPU (config 4 at any boards-per-GPU split)."""
+    from hzamd.infer import _heads_fc
+    g = torch.Generator().manual_seed(21)
+    torch.manual_seed(2)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    n = 4096
+    board = (torch.rand(n, 38, 5, 7, generator=g) > 0.8).float()
+    board[:, 37] = torch.randint(0, 3, (n, 1, 1), generator=g).float() / 3.0
+    glob = torch.rand(n, 42, generator=g)
+    fnet = FoldedNet(net.to("cuda"))
+    board, glob = board.cuda(), glob.cuda()
+    p_full, v_full = fnet.predict(board, glob)
+    for s in (1, 7, 10, 11, 32, 33, 300, 768, 769, 1024, 1025, 2048, 2049):
+        p, v = fnet.predict(board[:s].contiguous(), glob[:s].contiguous())
+        assert torch.equal(p, p_full[:s]) and torch.equal(v, v_full[:s]), s
+    # the two head kernels directly: rows of a 2,049-row call (k_heads_fc)
+    # equal those of a 300-row call (k_heads_fc1)
+    cl = torch.channels_last
+    x = torch.randn(2049, 128, 5, 7, generator=g).relu().cuda().contiguous(memory_format=cl)
+    gl = torch.rand(2049, 42, generator=g).cuda()
+    lo, pr, v = _heads_fc(x, gl, *fnet.heads, fnet.fc, logits=True, probs=True)
+    lo1, pr1, v1 = _heads_fc(x[:300].contiguous(memory_format=cl), gl[:300].contiguous(), *fnet.heads, fnet.fc,
+                             logits=True, probs=True)
+    assert torch.equal(lo1, lo[:300]) and torch.equal(pr1, pr[:300]) and torch.equal(v1, v[:300])

@@ -60,6 +60,32 @@ def test_forced_lr_reset_on_load():
     assert mm.scheduler.last_epoch == 1 and mm.get_current_lr() == 0.000125
 
 
+def test_capturable_checkpoint_trains_on_cpu(tmp_path):
+    """A checkpoint whose Adam groups say capturable=True (a GPU manager's
+    optimizer state) loads into a CPU manager that can still train: the
+    flag is set for the loading device and the step counters move to the
+    host; our own files are written with capturable=False."""
+    torch.manual_seed(4)
+    a = ModelManager(MODEL_CFG, TRAIN_CFG)
+    b, g = torch.rand(4, 38, 5, 7), torch.rand(4, 42)
+    pi = torch.softmax(torch.rand(4, 143), 1)
+    a.train_step(b, g, pi, torch.zeros(4, 1))
+    a.save_checkpoint(folder=tmp_path, filename="a.pth.tar", iteration=1)
+    ck = torch.load(tmp_path / "a.pth.tar", weights_only=True)
+    assert all(not gr.get("capturable", False) for gr in ck["optimizer_state_dict"]["param_groups"])
+    for gr in ck["optimizer_state_dict"]["param_groups"]:
+        gr["capturable"] = True                      # as a GPU-written file of round 2 had it
+    torch.save(ck, tmp_path / "gpu.pth.tar")
+    c = ModelManager(MODEL_CFG, TRAIN_CFG)
+    assert c.load_checkpoint(folder=tmp_path, filename="gpu.pth.tar") == (True, 1)
+    assert all(gr["capturable"] is False for gr in c.optimizer.param_groups)
+    loss = c.train_step(b, g, pi, torch.zeros(4, 1))
+    a.train_step(b, g, pi, torch.zeros(4, 1))
+    for k, v in a.model.state_dict().items():
+        assert torch.equal(c.model.state_dict()[k], v), k
+    assert np.isfinite(loss).all()
+
+
 def test_checkpoint_round_trip(tmp_path):
     torch.manual_seed(3)
     a = ModelManager(MODEL_CFG, TRAIN_CFG)

@@ -84,3 +84,67 @@ def test_selfplay_with_network_runs():
     assert set(np.unique(z)).issubset({-1.0, 0.0, 1.0})
     out = sp.outcomes(rec["final"]).cpu().numpy()
     assert (np.abs(out) <= 1).all()
+
+
+def test_root_noise_keyed_by_global_board():
+    """hz_root_noise: Dirichlet rows over the live children (sum 1, zeros past
+    the legal count), u in [0, 1), and every board's draws depend only on
+    (seed, global board id, move): the same in a 64-board batch and in a
+    32-board batch whose board_base is 32 further on."""
+    from hzamd.selfplay import NoiseSource
+    g = torch.Generator().manual_seed(3)
+    cnt = torch.randint(0, 70, (64,), generator=g, dtype=torch.int32).to(DEV)
+    cnt[0], cnt[1] = 0, 69
+    a = NoiseSource(1000, DEV)
+    noise, u = a.draw(5, cnt, 0.4)
+    live = torch.arange(69, device=DEV).unsqueeze(0) < cnt.unsqueeze(1).long()
+    assert (noise[~live] == 0).all() and (noise >= 0).all()
+    s = noise.sum(1)
+    assert torch.allclose(s[cnt > 0], torch.ones_like(s[cnt > 0]), atol=1e-12)
+    assert ((u >= 0) & (u < 1)).all()
+    b = NoiseSource(1032, DEV)
+    n2, u2 = b.draw(5, cnt[32:].contiguous(), 0.4)
+    assert torch.equal(n2, noise[32:]) and torch.equal(u2, u[32:])
+    n3, _ = a.draw(6, cnt, 0.4)
+    assert not torch.equal(n3, noise)
+
+
+def test_root_noise_is_dirichlet():
+    """Moments of Dirichlet(0.4 * 1_L) at L = 10 over 8,192 draws: mean 1/L,
+    variance a(a0 - a) / (a0^2 (a0 + 1)) = 0.018, within sampling error."""
+    from hzamd.selfplay import NoiseSource
+    n, L = 8192, 10
+    cnt = torch.full((n,), L, dtype=torch.int32, device=DEV)
+    noise, u = NoiseSource(0, DEV).draw(0, cnt, 0.4)
+    x = noise[:, :L].double()
+    assert abs(x.mean().item() - 0.1) < 0.003
+    var = x.var(0).mean().item()
+    assert abs(var - 0.018) < 0.0015, var
+    assert abs(u.mean().item() - 0.5) < 0.02
+
+
+@pytest.mark.parametrize("net", [False, True])
+def test_selfplay_split_invariant(net):
+    """Per-board self-play records do not depend on how boards are split over
+    GPUs: 2 x 24 boards (board bases 700, 724) give
+    the same states, visit counts, validity and final states, board by
+    board, as 1 x 48 (base 700): the root noise is keyed by global board id
+    and every evaluator row is computed independently of its batch."""
+    from hzamd.mcts import BatchedPredictor, stub_evaluator
+    from hzamd.net import TINY, HarmoniesNet
+    from hzamd.selfplay import SelfPlay
+    cfg = {"num_simulations": 6, "cpuct": 2.0, "testing": False, "turns_until_tau0": 15}
+    if net:
+        torch.manual_seed(0)
+        ev = BatchedPredictor(HarmoniesNet().to(DEV).eval())
+    else:
+        ev = stub_evaluator
+    recs = [SelfPlay(n, ev, cfg, seed_base=base, device=DEV).play() for n, base in ((48, 700), (24, 700), (24, 724))]
+    whole, parts = recs[0], recs[1:]
+    for k, part in enumerate(parts):
+        sl = slice(24 * k, 24 * k + 24)
+        T = part["plies"]
+        assert torch.equal(part["valid"], whole["valid"][:T, sl]) and not whole["valid"][T:, sl].any()
+        assert torch.equal(part["states"], whole["states"][:T, :, sl])
+        assert torch.equal(part["visits"], whole["visits"][:T, sl])
+        assert torch.equal(part["final"], whole["final"][:, sl])
