@@ -1258,6 +1258,74 @@ __global__ void __launch_bounds__(192, 1)
 }
 }  // namespace
 
+// Workgroups of k_tower_x6_split the current device holds at once (its CU
+// count x the kernel's occupancy per CU, from the occupancy API), cached per
+// device; 0 if the query fails.  A launch whose grid exceeds it could leave
+// groups waiting for groups that cannot start, so hz_tower_x6_split refuses
+// it (HZ_E_NOT_RESIDENT) and the caller takes the resident tower.
+static std::atomic<int32_t> g_split_group_limit{0};  // hz_tower_x6_split_set_limit (0: none)
+
+static int32_t split_resident_groups_device();
+static int32_t split_resident_groups() {
+  const int32_t v = split_resident_groups_device(), lim = g_split_group_limit.load(std::memory_order_relaxed);
+  return lim > 0 && lim < v ? lim : v;
+}
+
+static int32_t split_resident_groups_device() {
+  static std::atomic<int32_t> cache[64];
+  static std::atomic<uint64_t> known{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (known.load(std::memory_order_acquire) >> dev & 1) return cache[dev].load(std::memory_order_relaxed);
+  hipDeviceProp_t prop;
+  int per_cu = 0, per_cu3 = 0;
+  int32_t v = 0;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+      hipFuncSetAttribute((const void *)k_tower_x6_split<4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kTSLds) == hipSuccess &&
+      hipFuncSetAttribute((const void *)k_tower_x6_split<4, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kTSLds) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_tower_x6_split<4, 1>, 192, kTSLds) ==
+          hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, (const void *)k_tower_x6_split<4, 3>, 192, kTSLds) ==
+          hipSuccess) {
+    const int pc = per_cu < per_cu3 ? per_cu : per_cu3;
+    v = pc > 0 ? (int32_t)(pc * prop.multiProcessorCount) : 0;
+  }
+  cache[dev].store(v, std::memory_order_relaxed);
+  known.fetch_or(1ull << dev, std::memory_order_release);
+  return v;
+}
+
+// the split tower's workgroups per state at a batch (the one-row-block form
+// up to rb1max states, 24 per state; else 8)
+static int32_t split_groups_per_state(int32_t batch, int32_t rb1max) { return batch <= rb1max ? 3 * kTSG : kTSG; }
+
+static int32_t split_rb1max() {
+  // one row block per workgroup (3 x kTSG groups per state) up to this batch
+  // (HZ_TS_RB1_MAX; at most 256 / (3 x kTSG))
+  static const int rb1max = [] {
+    const char *e = getenv("HZ_TS_RB1_MAX");
+    const int v = e ? atoi(e) : kTSRb1Max;
+    return v < 0 ? 0 : v > 256 / (3 * kTSG) ? 256 / (3 * kTSG) : v;
+  }();
+  return rb1max;
+}
+
+extern "C" int hz_tower_x6_split_set_limit(int32_t groups) {
+  if (groups < 0) return -1;
+  g_split_group_limit.store(groups, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int32_t hz_tower_x6_split_max_batch(void) {
+  const int32_t cap = split_resident_groups(), rb1max = split_rb1max();
+  int32_t best = 0;
+  for (int32_t b = 1; b <= kTSMaxBatch; b++)
+    if (b * split_groups_per_state(b, rb1max) <= cap && b * split_groups_per_state(b, rb1max) <= 256) best = b;
+  return best;
+}
+
 extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const float *bias, float *out, float *xch,
                                  uint32_t *sync, int32_t nconv, int32_t batch, const int32_t *live, void *stream) {
   if (!x0 || !wpack6 || !bias || !out || !xch || !sync || batch < 0 || batch > kTSMaxBatch || nconv < 2 ||
@@ -1265,20 +1333,16 @@ extern "C" int hz_tower_x6_split(const float *x0, const void *wpack6, const floa
     return -1;
   if (((uintptr_t)x0 | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)xch | (uintptr_t)sync) & 15) return -1;
   if (batch == 0) return 0;
+  // every workgroup of the launch must be resident at once (the hand-off
+  // waits on all of them): refuse a grid the device cannot hold
+  if (batch * split_groups_per_state(batch, split_rb1max()) > split_resident_groups()) return -2;
   // K-steps of B fragments in flight (HZ_TS_AHEAD=12 for measurements; 4,
   // 6, 9, 12 and 18 measured alike with three row blocks per workgroup)
   static const int ahead = [] {
     const char *e = getenv("HZ_TS_AHEAD");
     return e && atoi(e) == 12 ? 12 : kTSAhead;
   }();
-  // one row block per workgroup (3 x kTSG groups per state) up to this batch
-  // (HZ_TS_RB1_MAX; at most 256 / (3 x kTSG) so that every group is resident)
-  static const int rb1max = [] {
-    const char *e = getenv("HZ_TS_RB1_MAX");
-    const int v = e ? atoi(e) : kTSRb1Max;
-    return v < 0 ? 0 : v > 256 / (3 * kTSG) ? 256 / (3 * kTSG) : v;
-  }();
-  const bool rb1 = batch <= rb1max;
+  const bool rb1 = batch <= split_rb1max();
   static std::atomic<uint64_t> init_mask{0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;

@@ -65,6 +65,8 @@ _SIGS = {
     "hz_stem3x3_x6_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_resident": ([_vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_tower_x6_split_max_batch": ([], _c.c_int32),
+    "hz_tower_x6_split_set_limit": ([_c.c_int32], _c.c_int),
     "hz_stem3x3_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_version": ([], _c.c_char_p),
 }

@@ -96,20 +96,68 @@ def _tower_resident(x, allw, allb, live=None):
     return out
 
 
-_SPLIT_SYNC = {}  # device -> the hand-off counter block (zeroed once; every launch leaves it zeroed)
+_SPLIT_SYNC = {}  # (device, stream) -> hand-off counter block (zeroed once; every launch leaves it zeroed)
+_SPLIT_CAP = {}   # device -> the largest batch hz_tower_x6_split accepts there (occupancy API)
+_SPLIT_PENDING = set()  # devices with split-tower launches since the last check_split_timeouts()
+SPLIT_TIMEOUT_WORD = 32 * 32
 
 
-def _split_sync(device):
-    t = _SPLIT_SYNC.get(device)
+def _split_sync(device, stream=None):
+    """The counter block of the split tower's launches on (device, stream):
+    a block is used by the launches of one stream only, in stream order
+    (launches on two streams sharing one block would corrupt its counters)."""
+    stream = torch.cuda.current_stream(device) if stream is None else stream
+    key = (device, stream.cuda_stream)
+    t = _SPLIT_SYNC.get(key)
     if t is None:
-        t = _SPLIT_SYNC[device] = torch.zeros(33 * 32, dtype=torch.int32, device=device)
+        t = _SPLIT_SYNC[key] = torch.zeros(33 * 32, dtype=torch.int32, device=device)
     return t
+
+
+def split_max_batch(device):
+    """Largest batch the split tower may run on `device` with all its
+    workgroups resident at once (hz_tower_x6_split_max_batch: CU count x
+    occupancy); larger batches take the resident tower."""
+    cap = _SPLIT_CAP.get(device)
+    if cap is None:
+        with torch.cuda.device(device):
+            cap = _SPLIT_CAP[device] = int(lib().hz_tower_x6_split_max_batch())
+    return cap
+
+
+def check_split_timeouts(device=None):
+    """Raise NativeError if a split-tower hand-off on `device` (all devices
+    when None) gave up waiting since the last check (its state's outputs
+    came out NaN); the timeout word is cleared first, so a caller may retry.
+    Reads one word per counter block (a device -> host copy: never call it
+    inside a graph capture)."""
+    if device is not None:
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+    if not _SPLIT_PENDING or (device is not None and device not in _SPLIT_PENDING):
+        return
+    if device is None:
+        _SPLIT_PENDING.clear()
+    else:
+        _SPLIT_PENDING.discard(device)
+    bad = []
+    for (dev, _), t in list(_SPLIT_SYNC.items()):
+        if device is not None and torch.device(dev) != device:
+            continue
+        if int(t[SPLIT_TIMEOUT_WORD].item()) != 0:
+            t[SPLIT_TIMEOUT_WORD] = 0
+            bad.append(str(dev))
+    if bad:
+        raise NativeError(f"split tower: a hand-off timed out on {', '.join(bad)} (workgroups not co-resident: is "
+                          "another process sharing the GPU?); the affected predictions were NaN and are discarded")
 
 
 def _tower_split(x, allw, allb, live=None, sync_out=None):
     """_tower_resident with 24 or 8 workgroups per state (hz_tower_x6_split,
     batch <= 32): bit-identical, the weights streamed by 8 CUs per state.
-    The counter block is shared per device: calls run in stream order.
+    Returns None (nothing enqueued) when the device cannot hold the launch's
+    workgroups at once (the caller takes the resident tower).
     sync_out (list, tests): receives the counter/timeout block."""
     B = x.shape[0]
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
@@ -123,8 +171,11 @@ def _tower_split(x, allw, allb, live=None, sync_out=None):
     rc = lib().hz_tower_x6_split(x.data_ptr(), allw.data_ptr(), allb.data_ptr(), out.data_ptr(), xch.data_ptr(),
                                  sync.data_ptr(), allw.shape[0], B, _live_ptr(live),
                                  torch.cuda.current_stream(x.device).cuda_stream)
+    if rc == -2:  # HZ_E_NOT_RESIDENT: the grid exceeds what the device holds at once
+        return None
     if rc != 0:
         raise NativeError(f"hz_tower_x6_split failed ({rc})")
+    _SPLIT_PENDING.add(x.device)
     if sync_out is not None:
         sync_out.append(sync)
     return out
@@ -372,9 +423,13 @@ class FoldedNet(nn.Module):
             x = (_stem_x6_act if self.tower == "x6" else _stem_act)(board, self.stem_packed, b, live)
         else:
             x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
-        if self.resident is not None and board.shape[0] <= min(self.split_max, 32):
-            x = _tower_split(x, *self.resident, live)
-        elif self.resident is not None and board.shape[0] <= self.resident_max:
+        B = board.shape[0]
+        xs = None
+        if self.resident is not None and B <= min(self.split_max, split_max_batch(board.device)):
+            xs = _tower_split(x, *self.resident, live)
+        if xs is not None:
+            x = xs
+        elif self.resident is not None and B <= max(self.resident_max, min(self.split_max, 32)):
             x = _tower_resident(x, *self.resident, live)
         elif self.packed is not None:
             conv = _conv3x3_x6_act if self.tower == "x6" else _conv3x3_act

@@ -96,7 +96,9 @@ class ModelManager:
             board = board_tensor.to(self.device, torch.float32)
             glob = global_features_tensor.to(self.device, torch.float32)
             if fast is not None:
+                from .infer import check_split_timeouts
                 probs, value = fast.predict(board.contiguous(), glob.contiguous())
+                check_split_timeouts(self.device)  # never hand a timed-out (NaN) prediction back
             else:
                 logits, value = self.model(board, glob)
                 probs = torch.softmax(logits, dim=1)

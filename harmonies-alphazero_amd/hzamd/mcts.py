@@ -179,7 +179,7 @@ class BatchedMCTS:
                     self._graph_cache = (key, g, gk[0])  # holds the network: its id stays unique
             for _ in range(total - 1):
                 g.replay()
-            return self.result()
+            return self._finish()
         for _ in range(total):
             self.select(cpuct, active)
             if not gather:
@@ -200,7 +200,16 @@ class BatchedMCTS:
                 else:
                     policy, value = self._nil_pol, self._nil_val
             self.expand_backup(policy, value, noise, eps, testing, gathered=True)
-        return self.result()
+        return self._finish()
+
+    def _finish(self):
+        """Root visits of the search just run, after making sure no leaf
+        evaluation of it went through a timed-out split-tower hand-off (whose
+        NaN priors would have steered PUCT silently): NativeError if one did."""
+        from .infer import check_split_timeouts
+        visits = self.result()
+        check_split_timeouts(self.device)
+        return visits
 
 
 def choose_actions(visits, explore, u):

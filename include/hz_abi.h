@@ -265,6 +265,18 @@ int hz_tower_x6_resident(const float *x0, const void *wpack6, const float *bias,
 int hz_tower_x6_split(const float *x0, const void *wpack6, const float *bias, float *out, float *xch, uint32_t *sync,
                       int32_t nconv, int32_t batch, const int32_t *live, void *stream);
 
+/* Every workgroup of an hz_tower_x6_split launch must be resident at once
+ * (its hand-offs wait on all of them).  hz_tower_x6_split returns
+ * HZ_E_NOT_RESIDENT (-2), enqueuing nothing, when the launch's grid
+ * (24 workgroups per state up to 10 states, else 8) exceeds what the current
+ * device holds at once (CU count x the kernel's occupancy per CU, from the
+ * occupancy API) or the limit set here; callers then take
+ * hz_tower_x6_resident.  max_batch: the largest batch it accepts on the
+ * current device (0: none).  set_limit: cap the workgroups (0 = no cap
+ * beyond the device's), e.g. when other work shares the GPU. */
+int32_t hz_tower_x6_split_max_batch(void);
+int hz_tower_x6_split_set_limit(int32_t groups);
+
 /* The heads of model.py:336-351 up to their linear layers, BN folded:
  * pcat[b] = relu(hw[0..1] . x[b][cell] + hb[0..1]) in NCHW flatten order (70)
  * || glob[b] (42); vcat[b] = relu(hw[2] . x[b][cell] + hb[2]) (35) || glob[b].

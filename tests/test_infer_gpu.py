@@ -503,3 +503,57 @@ def test_predict_rows_do_not_depend_on_batch_size():
     lo1, pr1, v1 = _heads_fc(x[:300].contiguous(memory_format=cl), gl[:300].contiguous(), *fnet.heads, fnet.fc,
                              logits=True, probs=True)
     assert torch.equal(lo1, lo[:300]) and torch.equal(pr1, pr[:300]) and torch.equal(v1, v[:300])
+
+
+def test_split_tower_refused_when_not_resident_falls_back():
+    """hz_tower_x6_split launches only grids the device holds at once
+    (CU count x occupancy): with the workgroup limit below a launch's grid it
+    enqueues nothing (HZ_E_NOT_RESIDENT) and FoldedNet takes the resident
+    tower, bit-identical and finite; never NaN."""
+    from hzamd._native import lib
+    from hzamd.infer import _tower_split, split_max_batch
+    assert split_max_batch(torch.device("cuda", 0)) == 32  # 256 CUs hold every split launch
+    g = torch.Generator().manual_seed(77)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    fnet = FoldedNet(net.cuda())
+    board = (torch.rand(5, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    glob = torch.rand(5, 42, generator=g).cuda()
+    p0, v0 = fnet.predict(board, glob)                     # split tower (24 groups per state)
+    x = torch.rand(5, 128, 5, 7, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    try:
+        assert lib().hz_tower_x6_split_set_limit(5 * 24 - 1) == 0
+        assert lib().hz_tower_x6_split_max_batch() == 4
+        assert _tower_split(x, *fnet.resident) is None       # refused, nothing enqueued
+        p1, v1 = fnet.predict(board, glob)                 # -> resident tower
+    finally:
+        lib().hz_tower_x6_split_set_limit(0)
+    assert torch.equal(p0, p1) and torch.equal(v0, v1) and bool(torch.isfinite(p1).all())
+
+
+def test_split_tower_timeout_is_loud():
+    """A split-tower hand-off that gave up waiting (its state's outputs NaN,
+    the timeout word set) raises NativeError at the end of the search or
+    predict that used it, instead of letting NaN priors steer PUCT; the word
+    is cleared, so the next search runs normally."""
+    from hzamd._native import NativeError
+    from hzamd.env import BatchedEnv
+    from hzamd.infer import SPLIT_TIMEOUT_WORD, _split_sync
+    from hzamd.mcts import BatchedMCTS, BatchedPredictor
+    torch.manual_seed(0)
+    net = HarmoniesNet().cuda().eval()
+    ev = BatchedPredictor(net)
+    env = BatchedEnv(3, seed_base=5, device="cuda:0")
+    env.reset()
+    mcts = BatchedMCTS(env, 4)
+    v = mcts.search(ev, 2.0)                               # 3 boards: the split tower, no time-out
+    assert int(v.sum()) == 3 * 4
+    sync = _split_sync(torch.device("cuda", 0))
+    sync[SPLIT_TIMEOUT_WORD] = 1                            # as a workgroup that gave up would leave it
+    with pytest.raises(NativeError, match="timed out"):
+        mcts.search(ev, 2.0)
+    assert int(sync[SPLIT_TIMEOUT_WORD]) == 0
+    v = mcts.search(ev, 2.0)
+    assert int(v.sum()) == 3 * 4
+    mcts.close()
+    env.close()
