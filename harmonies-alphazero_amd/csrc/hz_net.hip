@@ -776,12 +776,276 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   HZ_STAMP_RT(9)
 }
 #undef HZ_X6_LOAD
-#undef HZ_STAMP
-#undef HZ_STAMP_RT
 #undef HZ_X6_STORE
 #undef HZ_X6_SYNC
 
 }  // namespace
+
+// ---- the tower conv with one wave per SIMD (the default at > 768 rows) ----
+//
+// k_conv3x3_x6<4, false, 8, 2>'s arithmetic (the same bf16x6 products in the
+// same K order per output, the same epilogue: bit-identical outputs) with 4
+// waves of up to 512 registers instead of 8 of 256: wave w = (row half
+// rh = w >> 1, output channels 64 (w & 1) .. +64), 9 row blocks x 4 column
+// blocks = 36 accumulator tiles (144 registers).
+//  - every A fragment read from LDS feeds twice the MFMAs: half the LDS read
+//    bytes per MFMA (LDS bytes cost power, and the chip holds its clock down
+//    under this kernel);
+//  - the next chunk's staging no longer runs as a block before the chunk's
+//    barrier: its global loads are issued after tap 0's wait and each staged
+//    float4 is split and stored between the MFMAs of taps 2-7, so only the
+//    barrier itself separates the chunks;
+//  - every vector-memory load of the main loop is an asm statement, issued in
+//    program order, so one counted wait per tap (vmcnt 12: the next K-step's
+//    B fragments stay in flight) covers this K-step's B fragments and the
+//    staged chunk.
+namespace {
+constexpr int kW4Stg = (kRows * 8 + 255) / 256;  // float4 staged per thread per chunk (9)
+
+__global__ void __launch_bounds__(256, 1)
+    k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
+                   const float *__restrict__ res, float *__restrict__ out, int32_t batch,
+                   const int32_t *__restrict__ live) {
+  constexpr int NQ = 4, kRBT = 9, NCB = 4;
+  constexpr int kZero = kCS * 35 * kX6Cell;  // 62,720 B: 256-B aligned
+  constexpr int kBufT = kZero + kX6Zero;
+  static_assert(kZero % 256 == 0, "zero region 256-B aligned");
+  extern __shared__ float4 lds4[];
+  char *lds = (char *)lds4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 1, chf = w & 1;
+  const int s0 = blockIdx.x * kCS;
+  if (live) batch = *live < batch ? *live : batch;
+  if (s0 >= batch) return;
+  const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+
+  if (t < 2 * kX6Zero / 16) {
+    const int b = t / (kX6Zero / 16), k = t - b * (kX6Zero / 16);
+    *(float4 *)(lds + b * kBufT + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..)
+  f32x4 stg[kW4Stg];
+  const float *gsrc[kW4Stg];
+  int ldst[kW4Stg];
+#pragma unroll
+  for (int it = 0; it < kW4Stg; it++) {
+    int f = it * 256 + t;
+    f = f < kRows * 8 ? f : kRows * 8 - 1;
+    const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
+    gsrc[it] = x + (size_t)(s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
+    ldst[it] = sc * kX6Cell + 8 * part;
+  }
+  auto stage_issue = [&](int q) {
+#pragma unroll
+    for (int it = 0; it < kW4Stg; it++)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(gsrc[it] + 32 * q) : "memory");
+  };
+  auto stage_put = [&](int it, int buf) {
+    uint2 h, m, l;
+    split4(stg[it], h, m, l);
+    char *d = lds + buf * kBufT + ldst[it];
+    *(uint2 *)d = h;
+    *(uint2 *)(d + 64) = m;
+    *(uint2 *)(d + 128) = l;
+  };
+
+  int cbase[kRBT], erow[kRBT];
+  uint32_t valid[kRBT];
+#pragma unroll
+  for (int rb = 0; rb < kRBT; rb++) {
+    int r = kX6ClassRow[rh * kRBT + rb][lane & 15];
+    r = r >= 0 ? r : kX6ClassRow[rh * kRBT + rb][0];  // padding rows read a real row (not stored)
+    const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
+    cbase[rb] = r * kX6Cell + 16 * kg;
+    uint32_t v = 0;
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+      const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
+      v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
+    }
+    valid[rb] = v;
+    erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
+  }
+  auto aoff = [&](int rb, int tap) -> int {
+    const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
+    const int a = cbase[rb] + d;
+    return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
+  };
+
+  f32x4 acc[kRBT][NCB];
+#pragma unroll
+  for (int rb = 0; rb < kRBT; rb++)
+#pragma unroll
+    for (int cb = 0; cb < NCB; cb++) acc[rb][cb] = (f32x4){};
+
+  // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
+  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
+  const int co0 = 64 * chf + (lane & 15);
+  const bf16x8 *wl = wp + co0 * 4 + kg;
+  auto bissue = [&](bf16x8(&dst)[3][NCB], int L) {
+    L = L < 9 * NQ ? L : 9 * NQ - 1;
+    const int q2 = L / 9, t2 = L - 9 * q2;
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      const bf16x8 *src = wl + ((t2 * NQ + q2) * 3 + p) * 512;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p][0]) : "v"(src) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(dst[p][1]) : "v"(src) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(dst[p][2]) : "v"(src) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:3072" : "=v"(dst[p][3]) : "v"(src) : "memory");
+    }
+  };
+  // wait until at most N vector-memory operations are outstanding; the B
+  // fragments named are then valid (the split's arithmetic cannot move above)
+#define HZ_W4_WAIT(N, b)                                                                                   \
+  asm volatile("s_waitcnt vmcnt(" #N ")"                                                                   \
+               : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[0][3]), "+v"(b[1][0]), "+v"(b[1][1]), \
+                 "+v"(b[1][2]), "+v"(b[1][3]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]), "+v"(b[2][3])   \
+               :                                                                                           \
+               : "memory")
+
+  HZ_STAMP(1)
+  stage_issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4]), "+v"(stg[5]),
+               "+v"(stg[6]), "+v"(stg[7]), "+v"(stg[8]));
+#pragma unroll
+  for (int it = 0; it < kW4Stg; it++) stage_put(it, 0);
+  bf16x8 b[3][NCB], bn[3][NCB];
+  bissue(b, 0);
+  __syncthreads();
+  HZ_STAMP(2)
+
+  auto classed = [&](auto half) {
+    constexpr int H = decltype(half)::value;
+    for (int q = 0; q < NQ; q++) {
+      const char *lb = lds + (q & 1) * kBufT;
+      const bool stage = q < NQ - 1;  // workgroup-uniform
+#pragma unroll
+      for (int tap = 0; tap < 9; tap++) {
+        const int L = q * 9 + tap;
+        bissue(bn, L + 1);
+        if (tap == 1 && stage)
+          HZ_W4_WAIT(21, b);  // the staging loads (issued at tap 0, after b) may still be in flight
+        else
+          HZ_W4_WAIT(12, b);
+        if (tap == 0 && stage) stage_issue(q + 1);
+        if (tap == 2 && stage)
+          asm volatile("" : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4]), "+v"(stg[5]),
+                       "+v"(stg[6]), "+v"(stg[7]), "+v"(stg[8]));
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          bf16x8 a[kRBT];
+#pragma unroll
+          for (int rb = 0; rb < kRBT; rb++) {
+            if (!((kX6ClassTaps[H][rb] >> tap) & 1)) continue;
+            constexpr int kNeg = 8 * kX6Cell;
+            const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell + kNeg + 64 * pa;
+            a[rb] = (kX6ClassSel[H][rb] >> tap) & 1 ? *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa)
+                                                    : *(const bf16x8 *)(lb - kNeg + cbase[rb] + d);
+          }
+#pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++)
+#pragma unroll
+            for (int rb = 0; rb < kRBT; rb++)
+              if ((kX6ClassTaps[H][rb] >> tap) & 1)
+#pragma unroll
+                for (int cb = 0; cb < NCB; cb++)
+                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
+          // the next chunk's staged float4s, split and stored among this tap's MFMAs
+          if (stage && pa == 0) {
+            const int nb = (q + 1) & 1;
+            if (tap >= 2 && tap <= 4) {
+              stage_put(2 * (tap - 2), nb);
+              stage_put(2 * (tap - 2) + 1, nb);
+            } else if (tap >= 5 && tap <= 7) {
+              stage_put(tap + 1, nb);
+            }
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+          for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (stage) __syncthreads();
+      HZ_STAMP(3 + q)
+    }
+  };
+  if (rh == 0)
+    classed(std::integral_constant<int, 0>{});
+  else
+    classed(std::integral_constant<int, 1>{});
+#undef HZ_W4_WAIT
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B ring's request past the last K-step
+
+  // Epilogue as k_conv3x3_x6: relu((acc + bias) + res) through a per-wave LDS
+  // transpose of each 16x16 tile (buffer 0: last read in chunk 2, before the
+  // barrier that closed it), float4 residual loads and stores.
+  constexpr int kTS = 20, kT = 6;
+  static_assert(4 * kT * 16 * kTS * 4 <= kZero, "per-wave tiles fit in buffer 0");
+  float *tile = (float *)lds + w * 16 * kTS * kT;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
+  const int cow = 64 * chf + tcol;
+  const int nrow = ns * 35;
+  const size_t gbase = (size_t)s0 * 35 * 128;
+  auto orow = [&](int rb) -> int {
+    const int row = erow[rb];
+    return row >= 0 && row < nrow ? row : -1;
+  };
+  // every residual load in flight at once (36 float4 per lane)
+  float4 rv[kRBT * NCB];
+#pragma unroll
+  for (int k = 0; k < kRBT * NCB; k++) {
+    const int rb = k / NCB, cb = k % NCB;
+    const int row = orow(rb);
+    rv[k] = res && row >= 0 ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 bv[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(bias + cow + 16 * cb);
+#pragma unroll
+  for (int r0 = 0; r0 < kRBT * NCB; r0 += kT) {
+#pragma unroll
+    for (int k = 0; k < kT; k++) {
+      const int rb = (r0 + k) / NCB, cb = (r0 + k) % NCB;
+#pragma unroll
+      for (int j = 0; j < 4; j++) tile[k * 16 * kTS + (4 * kg + j) * kTS + (lane & 15)] = acc[rb][cb][j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    float4 a4[kT];
+#pragma unroll
+    for (int k = 0; k < kT; k++) a4[k] = *(const float4 *)(tile + k * 16 * kTS + trow * kTS + tcol);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < kT; k++) {
+      const int rb = (r0 + k) / NCB, cb = (r0 + k) % NCB;
+      const int row = orow(rb);
+      if (row >= 0) {
+        float4 v;
+        v.x = a4[k].x + bv[cb].x;
+        v.y = a4[k].y + bv[cb].y;
+        v.z = a4[k].z + bv[cb].z;
+        v.w = a4[k].w + bv[cb].w;
+        if (res) {
+          v.x = v.x + rv[r0 + k].x;
+          v.y = v.y + rv[r0 + k].y;
+          v.z = v.z + rv[r0 + k].z;
+          v.w = v.w + rv[r0 + k].w;
+        }
+        v.x = v.x > 0.f ? v.x : 0.f;
+        v.y = v.y > 0.f ? v.y : 0.f;
+        v.z = v.z > 0.f ? v.z : 0.f;
+        v.w = v.w > 0.f ? v.w : 0.f;
+        *(float4 *)(out + gbase + (size_t)row * 128 + cow + 16 * cb) = v;
+      }
+    }
+  }
+  HZ_STAMP(7)
+}
+}  // namespace
+#undef HZ_STAMP
+#undef HZ_STAMP_RT
 
 template <int NQ, bool Stem, int CS, int NCB>
 static int launch_x6_cs(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
@@ -822,10 +1086,39 @@ static int32_t x6_tiny_max() {
   return v;
 }
 
+// the tower's 8-state conv: the 4-wave form (k_conv3x3_x6w4, bit-identical)
+// with HZ_X6_W4=1 (A/B measurements)
+static bool x6_w4() {
+  static const bool v = [] {
+    const char *e = getenv("HZ_X6_W4");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
+static int launch_x6w4(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
+                       int32_t batch, const int32_t *live, void *stream) {
+  static std::atomic<uint64_t> init_mask{0};
+  const size_t lds = 2 * (size_t)(kCS * 35 * kX6Cell + kX6Zero);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6w4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL(k_conv3x3_x6w4, dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
+                     (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 template <int NQ, bool Stem>
 static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                      int32_t batch, const int32_t *live, void *stream) {
   if (batch <= x6_tiny_max()) return launch_x6_cs<NQ, Stem, 1, 1>(x, wpack6, bias, res, out, batch, live, stream);
+  if constexpr (NQ == 4 && !Stem)
+    if (batch > x6_small_max() && x6_w4()) return launch_x6w4(x, wpack6, bias, res, out, batch, live, stream);
   return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1, 2>(x, wpack6, bias, res, out, batch, live, stream)
                                  : launch_x6_cs<NQ, Stem, 8, 2>(x, wpack6, bias, res, out, batch, live, stream);
 }

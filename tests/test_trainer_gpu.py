@@ -153,3 +153,36 @@ def test_manager_predict_uses_folded_kernels_and_follows_weight_changes():
     other = HarmoniesNet().cuda()
     mm.model.load_state_dict(other.state_dict())
     check()
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_gpu_train_step_matches_reference_fixture(graphed):
+    """ModelManager.train_step on the GPU (capturable Adam; eager, or through
+    train.GraphedStep, which replays one captured forward + backward + Adam
+    step) against the reference's CPU train steps (tests/golden/train.npz,
+    model.py:112-159): the three steps' losses and the final weights within
+    fp32 tolerance (the GPU convolutions sum in another order, and Adam
+    divides by the gradients' own scale, so differences stay at rounding)."""
+    import numpy as np
+    from hzamd.train import GraphedStep
+    from test_manager_cpu import TRAIN_CFG, fixture, state
+    f = fixture()
+    mm = ModelManager(MODEL_CFG, dict(TRAIN_CFG, device="cuda"))
+    mm.model.load_state_dict(state(f, "init/"))
+    b, g, pi, z = (torch.from_numpy(f[k]).cuda() for k in ("board", "glob", "pi", "z"))
+    if graphed:
+        gs = GraphedStep(mm, warmup=1)                      # step 1 eager, steps 2-3 replay the captured graph
+        losses = [[x.item() for x in gs.step(b, g, pi, z)] for _ in range(3)]
+        assert gs.graph is not None
+    else:
+        losses = [mm.train_step(b, g, pi, z) for _ in range(3)]
+    d_loss = np.abs(np.array(losses) - f["losses"]).max()
+    assert d_loss <= 2e-5, d_loss
+    worst = 0.0
+    for k, v in state(f, "final/").items():
+        got = mm.model.state_dict()[k].cpu()
+        if got.is_floating_point():
+            worst = max(worst, (got - v).abs().max().item())
+        else:
+            assert torch.equal(got, v), k
+    assert worst <= 5e-5, worst
