@@ -802,6 +802,20 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
 namespace {
 constexpr int kW4Stg = (kRows * 8 + 255) / 256;  // float4 staged per thread per chunk (9)
 
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+// row blocks of row half h whose tap set holds tap
+constexpr int x6_class_blocks(int h, int tap) {
+  int k = 0;
+  for (int rb = 0; rb < 9; rb++) k += (kX6ClassTaps[h][rb] >> tap) & 1;
+  return k;
+}
+
 __global__ void __launch_bounds__(256, 1)
     k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                    const float *__restrict__ res, float *__restrict__ out, int32_t batch,
@@ -817,38 +831,39 @@ __global__ void __launch_bounds__(256, 1)
   if (live) batch = *live < batch ? *live : batch;
   if (s0 >= batch) return;
   const int ns = batch - s0 < kCS ? batch - s0 : kCS;
+  HZ_STAMP(0)
+  HZ_STAMP_RT(8)
 
   if (t < 2 * kX6Zero / 16) {
     const int b = t / (kX6Zero / 16), k = t - b * (kX6Zero / 16);
     *(float4 *)(lds + b * kBufT + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..)
+  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..);
+  // the addresses are recomputed per use (registers are the constraint here)
   f32x4 stg[kW4Stg];
-  const float *gsrc[kW4Stg];
-  int ldst[kW4Stg];
-#pragma unroll
-  for (int it = 0; it < kW4Stg; it++) {
-    int f = it * 256 + t;
-    f = f < kRows * 8 ? f : kRows * 8 - 1;
-    const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
-    gsrc[it] = x + (size_t)(s < ns ? s0 * 35 + sc : (s0 + ns - 1) * 35 + cell) * 128 + 4 * part;
-    ldst[it] = sc * kX6Cell + 8 * part;
-  }
+  auto stage_f = [&](int it) {
+    const int f = it * 256 + t;
+    return f < kRows * 8 ? f : kRows * 8 - 1;
+  };
+  const int last_row = s0 * 35 + ns * 35 - 1;  // rows past the batch reread its last one
   auto stage_issue = [&](int q) {
 #pragma unroll
-    for (int it = 0; it < kW4Stg; it++)
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(stg[it]) : "v"(gsrc[it] + 32 * q) : "memory");
+    for (int it = 0; it < kW4Stg; it++) {
+      const int f = stage_f(it), sc = s0 * 35 + (f >> 3);
+      stg[it] = *(const f32x4 *)(x + (size_t)(sc < last_row ? sc : last_row) * 128 + 4 * (f & 7) + 32 * q);
+    }
   };
   auto stage_put = [&](int it, int buf) {
     uint2 h, m, l;
     split4(stg[it], h, m, l);
-    char *d = lds + buf * kBufT + ldst[it];
+    const int f = stage_f(it);
+    char *d = lds + buf * kBufT + (f >> 3) * kX6Cell + 8 * (f & 7);
     *(uint2 *)d = h;
     *(uint2 *)(d + 64) = m;
     *(uint2 *)(d + 128) = l;
   };
 
-  int cbase[kRBT], erow[kRBT];
+  int cbase[kRBT];
   uint32_t valid[kRBT];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
@@ -863,7 +878,6 @@ __global__ void __launch_bounds__(256, 1)
       v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
     }
     valid[rb] = v;
-    erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
   }
   auto aoff = [&](int rb, int tap) -> int {
     const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
@@ -885,28 +899,13 @@ __global__ void __launch_bounds__(256, 1)
     L = L < 9 * NQ ? L : 9 * NQ - 1;
     const int q2 = L / 9, t2 = L - 9 * q2;
 #pragma unroll
-    for (int p = 0; p < 3; p++) {
-      const bf16x8 *src = wl + ((t2 * NQ + q2) * 3 + p) * 512;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[p][0]) : "v"(src) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:1024" : "=v"(dst[p][1]) : "v"(src) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:2048" : "=v"(dst[p][2]) : "v"(src) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:3072" : "=v"(dst[p][3]) : "v"(src) : "memory");
-    }
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+      for (int cb = 0; cb < NCB; cb++) dst[p][cb] = wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
   };
-  // wait until at most N vector-memory operations are outstanding; the B
-  // fragments named are then valid (the split's arithmetic cannot move above)
-#define HZ_W4_WAIT(N, b)                                                                                   \
-  asm volatile("s_waitcnt vmcnt(" #N ")"                                                                   \
-               : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[0][3]), "+v"(b[1][0]), "+v"(b[1][1]), \
-                 "+v"(b[1][2]), "+v"(b[1][3]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]), "+v"(b[2][3])   \
-               :                                                                                           \
-               : "memory")
 
   HZ_STAMP(1)
   stage_issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("" : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4]), "+v"(stg[5]),
-               "+v"(stg[6]), "+v"(stg[7]), "+v"(stg[8]));
 #pragma unroll
   for (int it = 0; it < kW4Stg; it++) stage_put(it, 0);
   bf16x8 b[3][NCB], bn[3][NCB];
@@ -914,59 +913,86 @@ __global__ void __launch_bounds__(256, 1)
   __syncthreads();
   HZ_STAMP(2)
 
+  // One wave per SIMD: every instruction that is not an MFMA costs issue
+  // cycles unless it sits in an MFMA's shadow (an MFMA holds the wave's issue
+  // for 8 of its 16 cycles), so the loop is built as regions of MFMAs with
+  // their "fillers" spread one per MFMA (sched_group_barrier; taps and planes
+  // are compile-time, so every count is): the LDS reads of the next A plane
+  // (plane pa + 1 of the tap, or plane 0 of the next tap: each read has a
+  // plane's MFMAs to land in), the next K-step's B fragments (plane-0
+  // region: a whole tap to land in) and the next chunk's staging (issued in
+  // tap 0, split and stored in the plane-1 regions of taps 2-7).  Loads are
+  // compiler-tracked, so its counted waits follow them.
   auto classed = [&](auto half) {
     constexpr int H = decltype(half)::value;
+    auto aread = [&](bf16x8(&dst)[kRBT], const char *lb, auto tapc, int pa) {
+      constexpr int tap = decltype(tapc)::value;
+      static_for<0, kRBT>([&](auto rbc) {
+        constexpr int rb = decltype(rbc)::value;
+        if constexpr ((kX6ClassTaps[H][rb] >> tap) & 1) {
+          constexpr int kNeg = 8 * kX6Cell;
+          const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell + kNeg + 64 * pa;
+          if constexpr ((kX6ClassSel[H][rb] >> tap) & 1)
+            dst[rb] = *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa);
+          else
+            dst[rb] = *(const bf16x8 *)(lb - kNeg + cbase[rb] + d);
+        }
+      });
+    };
     for (int q = 0; q < NQ; q++) {
       const char *lb = lds + (q & 1) * kBufT;
       const bool stage = q < NQ - 1;  // workgroup-uniform
-#pragma unroll
-      for (int tap = 0; tap < 9; tap++) {
+      const int nb = (q + 1) & 1;
+      bf16x8 a[2][kRBT];  // [plane parity]: the plane in use, the one being read
+      aread(a[0], lb, std::integral_constant<int, 0>{}, 0);
+      static_for<0, 9>([&](auto tapc) {
+        constexpr int tap = decltype(tapc)::value;
         const int L = q * 9 + tap;
-        bissue(bn, L + 1);
-        if (tap == 1 && stage)
-          HZ_W4_WAIT(21, b);  // the staging loads (issued at tap 0, after b) may still be in flight
-        else
-          HZ_W4_WAIT(12, b);
-        if (tap == 0 && stage) stage_issue(q + 1);
-        if (tap == 2 && stage)
-          asm volatile("" : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]), "+v"(stg[4]), "+v"(stg[5]),
-                       "+v"(stg[6]), "+v"(stg[7]), "+v"(stg[8]));
-#pragma unroll
-        for (int pa = 0; pa < 3; pa++) {
-          bf16x8 a[kRBT];
-#pragma unroll
-          for (int rb = 0; rb < kRBT; rb++) {
-            if (!((kX6ClassTaps[H][rb] >> tap) & 1)) continue;
-            constexpr int kNeg = 8 * kX6Cell;
-            const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell + kNeg + 64 * pa;
-            a[rb] = (kX6ClassSel[H][rb] >> tap) & 1 ? *(const bf16x8 *)(lb + aoff(rb, tap) + 64 * pa)
-                                                    : *(const bf16x8 *)(lb - kNeg + cbase[rb] + d);
+        static_for<0, 3>([&](auto pac) {
+          constexpr int pa = decltype(pac)::value;
+          constexpr int cur = (3 * tap + pa) & 1, nxt = cur ^ 1;
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (pa < 2)
+            aread(a[nxt], lb, tapc, pa + 1);
+          else if constexpr (tap < 8)
+            aread(a[nxt], lb, std::integral_constant<int, tap + 1>{}, 0);
+          if constexpr (pa == 0) {
+            bissue(bn, L + 1);
+            if (tap == 0 && stage) stage_issue(q + 1);
+          }
+          if constexpr (pa == 1) {
+            if (stage) {
+              if constexpr (tap >= 2 && tap <= 4) {
+                stage_put(2 * (tap - 2), nb);
+                stage_put(2 * (tap - 2) + 1, nb);
+              } else if constexpr (tap >= 5 && tap <= 7) {
+                stage_put(tap + 1, nb);
+              }
+            }
           }
 #pragma unroll
           for (int pb = 0; pb < 3 - pa; pb++)
-#pragma unroll
-            for (int rb = 0; rb < kRBT; rb++)
-              if ((kX6ClassTaps[H][rb] >> tap) & 1)
+            static_for<0, kRBT>([&](auto rbc) {
+              constexpr int rb = decltype(rbc)::value;
+              if constexpr ((kX6ClassTaps[H][rb] >> tap) & 1) {
 #pragma unroll
                 for (int cb = 0; cb < NCB; cb++)
-                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
-          // the next chunk's staged float4s, split and stored among this tap's MFMAs
-          if (stage && pa == 0) {
-            const int nb = (q + 1) & 1;
-            if (tap >= 2 && tap <= 4) {
-              stage_put(2 * (tap - 2), nb);
-              stage_put(2 * (tap - 2) + 1, nb);
-            } else if (tap >= 5 && tap <= 7) {
-              stage_put(tap + 1, nb);
-            }
-          }
-        }
+                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
+              }
+            });
+          // one filler (VALU, LDS read or write, global load) after each MFMA
+          constexpr int nm = (3 - pa) * x6_class_blocks(H, tap) * NCB;
+          static_for<0, nm>([&](auto) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x322, 1, 0);
+          });
+        });
 #pragma unroll
         for (int p = 0; p < 3; p++)
 #pragma unroll
           for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      });
+      __builtin_amdgcn_sched_barrier(0);
       if (stage) __syncthreads();
       HZ_STAMP(3 + q)
     }
@@ -975,8 +1001,6 @@ __global__ void __launch_bounds__(256, 1)
     classed(std::integral_constant<int, 0>{});
   else
     classed(std::integral_constant<int, 1>{});
-#undef HZ_W4_WAIT
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B ring's request past the last K-step
 
   // Epilogue as k_conv3x3_x6: relu((acc + bias) + res) through a per-wave LDS
   // transpose of each 16x16 tile (buffer 0: last read in chunk 2, before the
@@ -988,6 +1012,9 @@ __global__ void __launch_bounds__(256, 1)
   const int cow = 64 * chf + tcol;
   const int nrow = ns * 35;
   const size_t gbase = (size_t)s0 * 35 * 128;
+  int erow[kRBT];  // the lane's output row of each block (transposed tiles: lane -> row lane >> 2)
+#pragma unroll
+  for (int rb = 0; rb < kRBT; rb++) erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
   auto orow = [&](int rb) -> int {
     const int row = erow[rb];
     return row >= 0 && row < nrow ? row : -1;
@@ -1042,6 +1069,7 @@ __global__ void __launch_bounds__(256, 1)
     }
   }
   HZ_STAMP(7)
+  HZ_STAMP_RT(9)
 }
 }  // namespace
 #undef HZ_STAMP
@@ -1613,9 +1641,12 @@ extern "C" int hz_tower_x6_split_set_limit(int32_t groups) {
 
 extern "C" int32_t hz_tower_x6_split_max_batch(void) {
   const int32_t cap = split_resident_groups(), rb1max = split_rb1max();
-  int32_t best = 0;
-  for (int32_t b = 1; b <= kTSMaxBatch; b++)
-    if (b * split_groups_per_state(b, rb1max) <= cap && b * split_groups_per_state(b, rb1max) <= 256) best = b;
+  int32_t best = 0;  // every batch up to it fits (callers route by batch <= max_batch)
+  for (int32_t b = 1; b <= kTSMaxBatch; b++) {
+    const int32_t g = b * split_groups_per_state(b, rb1max);
+    if (g > cap || g > 256) break;
+    best = b;
+  }
   return best;
 }
 

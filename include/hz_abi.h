@@ -271,8 +271,8 @@ int hz_tower_x6_split(const float *x0, const void *wpack6, const float *bias, fl
  * (24 workgroups per state up to 10 states, else 8) exceeds what the current
  * device holds at once (CU count x the kernel's occupancy per CU, from the
  * occupancy API) or the limit set here; callers then take
- * hz_tower_x6_resident.  max_batch: the largest batch it accepts on the
- * current device (0: none).  set_limit: cap the workgroups (0 = no cap
+ * hz_tower_x6_resident.  max_batch: the largest batch up to which it accepts
+ * every batch on the current device (0: none).  set_limit: cap the workgroups (0 = no cap
  * beyond the device's), e.g. when other work shares the GPU. */
 int32_t hz_tower_x6_split_max_batch(void);
 int hz_tower_x6_split_set_limit(int32_t groups);

@@ -547,13 +547,13 @@ def test_split_tower_timeout_is_loud():
     env.reset()
     mcts = BatchedMCTS(env, 4)
     v = mcts.search(ev, 2.0)                               # 3 boards: the split tower, no time-out
-    assert int(v.sum()) == 3 * 4
+    assert int(v.sum()) == 3 * (4 - 1)                     # the first simulation expands the root
     sync = _split_sync(torch.device("cuda", 0))
     sync[SPLIT_TIMEOUT_WORD] = 1                            # as a workgroup that gave up would leave it
     with pytest.raises(NativeError, match="timed out"):
         mcts.search(ev, 2.0)
     assert int(sync[SPLIT_TIMEOUT_WORD]) == 0
     v = mcts.search(ev, 2.0)
-    assert int(v.sum()) == 3 * 4
+    assert int(v.sum()) == 3 * (4 - 1)
     mcts.close()
     env.close()

