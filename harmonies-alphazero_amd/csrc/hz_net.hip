@@ -1114,12 +1114,13 @@ static int32_t x6_tiny_max() {
   return v;
 }
 
-// the tower's 8-state conv: the 4-wave form (k_conv3x3_x6w4, bit-identical)
-// with HZ_X6_W4=1 (A/B measurements)
+// the tower's 8-state conv: the 4-wave form (k_conv3x3_x6w4, bit-identical;
+// complete self-play games 131.6 vs 127.4-127.7 games/s on one box,
+// profiles/r03/ab_w4_fullgame.json) unless HZ_X6_W4=0 (A/B measurements)
 static bool x6_w4() {
   static const bool v = [] {
     const char *e = getenv("HZ_X6_W4");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   return v;
 }

@@ -1,10 +1,10 @@
 """A/B of the tower conv's 8-state forms at the leaf-eval batch, one form per
-process (the form is chosen once per process: HZ_X6_W4=1 -> the 4-wave
-k_conv3x3_x6w4, otherwise the 8-wave k_conv3x3_x6<4,false,8,2>).
+process (the form is chosen once per process: HZ_X6_W4=0 -> the 8-wave
+k_conv3x3_x6<4,false,8,2>, otherwise the 4-wave k_conv3x3_x6w4).
 Times back-to-back launches with HIP events (with and without the residual,
 interleaved in blocks so both see the same clock history), saves the outputs
 for a bitwise comparison and prints one JSON line.
-Usage (GPU box): python tools/conv_ab.py out_a.pt; HZ_X6_W4=1 python tools/conv_ab.py out_b.pt
+Usage (GPU box): HZ_X6_W4=0 python tools/conv_ab.py out_a.pt; python tools/conv_ab.py out_b.pt
                  python tools/conv_ab.py --compare out_a.pt out_b.pt"""
 import json
 import os
@@ -30,7 +30,7 @@ w = pack_conv3x3_x6(torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.
 bias = torch.randn(128, device="cuda", generator=g)
 r = torch.randn(B, 128, 5, 7, device="cuda", generator=g).contiguous(memory_format=cl)
 flop = 2.0 * B * 35 * 128 * 1152
-res = {"form": "w4" if os.environ.get("HZ_X6_W4", "0") == "1" else "w8", "batch": B}
+res = {"form": "w8" if os.environ.get("HZ_X6_W4", "1") == "0" else "w4", "batch": B}
 outs = {"res": _conv3x3_x6_act(x, w, bias, r), "nores": _conv3x3_x6_act(x, w, bias, None)}
 for _ in range(200):  # ~30 ms of warm-up: the clock settles under load
     _conv3x3_x6_act(x, w, bias, r)
