@@ -369,20 +369,30 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XFLAG(k, v)
 #endif
 static_assert(kChildLds >= kMaxChildren, "child arrays hold every legal move");
-// 12.3 KB: three waves per SIMD (was 19.5 KB with 128-row arrays: two)
+// 9.8 KB (was 12.3 KB, 19.5 KB before that).  The turn-end stream copy and
+// the children's states share their bytes (the stream is written back before
+// the first child state is stored).  The children's keys stay in LDS:
+// rebuilding a key from the child's state at each hash match instead (most
+// children of a placement meet an existing node: tile orders transpose)
+// made the kernel 3x slower (209 vs 64 us per sim step, profiles/r03).
 struct ExpandLds {
-  uint32_t mt[kMT];
+  union {
+    uint32_t mt[kMT];
+    uint64_t state[kChildLds][6];
+  };
   uint64_t script[kChildLds];
-  uint64_t state[kChildLds][6];
   uint64_t key[kChildLds][8];
   uint64_t hash[kChildLds];
   int32_t child[kChildLds];
   int32_t flag[kChildLds];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
 };
+static_assert(sizeof(uint64_t) * kChildLds * 6 >= sizeof(uint32_t) * kMT, "the states cover the stream copy");
+
 
 // expand_leaf (MCTS.py:151-218) + back_fill (:220-266) + the root Dirichlet
 // mix (:308-327).  noise[b*69 + i] is the i-th legal move's Dirichlet sample.
-__global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
+template <int Waves>  // minimum waves per SIMD the register allocation must allow (3: none forced)
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
                                                          int32_t *__restrict__ mtcur,
                                                          const float *__restrict__ policy,
                                                          const float *__restrict__ value,
@@ -454,6 +464,7 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
         }
         __syncthreads();
         for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];  // stores: no round trip to wait for
+        __syncthreads();  // the stream copy is read before the children's states overwrite it
       }
       HZ_XSTAMP(2)
       // children: lane handles child c = lane and lane + 64
@@ -486,16 +497,26 @@ __global__ void __launch_bounds__(kWave) k_expand_backup(hz_mcts m, uint32_t *__
       for (int c = lane; c < kChildSlots; c += kWave) {
         if (c >= nl) continue;
         uint64_t h = L.hash[c];
-        CKey k;
-#pragma unroll
-        for (int w = 0; w < 8; w++) k.w[w] = L.key[c][w];
         for (uint64_t slot = h & hmask;; slot = (slot + 1) & hmask) {
           uint64_t e = ht[slot];
           if ((int)(e >> 32) != gen) break;
           int nid = (int)(uint32_t)e;
           if (m.node_hash[nb + nid] != h) continue;
-          State os = load_node(m.node_state + (nb + nid) * 6);
-          if (key_eq(canon_key(os, !m.exact_keys), k)) {
+          // equal state words give equal keys: the common transposition (the
+          // same tiles placed in another order) is accepted without building
+          // the node's canonical key, which costs more than the rest of a probe
+          const uint64_t *ns = m.node_state + (nb + nid) * 6;
+          bool same = true;
+#pragma unroll
+          for (int w = 0; w < 6; w++) same = same && ns[w] == L.state[c][w];
+          bool eq = same;
+          if (!same) {
+            CKey k;
+#pragma unroll
+            for (int w = 0; w < 8; w++) k.w[w] = L.key[c][w];
+            eq = key_eq(canon_key(load_node(ns), !m.exact_keys), k);
+          }
+          if (eq) {
             L.flag[c] = nid == leaf ? 2 : 1;
             L.child[c] = nid;
             break;
@@ -813,8 +834,18 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
                          double eps, int32_t testing, const int32_t *slot) {
   if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
   float ome = (float)(1.0 - eps);
-  hipLaunchKernelGGL(k_expand_backup, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
+  // HZ_EXPAND_WAVES=4: registers capped for four waves per SIMD (spills a
+  // little); default three (A/B measurements, profiles/r03)
+  static const int waves = [] {
+    const char *e = getenv("HZ_EXPAND_WAVES");
+    return e && atoi(e) == 4 ? 4 : 3;
+  }();
+  if (waves == 4)
+    hipLaunchKernelGGL(k_expand_backup<4>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
+                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
+  else
+    hipLaunchKernelGGL(k_expand_backup<3>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
+                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
   return launch_err();
 }
 
