@@ -862,6 +862,23 @@ __global__ void __launch_bounds__(256, 1)
     *(uint2 *)(d + 64) = m;
     *(uint2 *)(d + 128) = l;
   };
+  // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
+  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
+  const int co0 = 64 * chf + (lane & 15);
+  const bf16x8 *wl = wp + co0 * 4 + kg;
+  auto bissue = [&](bf16x8(&dst)[3][NCB], int L) {
+    L = L < 9 * NQ ? L : 9 * NQ - 1;
+    const int q2 = L / 9, t2 = L - 9 * q2;
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+      for (int cb = 0; cb < NCB; cb++) dst[p][cb] = wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
+  };
+  // chunk 0's loads and the first K-step's B fragments first: the rest of
+  // the setup runs under their latency
+  stage_issue(0);
+  bf16x8 b[3][NCB], bn[3][NCB];
+  bissue(b, 0);
 
   int cbase[kRBT];
   uint32_t valid[kRBT];
@@ -891,25 +908,9 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int cb = 0; cb < NCB; cb++) acc[rb][cb] = (f32x4){};
 
-  // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
-  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
-  const int co0 = 64 * chf + (lane & 15);
-  const bf16x8 *wl = wp + co0 * 4 + kg;
-  auto bissue = [&](bf16x8(&dst)[3][NCB], int L) {
-    L = L < 9 * NQ ? L : 9 * NQ - 1;
-    const int q2 = L / 9, t2 = L - 9 * q2;
-#pragma unroll
-    for (int p = 0; p < 3; p++)
-#pragma unroll
-      for (int cb = 0; cb < NCB; cb++) dst[p][cb] = wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
-  };
-
   HZ_STAMP(1)
-  stage_issue(0);
 #pragma unroll
   for (int it = 0; it < kW4Stg; it++) stage_put(it, 0);
-  bf16x8 b[3][NCB], bn[3][NCB];
-  bissue(b, 0);
   __syncthreads();
   HZ_STAMP(2)
 
