@@ -72,7 +72,7 @@ def parse():
                     help="skip the chance-ahead-off comparison run (profiling)")
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03_traffic.json"))
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="1: one game at a time through the drop-in modules (profile_self_play.py); "
                          "2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "

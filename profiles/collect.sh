@@ -28,3 +28,6 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
 done
 python3 "$REPO/tools/pmc_summary.py" "$OUT/pmc" > "$OUT/pmc/summary.json"
 python3 "$REPO/tools/make_traffic.py" "$OUT/pmc/summary.json" "$OUT/traffic.json"
+# the per-dispatch CSVs are large (gpurun copies back at most 64 MiB): keep
+# the stats and the summaries only
+find "$OUT" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" -o -name "*.db" \) -delete
