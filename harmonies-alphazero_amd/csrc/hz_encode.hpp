@@ -84,18 +84,17 @@ __device__ __forceinline__ float glob_value(const uint64_t *__restrict__ st, lon
   return val;
 }
 
-// Glob: the wave also writes its pair's global features (small batches: one
-// launch instead of two; at 4096 items two launches measured faster)
+// One wave encodes the pair of items (j0, j0 + 1): its channel masks in the
+// wave's own LDS rows (smask / sval: 76 entries each), then the pair's 665
+// float4.  Glob: the wave also writes its pair's global features (small
+// batches: one launch instead of two; at 4096 items two launches measured
+// faster).  Only the wave's own LDS rows are touched, so a wave barrier
+// separates the two phases.
 template <bool Glob>
-__global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
-                                                      long item_stride, const int32_t *__restrict__ idx, int m,
-                                                      const int32_t *__restrict__ mcount, float *__restrict__ board,
-                                                      float *__restrict__ glob) {
-  __shared__ uint64_t smask[kEncWaves][76];
-  __shared__ float sval[kEncWaves][76];
-  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (mcount) m = *mcount < m ? *mcount : m;  // device-side item count (compacted leaf batches)
-  long j0 = 2 * ((long)blockIdx.x * kEncWaves + w);
+__device__ __forceinline__ void encode_pair(const uint64_t *__restrict__ st, long word_stride, long item_stride,
+                                            const int32_t *__restrict__ idx, int m, float *__restrict__ board,
+                                            float *__restrict__ glob, int lane, long j0, uint64_t *smask,
+                                            float *sval) {
   bool live = j0 < m;
 #pragma unroll
   for (int r = 0; r < 2; r++) {
@@ -129,7 +128,8 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
             m23 |= ((set >> code) & 1u) ? hit : 0u;
           }
           mask = to_grid35(m23);
-          val = 1.f;        } else {
+          val = 1.f;
+        } else {
           uint64_t misc = sb[5 * word_stride];
           mask = kValid35;
           if (ch == 36) {
@@ -140,11 +140,13 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
           }
         }
       }
-      smask[w][c] = mask;
-      sval[w][c] = val;
+      smask[c] = mask;
+      sval[c] = val;
     }
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (!live) return;
   int nfl = j0 + 1 < m ? 2660 : 1330;
   float *out = board + j0 * 1330;
@@ -155,8 +157,8 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
   for (int q = lane; q < nfl / 4; q += 64) {
     // the four elements lie in channel c0 and possibly c0 + 1 (boards
     // switch at element 1330 = 38 x 35: channel 38 onward is the second)
-    uint64_t ma = smask[w][c0], mb = smask[w][c0 + 1 < 76 ? c0 + 1 : c0];
-    float va = sval[w][c0], vb = sval[w][c0 + 1 < 76 ? c0 + 1 : c0];
+    uint64_t ma = smask[c0], mb = smask[c0 + 1 < 76 ? c0 + 1 : c0];
+    float va = sval[c0], vb = sval[c0 + 1 < 76 ? c0 + 1 : c0];
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
   }
   if (nfl == 1330 && lane < 2) {  // odd tail: floats 1328, 1329
     int el = 1328 + lane, ch = el / 35, yx = el - 35 * ch;
-    out[el] = ((smask[w][ch] >> yx) & 1) ? sval[w][ch] : 0.f;
+    out[el] = ((smask[ch] >> yx) & 1) ? sval[ch] : 0.f;
   }
   if constexpr (Glob) {
 #pragma unroll
@@ -182,6 +184,19 @@ __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict
       if (i < 84 && j < m) glob[j * 42 + i - 42 * (i >= 42 ? 1 : 0)] = glob_value(st, word_stride, item_stride, idx, j, i % 42);
     }
   }
+}
+
+template <bool Glob>
+__global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
+                                                      long item_stride, const int32_t *__restrict__ idx, int m,
+                                                      const int32_t *__restrict__ mcount, float *__restrict__ board,
+                                                      float *__restrict__ glob) {
+  __shared__ uint64_t smask[kEncWaves][76];
+  __shared__ float sval[kEncWaves][76];
+  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (mcount) m = *mcount < m ? *mcount : m;  // device-side item count (compacted leaf batches)
+  encode_pair<Glob>(st, word_stride, item_stride, idx, m, board, glob, lane,
+                    2 * ((long)blockIdx.x * kEncWaves + w), smask[w], sval[w]);
 }
 
 __global__ void __launch_bounds__(256) k_encode_glob(const uint64_t *__restrict__ st, long word_stride,

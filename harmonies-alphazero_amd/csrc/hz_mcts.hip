@@ -122,9 +122,8 @@ __global__ void __launch_bounds__(kWave) k_begin(hz_mcts m, const uint64_t *__re
 // with NumPy promotion: cpuct*P in float32, the rest float64; Q = W/N
 // (0 while N == 0); the first edge (insertion = ascending action order)
 // with the largest Q+U by strict '>' wins.
-__global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__restrict__ active, float cpuct) {
-  int b = blockIdx.x;
-  int lane = threadIdx.x;
+__device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
+                                             float cpuct) {
   int32_t *cnt = m.counts + (size_t)b * 4;
   if ((active && !active[b]) || cnt[0] == 0) {
     if (lane == 0) {
@@ -198,6 +197,10 @@ __global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__re
   }
 }
 
+__global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__restrict__ active, float cpuct) {
+  select_board(m, blockIdx.x, threadIdx.x, active, cpuct);
+}
+
 // ------------------------------------------------------------ gather leaves
 // The boards whose selected leaf needs the network (active, not terminal:
 // MCTS.py:297-341 never calls predict on a terminal leaf), in board order:
@@ -237,6 +240,51 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
     count[0] = part[t];
     if (m.eval_ctr) m.eval_ctr[0] += part[t];  // one workgroup, stream-ordered: no atomic needed
   }
+}
+
+// --------------------------------- select + gather + encode for small batches
+// At most kFusedMax boards (config 1's one-board searches, the arena's few
+// dozen games): one workgroup runs move_to_leaf for every board (wave per
+// board), gathers the leaves that need the network (one wave's ballot
+// prefix: board order kept) and encodes them (wave per pair of rows), so a
+// simulation's tree side before the network is one launch instead of three
+// (each a few us of launch latency at this size).  Same results as
+// k_select + k_gather + the encoder.
+constexpr int kFusedMax = 32;
+constexpr int kFusedWaves = 16;
+static_assert(kFusedMax <= 2 * kFusedWaves && kFusedMax <= kWave, "one pair per wave, one gather wave");
+__global__ void __launch_bounds__(kFusedWaves * kWave) k_select_gather_encode(hz_mcts m,
+                                                                           const uint8_t *__restrict__ active,
+                                                                           float cpuct, int32_t *__restrict__ rows,
+                                                                           int32_t *__restrict__ count,
+                                                                           float *__restrict__ board,
+                                                                           float *__restrict__ glob) {
+  __shared__ uint64_t smask[kFusedWaves][76];
+  __shared__ float sval[kFusedWaves][76];
+  __shared__ int32_t s_count;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b = w; b < m.n; b += kFusedWaves) select_board(m, b, lane, active, cpuct);
+  __syncthreads();  // every board's leaf_gidx (written by its wave) is visible to the workgroup
+  if (w == 0) {
+    const int g = lane < m.n ? m.leaf_gidx[lane] : -1;
+    const uint64_t need = __ballot(g >= 0);
+    const int j = __popcll(need & ((1ull << lane) - 1));
+    if (lane < m.n) {
+      m.slot[lane] = g >= 0 ? j : -1;
+      if (g >= 0) {
+        m.gidx_c[j] = g;
+        if (rows) rows[j] = lane;
+      }
+    }
+    if (lane == 0) {
+      const int c = __popcll(need);
+      count[0] = c;
+      s_count = c;
+      if (m.eval_ctr) m.eval_ctr[0] += c;
+    }
+  }
+  __syncthreads();
+  encode_pair<true>(m.node_state, 1, 6, m.gidx_c, s_count, board, glob, lane, 2 * w, smask[w], sval[w]);
 }
 
 // ------------------------------------------------ turn-end chance, in parallel
@@ -820,6 +868,18 @@ int hz_mcts_select(hz_mcts *m, const uint8_t *active, float cpuct) {
 int hz_mcts_encode_leaves(hz_mcts *m, float *board, float *glob) {
   if (!m || (!board && !glob)) return -1;
   launch_encode(m->node_state, 1, 6, m->leaf_gidx, m->n, board, glob, m->stream);
+  return launch_err();
+}
+
+int hz_mcts_select_gather(hz_mcts *m, const uint8_t *active, float cpuct, float *board, float *glob, int32_t *rows,
+                          int32_t *count) {
+  if (!m || !count || !board || !glob) return -1;
+  if (m->n > kFusedMax) {
+    const int rc = hz_mcts_select(m, active, cpuct);
+    return rc ? rc : hz_mcts_gather_leaves(m, board, glob, rows, count);
+  }
+  hipLaunchKernelGGL(k_select_gather_encode, dim3(1), dim3(kFusedWaves * kWave), 0, m->stream, *m, active, cpuct,
+                     rows, count, board, glob);
   return launch_err();
 }
 

@@ -82,6 +82,14 @@ class BatchedMCTS:
                   "hz_mcts_encode_leaves")
         return self.board, self.glob
 
+    def select_gather(self, cpuct, active=None):
+        """select then gather_leaves; one launch when the handle has at most
+        32 boards (hz_mcts_select_gather)."""
+        nat.check(nat.lib().hz_mcts_select_gather(self._h, nat.ptr(active), float(cpuct), nat.ptr(self.board),
+                                                  nat.ptr(self.glob), nat.ptr(self.rows), nat.ptr(self.count)),
+                  "hz_mcts_select_gather")
+        return self.board, self.glob, self.rows, self.count
+
     def gather_leaves(self):
         """The leaves that need the network, in board order: (board, glob,
         rows, count) with rows [0, count[0]) live (hz_mcts_gather_leaves)."""
@@ -112,8 +120,7 @@ class BatchedMCTS:
     # -- one full search per board -------------------------------------------
     def _device_step(self, evaluator, cpuct, active, noise, eps, testing, max_rows=None):
         """One simulation with a device-row evaluator: no host round trip."""
-        self.select(cpuct, active)
-        board, glob, rows, count = self.gather_leaves()  # (adds count to eval_rows)
+        board, glob, rows, count = self.select_gather(cpuct, active)  # (adds count to eval_rows)
         if max_rows is not None:  # the live rows are a prefix of at most max_rows
             board, glob = board[:max_rows], glob[:max_rows]
         policy, value = evaluator(board, glob, rows, count)
@@ -181,14 +188,14 @@ class BatchedMCTS:
                 g.replay()
             return self._finish()
         for _ in range(total):
-            self.select(cpuct, active)
             if not gather:
+                self.select(cpuct, active)
                 board, glob = self.encode_leaves()
                 policy, value = evaluator(board, glob)
                 self.eval_rows += self.n
                 self.expand_backup(policy, value, noise, eps, testing)
                 continue
-            board, glob, rows, count = self.gather_leaves()  # (adds count to eval_rows)
+            board, glob, rows, count = self.select_gather(cpuct, active)  # (adds count to eval_rows)
             if device_rows:
                 if max_rows is not None:
                     board, glob = board[:max_rows], glob[:max_rows]

@@ -176,6 +176,12 @@ int hz_mcts_encode_leaves(hz_mcts *mcts, float *board, float *glob);
  * leaf-eval kernels below take `count` as their live-row bound.  Pair with
  * hz_mcts_expand_backup_gathered. */
 int hz_mcts_gather_leaves(hz_mcts *mcts, float *board, float *glob, int32_t *rows, int32_t *count);
+/* hz_mcts_select followed by hz_mcts_gather_leaves (board and glob both
+ * required), as one launch when the handle has at most 32 boards (config 1's
+ * one-board searches, the arena): same results, two launch latencies less
+ * per simulation. */
+int hz_mcts_select_gather(hz_mcts *mcts, const uint8_t *active, float cpuct, float *board, float *glob,
+                          int32_t *rows, int32_t *count);
 /* counter (device int64, may be NULL to detach): every later
  * hz_mcts_gather_leaves adds its row count k to counter[0] on the device
  * (the number of leaf evaluations of a search without a separate kernel). */

@@ -248,3 +248,30 @@ def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
     assert k > 3000
     mcts.close()
     env.close()
+
+
+@pytest.mark.parametrize("n", [1, 7, 32, 33])
+def test_fused_select_gather_matches_separate_launches(n):
+    """hz_mcts_select_gather (one launch of select + gather + encode up to 32
+    boards) leaves the same leaves, gathered rows, slots, count and encoded
+    tensors as hz_mcts_select + hz_mcts_gather_leaves, after a few
+    simulations of tree growth with some boards inactive and some terminal."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    env = BatchedEnv(n, seed_base=600, device=DEV)
+    env.reset()
+    mcts = BatchedMCTS(env, 16)
+    active = torch.ones(n, dtype=torch.uint8, device=DEV)
+    active[::5] = 0 if n > 1 else 1
+    mcts.search(stub_evaluator, 2.0, active=active, sims=6)   # grow the trees (eager, host-row evaluator)
+    b1, g1, r1, c1 = (t.clone() for t in mcts.select_gather(2.0, active))
+    mcts.board.zero_()
+    mcts.glob.zero_()
+    mcts.select(2.0, active)
+    b2, g2, r2, c2 = mcts.gather_leaves()
+    k = int(c1.item())
+    assert int(c2.item()) == k and k > 0
+    assert torch.equal(r1[:k], r2[:k])
+    assert torch.equal(b1[:k], b2[:k]) and torch.equal(g1[:k], g2[:k])
+    mcts.close()
+    env.close()
