@@ -31,6 +31,7 @@ struct hz_env;  // defined in hz_env.hip; accessed through the ABI getters
 struct hz_mcts {
   int32_t n, max_nodes, max_edges, hcap, max_depth;
   int32_t exact_keys;
+  int32_t dedup_walk;    // hz_mcts_set_dedup_walk (tests): every sibling dedup takes the serial walk
   hipStream_t stream;
   uint64_t *node_state;  // [n][max_nodes][6]
   uint64_t *node_hash;   // [n][max_nodes]
@@ -59,6 +60,7 @@ constexpr int kWave = 64;
 constexpr int kMaxChildren = 69;  // measured max legal moves
 constexpr int kChildSlots = 128;  // two per lane (loop bound: lanes c and c + 64)
 constexpr int kChildLds = 72;     // LDS rows per child array: every access has c < nl <= kMaxChildren
+constexpr int kDedupSlots = 128;  // sibling-dedup table (load factor <= 69/128)
 
 inline int launch_err() {
   hipError_t e = hipGetLastError();
@@ -417,7 +419,7 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XFLAG(k, v)
 #endif
 static_assert(kChildLds >= kMaxChildren, "child arrays hold every legal move");
-// 9.8 KB (was 12.3 KB, 19.5 KB before that).  The turn-end stream copy and
+// 11.3 KB with the 1.5 KB dedup table (was 12.3 KB, 19.5 KB before that).  The turn-end stream copy and
 // the children's states share their bytes (the stream is written back before
 // the first child state is stored).  The children's keys stay in LDS:
 // rebuilding a key from the child's state at each hash match instead (most
@@ -433,6 +435,9 @@ struct ExpandLds {
   uint64_t hash[kChildLds];
   int32_t child[kChildLds];
   int32_t flag[kChildLds];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
+  // sibling dedup: open-addressing table hash tag -> lowest new child index
+  uint64_t dtag[kDedupSlots];
+  int32_t didx[kDedupSlots];
 };
 static_assert(sizeof(uint64_t) * kChildLds * 6 >= sizeof(uint32_t) * kMT, "the states cover the stream copy");
 
@@ -515,10 +520,18 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
         __syncthreads();  // the stream copy is read before the children's states overwrite it
       }
       HZ_XSTAMP(2)
+      // the board's counters and the children's priors are loaded here, their
+      // latency hidden under the children's rule work (the counters are
+      // written by this wave alone, at the end)
+      const int gen = cnt[2], base_n = cnt[0], base_e = cnt[1];
+      float prior[2] = {0.f, 0.f};
       // children: lane handles child c = lane and lane + 64
-      for (int c = lane; c < kChildSlots; c += kWave) {
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const int c = lane + r * kWave;
         if (c < nl) {
           int a = kth_action(mk, c);
+          prior[r] = policy[row * kActions + a];
           State ch = ls;
           ScriptDraw sd{turn_end ? L.script[c] : ~0ull};
           step_state(ch, a, sd);
@@ -534,12 +547,15 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           L.flag[c] = 0;
         }
       }
+      for (int s = lane; s < kDedupSlots; s += kWave) {  // empty dedup table (tag 0: no hash has it, see below)
+        L.dtag[s] = 0;
+        L.didx[s] = INT32_MAX;
+      }
       __syncthreads();
       HZ_XSTAMP(3)
       // transpositions (MCTS.py:177-204): a child whose key is already in the
       // tree reuses that node (flag 1), or is skipped if it is the leaf itself
       // (flag 2) ...
-      int gen = cnt[2];
       uint64_t *ht = m.ht + (size_t)b * m.hcap;
       uint64_t hmask = (uint64_t)(m.hcap - 1);
       for (int c = lane; c < kChildSlots; c += kWave) {
@@ -574,18 +590,60 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
       __syncthreads();
       HZ_XSTAMP(4)
       // ... and among the remaining children the first of equal keys creates
-      // the node, later siblings reuse it (flag 3: child[c] = that sibling).
-      // Wave-uniform walk over the new children c2 in ascending order: c2's
-      // hash is broadcast from its lane's register (readlane), every lane
-      // compares it with its own children's; keys are compared only on equal
-      // hashes.  The first match is the target (a target is never itself a
-      // duplicate: it has no earlier equal sibling).
+      // the node, later siblings reuse it (flag 3: child[c] = that sibling;
+      // a target is never itself a duplicate: it has no earlier equal sibling).
+      // Every new child enters its hash tag (hash | 1, so 0 marks an empty
+      // slot) into an LDS open-addressing table whose slot keeps the lowest
+      // child index of that tag (atomicMin).  Equal keys have equal hashes,
+      // so when the slot's lowest index f < c holds c's key, f is the first
+      // of c's equal siblings.  When f's key differs (a 64-bit hash collision
+      // or two hashes differing in bit 0 only) the lane is unresolved and the
+      // serial walk below decides it; it runs only if some lane needs it.
+      // (The walk alone cost up to ~30k cycles at 60+ children, profiles/r02.)
       {
         const int c0 = lane, c1 = lane + kWave;
         const bool new0 = c0 < nl && L.flag[c0] == 0, new1 = c1 < nl && L.flag[c1] == 0;
         const uint64_t h0 = new0 ? L.hash[c0] : 0, h1 = new1 ? L.hash[c1] : 0;
-        const uint64_t cand[2] = {__ballot(new0), __ballot(new1)};
+        auto enter = [&](uint64_t h, int c) {
+          const unsigned long long tag = h | 1ull;
+          for (int s = (int)(h >> 32) & (kDedupSlots - 1);; s = (s + 1) & (kDedupSlots - 1)) {
+            const unsigned long long prev = atomicCAS((unsigned long long *)&L.dtag[s], 0ull, tag);
+            if (prev == 0ull || prev == tag) {
+              atomicMin(&L.didx[s], c);
+              return s;
+            }
+          }
+        };
+        const int s0 = new0 ? enter(h0, c0) : 0;
+        const int s1 = new1 ? enter(h1, c1) : 0;
+        __syncthreads();
+        auto same_key = [&](int f, int c) {
+          bool eq = L.hash[f] == L.hash[c];
+#pragma unroll
+          for (int w = 0; w < 8; w++) eq = eq && L.key[f][w] == L.key[c][w];
+          return eq;
+        };
         int dup0 = -1, dup1 = -1;
+        bool open0 = false, open1 = false;  // unresolved lanes
+        if (new0) {
+          const int f = L.didx[s0];
+          if (f < c0) {
+            if (same_key(f, c0) && !m.dedup_walk) dup0 = f;
+            else open0 = true;
+          }
+        }
+        if (new1) {
+          const int f = L.didx[s1];
+          if (f < c1) {
+            if (same_key(f, c1) && !m.dedup_walk) dup1 = f;
+            else open1 = true;
+          }
+        }
+        // the serial walk for unresolved lanes: over the new children c2 in
+        // ascending order, c2's hash broadcast from its lane (readlane); the
+        // first c2 < c of equal key is the target
+        const bool any_open = __ballot(open0 || open1) != 0ull;
+        const uint64_t cand[2] = {any_open ? __ballot(new0) : 0ull, any_open ? __ballot(new1) : 0ull};
 #pragma unroll
         for (int r = 0; r < 2; r++) {
           uint64_t rest = cand[r];
@@ -597,18 +655,8 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
             const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)hv, src);
             const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(hv >> 32), src);
             const uint64_t hc2 = (uint64_t)hi << 32 | lo;
-            if (new0 && dup0 < 0 && c2 < c0 && h0 == hc2) {
-              bool eq = true;
-#pragma unroll
-              for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c0][w];
-              if (eq) dup0 = c2;
-            }
-            if (new1 && dup1 < 0 && c2 < c1 && h1 == hc2) {
-              bool eq = true;
-#pragma unroll
-              for (int w = 0; w < 8; w++) eq = eq && L.key[c2][w] == L.key[c1][w];
-              if (eq) dup1 = c2;
-            }
+            if (open0 && dup0 < 0 && c2 < c0 && h0 == hc2 && same_key(c2, c0)) dup0 = c2;
+            if (open1 && dup1 < 0 && c2 < c1 && h1 == hc2 && same_key(c2, c1)) dup1 = c2;
           }
         }
         __syncthreads();  // every lane has read the flags before any is rewritten
@@ -623,7 +671,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
       }
       __syncthreads();
       // new nodes get consecutive ids in child order; edges keep child order
-      int base_n = cnt[0], base_e = cnt[1];
       int n_new = 0, n_edges = 0;
       for (int r = 0; r < 2; r++) {
         int c = lane + r * kWave;
@@ -641,7 +688,9 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
       if (base_n + n_new > m.max_nodes || base_e + n_edges > m.max_edges) {
         if (lane == 0) cnt[3] = 1;  // capacity exhausted: leave the leaf unexpanded
       } else {
-        for (int c = lane; c < kChildSlots; c += kWave) {
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          const int c = lane + r * kWave;
           if (c >= nl) continue;
           int f = L.flag[c] & 15;
           int node_id = f == 3 ? L.child[L.child[c]] : L.child[c];
@@ -662,7 +711,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           }
           if (f != 2) {
             int a = kth_action(mk, c);
-            float p = policy[row * kActions + a];
+            float p = prior[r];
             if (noisy) p = __double2float_rn(__dadd_rn((double)__fmul_rn(one_minus_eps, p),
                                                        __dmul_rn(eps, noise[(size_t)b * kMaxChildren + c])));
             int e = base_e + (L.flag[c] >> 4);
@@ -843,6 +892,12 @@ void hz_mcts_destroy(hz_mcts *m) {
 int hz_mcts_set_eval_counter(hz_mcts *m, int64_t *counter) {
   if (!m) return -1;
   m->eval_ctr = counter;
+  return 0;
+}
+
+int hz_mcts_set_dedup_walk(hz_mcts *m, int32_t on) {
+  if (!m) return -1;
+  m->dedup_walk = on ? 1 : 0;
   return 0;
 }
 

@@ -34,6 +34,7 @@ class BatchedMCTS:
         self.device = env.device
         self.num_simulations = int(num_simulations)
         self._graph_cache = None  # (key, captured simulation, network) kept by search(graph=True)
+        self._capture_stream = None  # this handle's graph-capture stream (own split-tower counter block)
         self.max_nodes = int(max_nodes or 1 + MAX_CHILDREN * self.num_simulations)
         L = nat.lib()
         self._h = L.hz_mcts_create(self.n, self.max_nodes, int(max_depth), int(bool(exact_keys)),
@@ -133,8 +134,15 @@ class BatchedMCTS:
         only when it expands the root, which the first (eager) simulation does
         (hz_mcts.hip k_expand_backup: noisy = leaf == 0 && !testing && noise)."""
         g = torch.cuda.CUDAGraph()
+        if self._capture_stream is None:
+            self._capture_stream = torch.cuda.Stream(self.device)
+        # the split tower's counter block for this stream, zeroed now: created
+        # inside the capture, its zero-fill would be a graph node replayed
+        # with every simulation (hzamd.infer._split_sync)
+        from .infer import _split_sync
+        _split_sync(self.device, self._capture_stream)
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, stream=self._capture_stream):
                 self._sync()  # the handles launch on the capture stream
                 self._device_step(evaluator, cpuct, active, None, eps, testing, max_rows)
         finally:

@@ -186,6 +186,11 @@ int hz_mcts_select_gather(hz_mcts *mcts, const uint8_t *active, float cpuct, flo
  * hz_mcts_gather_leaves adds its row count k to counter[0] on the device
  * (the number of leaf evaluations of a search without a separate kernel). */
 int hz_mcts_set_eval_counter(hz_mcts *mcts, int64_t *counter);
+/* Test switch (no reference counterpart): on != 0 makes every expansion's
+ * sibling dedup take its serial walk instead of the LDS hash table (the path
+ * the table leaves to the walk only on a hash collision), so tests can check
+ * both give the same trees.  Off by default. */
+int hz_mcts_set_dedup_walk(hz_mcts *mcts, int32_t on);
 /* expand_leaf (MCTS.py:151-218) with policy[n][143] (probabilities, as
  * ModelManager.predict returns them, model.py:81-110), root Dirichlet mix
  * (MCTS.py:308-327) when !testing using noise[n][69] (i-th legal move), then

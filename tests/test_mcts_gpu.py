@@ -103,6 +103,44 @@ def test_mcts_4096_boards_vs_oracle():
         assert oracle.mt_next32(m2) == oracle.mt_next32(m), b
 
 
+def test_sibling_dedup_table_matches_serial_walk():
+    """k_expand_backup's sibling dedup: the LDS hash table (default) and the
+    serial walk it falls back to on a hash collision (forced on every
+    expansion by hz_mcts_set_dedup_walk) give the same trees, and both the
+    oracle's, on 1024 boards spread over the game (sibling duplicates: two
+    equal tiles in hand placed on the same hex)."""
+    import hzamd._native as nat
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, sims, cpuct = 1024, 24, 2.0
+    env = BatchedEnv(n, seed_base=900, device=DEV)
+    env.reset()
+    plies = torch.arange(n, device=DEV) % 53
+    for p in range(53):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+    st0, mt0, idx0 = env.export_state(with_mt=True)
+    active = torch.from_numpy(np.array([not oracle.is_game_over(unpack_ref(st0[:, b].cpu().numpy()))
+                                        for b in range(n)]))
+    runs = []
+    for walk in (0, 1):
+        env.import_state(st0, mt0, idx0)
+        mcts = BatchedMCTS(env, sims)
+        assert nat.lib().hz_mcts_set_dedup_walk(mcts._h, walk) == 0
+        v = mcts.search(stub_evaluator, cpuct, active=active).cpu().numpy()
+        runs.append((v, mcts.stats().cpu().numpy()))
+        mcts.close()
+    assert (runs[0][0] == runs[1][0]).all() and (runs[0][1] == runs[1][1]).all()
+    st0, mt0, idx0 = st0.cpu().numpy(), mt0.cpu().numpy().view(np.uint32), idx0.cpu().numpy()
+    for b in range(0, n, 8):
+        if not active[b]:
+            continue
+        m = oracle.mt_from_words(mt0[b], idx0[b])
+        _, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, cpuct, testing=True)
+        assert (runs[0][0][b] == ov).all() and (runs[0][1][b, 0], runs[0][1][b, 1]) == (nn, ne), b
+
+
 def test_mcts_exact_keys_mode():
     """exact_keys=1 keys transpositions by the true canonical tuple."""
     from hzamd.env import BatchedEnv
