@@ -298,13 +298,25 @@ __global__ void __launch_bounds__(kFusedWaves * kWave) k_select_gather_encode(hz
 // _randbelow(n), a repeat of the child's own earlier pick is drawn again),
 // the wave produces 64 tempered words at a time (twisting the generation in
 // place 64 words at a time: a block's sources are either old words beyond
-// it or new words before it), each lane tests its word against n, and one
-// wave-uniform scalar walk over the accepted words (readlane) groups them
-// into the children's three picks.  Returns the stream cursor (pos | tw <<
-// 16, as MTS) after the last child's third pick; script[c] = the pile the
-// c-th child draws, as replenish() records it.
+// it or new words before it), each lane tests its word against n and the
+// accepted values are appended, in stream order, to an LDS list.  The list
+// is then cut into the children's picks speculatively: lane k takes child
+// c + k's three picks as list entries s + 3k .. s + 3k + 2, which is right
+// for every child before the first whose triple holds a repeat (or runs past
+// the list); that child is resolved serially (skipping its repeats), and the
+// cut resumes after it.  A window therefore costs one parallel step per
+// repeat (~5 % of triples) instead of a serial step per pick.  Returns the
+// stream cursor (pos | tw << 16, as MTS) after the last child's third pick;
+// script[c] = the pile the c-th child draws, as replenish() records it.
+constexpr int kAccRing = 512;  // accepted-value ring (entries in flight: < 64 + 3)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, uint64_t misc, int nl, int lane,
-                                       uint64_t *script) {
+                                                       uint64_t *script, uint32_t *acc) {
   int cnt[6];
   uint32_t n = 0;
 #pragma unroll
@@ -312,12 +324,24 @@ __device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, 
     cnt[t] = bag_n(misc, t);
     n += (uint32_t)cnt[t];
   }
+  // flat bag index -> tile (insertion order water, plant, wood, stone,
+  // field, building: constants.py:41); three picks -> the pile's script
+  constexpr uint32_t kOrder = WATER | (PLANT << 3) | (WOOD << 6) | (STONE << 9) | (FIELD << 12) | (BUILDING << 15);
+  const uint32_t e0 = (uint32_t)cnt[WATER], e1 = e0 + (uint32_t)cnt[PLANT], e2 = e1 + (uint32_t)cnt[WOOD];
+  const uint32_t e3 = e2 + (uint32_t)cnt[STONE], e4 = e3 + (uint32_t)cnt[FIELD];
+  auto tile = [&](uint32_t x) {
+    const uint32_t o = (uint32_t)(x >= e0) + (uint32_t)(x >= e1) + (uint32_t)(x >= e2) + (uint32_t)(x >= e3) +
+                       (uint32_t)(x >= e4);
+    return (uint64_t)__builtin_amdgcn_ubfe(kOrder, 3 * o, 3);
+  };
+  auto pile = [&](uint32_t a, uint32_t b, uint32_t c) {
+    return (((1ull << 45) - 1) & ~0x1FFull) | tile(a) | tile(b) << 3 | tile(c) << 6;
+  };
   const int kb = 32 - __clz(n);
   int pos = cursor & 0xFFFF, tw = cursor >> 16;
-  int c = 0, got = 0;
-  uint32_t j0 = 0, j1 = 0;
-  // child c's picks, kept by lane c & 63 (children >= 64 in the second set)
-  uint32_t p0 = 0, p1 = 0, p2 = 0, q0 = 0, q1 = 0, q2 = 0;
+  int c = 0;      // next child to resolve (wave-uniform)
+  int s = 0;      // its first list entry
+  int k_end = 0;  // list length
   for (;;) {
     if (pos >= kMT) {  // next generation
       pos = 0;
@@ -337,38 +361,55 @@ __device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, 
       __builtin_amdgcn_wave_barrier();
       tw = tw + kWave < kMT ? tw + kWave : kMT;
     }
-    const int i = pos + lane;
-    const uint32_t r = i < kMT ? temper(w[i]) >> (32 - kb) : n;
-    uint64_t acc = __ballot(r < n);
+    {  // append this window's accepted values (value | window offset << 16)
+      const int i = pos + lane;
+      const uint32_t r = i < kMT ? temper(w[i]) >> (32 - kb) : n;
+      const uint64_t ok = __ballot(r < n);
+      if (r < n) acc[(k_end + __popcll(ok & ((1ull << lane) - 1))) & (kAccRing - 1)] = r | (uint32_t)lane << 16;
+      k_end += __popcll(ok);
+      wave_lds_sync();
+    }
     int last = -1;  // window offset of the word that completed the last child
-    while (acc) {
-      const int src = __builtin_ctzll(acc);  // wave-uniform
-      acc &= acc - 1;
-      const uint32_t v = __builtin_amdgcn_readlane(r, src);
-      if ((got >= 1 && v == j0) || (got >= 2 && v == j1)) continue;  // repeat: drawn again
-      if (got == 0) {
-        j0 = v;
-        got = 1;
-      } else if (got == 1) {
-        j1 = v;
-        got = 2;
-      } else {
-        if (lane == (c & 63)) {
-          if (c < kWave) {
-            p0 = j0;
-            p1 = j1;
-            p2 = v;
-          } else {
-            q0 = j0;
-            q1 = j1;
-            q2 = v;
-          }
-        }
-        got = 0;
-        if (++c == nl) {
-          last = src;
-          break;
-        }
+    for (;;) {
+      // speculative cut: lane k -> child c + k, entries s + 3k .. s + 3k + 2
+      const int ck = c + lane, sk = s + 3 * lane;
+      bool good = false;
+      uint32_t a0 = 0, a1 = 0, a2 = 0;
+      if (ck < nl && sk + 2 < k_end) {
+        a0 = acc[sk & (kAccRing - 1)] & 0xFFFFu;
+        a1 = acc[(sk + 1) & (kAccRing - 1)] & 0xFFFFu;
+        a2 = acc[(sk + 2) & (kAccRing - 1)] & 0xFFFFu;
+        good = a1 != a0 && a2 != a0 && a2 != a1;
+      }
+      const uint64_t bad = ~__ballot(good);
+      const int f = bad ? __builtin_ctzll(bad) : kWave;  // children c .. c + f - 1 are cut right
+      if (lane < f) script[ck] = pile(a0, a1, a2);
+      c += f;
+      s += 3 * f;
+      if (f > 0 && c >= nl) {
+        last = (int)(acc[(s - 1) & (kAccRing - 1)] >> 16);
+        break;
+      }
+      if (f == kWave) continue;
+      // child c: a repeat among its first three entries, or the list ends:
+      // serially, as random.sample draws (wave-uniform values)
+      uint32_t j0 = 0, j1 = 0, v = 0;
+      int got = 0, e = s;
+      while (got < 3 && e < k_end) {
+        v = __builtin_amdgcn_readfirstlane(acc[e & (kAccRing - 1)]) & 0xFFFFu;
+        e++;
+        if ((got >= 1 && v == j0) || (got >= 2 && v == j1)) continue;  // repeat: drawn again
+        if (got == 0) j0 = v;
+        else if (got == 1) j1 = v;
+        got++;
+      }
+      if (got < 3) break;  // the list ends inside child c: next window
+      if (lane == 0) script[c] = pile(j0, j1, v);
+      c++;
+      s = e;
+      if (c >= nl) {
+        last = (int)(acc[(s - 1) & (kAccRing - 1)] >> 16);
+        break;
       }
     }
     if (last >= 0) {
@@ -377,19 +418,7 @@ __device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, 
     }
     pos = need;
   }
-  // lane c: the tiles at flat indices p0, p1, p2 (insertion order water, plant,
-  // wood, stone, field, building: constants.py:41) -> the pile, the script
-  constexpr uint32_t kOrder = WATER | (PLANT << 3) | (WOOD << 6) | (STONE << 9) | (FIELD << 12) | (BUILDING << 15);
-  const uint32_t e0 = (uint32_t)cnt[WATER], e1 = e0 + (uint32_t)cnt[PLANT], e2 = e1 + (uint32_t)cnt[WOOD];
-  const uint32_t e3 = e2 + (uint32_t)cnt[STONE], e4 = e3 + (uint32_t)cnt[FIELD];
-  auto tile = [&](uint32_t x) {
-    const uint32_t o = (uint32_t)(x >= e0) + (uint32_t)(x >= e1) + (uint32_t)(x >= e2) + (uint32_t)(x >= e3) +
-                       (uint32_t)(x >= e4);
-    return __builtin_amdgcn_ubfe(kOrder, 3 * o, 3);
-  };
-  if (lane < nl) script[lane] = (((1ull << 45) - 1) & ~0x1FFull) | tile(p0) | tile(p1) << 3 | tile(p2) << 6;
-  if (lane + kWave < nl)
-    script[lane + kWave] = (((1ull << 45) - 1) & ~0x1FFull) | tile(q0) | tile(q1) << 3 | tile(q2) << 6;
+  wave_lds_sync();  // lane 0's script entries before the children read them
   return pos | (tw << 16);
 }
 
@@ -419,9 +448,10 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XFLAG(k, v)
 #endif
 static_assert(kChildLds >= kMaxChildren, "child arrays hold every legal move");
-// 11.3 KB with the 1.5 KB dedup table (was 12.3 KB, 19.5 KB before that).  The turn-end stream copy and
-// the children's states share their bytes (the stream is written back before
-// the first child state is stored).  The children's keys stay in LDS:
+// 9.8 KB (was 12.3 KB, 19.5 KB before that): 16 waves fit a CU.  The turn-end
+// stream copy and the children's states share their bytes (the stream is
+// written back before the first child state is stored); the sibling-dedup
+// table shares the chance scripts' (read by the children only).  The children's keys stay in LDS:
 // rebuilding a key from the child's state at each hash match instead (most
 // children of a placement meet an existing node: tile orders transpose)
 // made the kernel 3x slower (209 vs 64 us per sim step, profiles/r03).
@@ -430,15 +460,21 @@ struct ExpandLds {
     uint32_t mt[kMT];
     uint64_t state[kChildLds][6];
   };
-  uint64_t script[kChildLds];
-  uint64_t key[kChildLds][8];
+  union {
+    uint64_t script[kChildLds];
+    // sibling dedup: open addressing, slot word = (hash tag << 8) | lowest child index
+    uint32_t dslot[kDedupSlots];
+  };
+  union {
+    uint64_t key[kChildLds][8];
+    uint32_t acc[kAccRing];  // turn-end draws' accepted values (before any key is built)
+  };
   uint64_t hash[kChildLds];
   int32_t child[kChildLds];
   int32_t flag[kChildLds];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
-  // sibling dedup: open-addressing table hash tag -> lowest new child index
-  uint64_t dtag[kDedupSlots];
-  int32_t didx[kDedupSlots];
 };
+static_assert(kDedupSlots * sizeof(uint32_t) <= kChildLds * sizeof(uint64_t), "the dedup table fits the scripts");
+static_assert(kDedupSlots > kMaxChildren && kChildLds <= 256, "a free slot for every child, 8-bit child index");
 static_assert(sizeof(uint64_t) * kChildLds * 6 >= sizeof(uint32_t) * kMT, "the states cover the stream copy");
 
 
@@ -500,12 +536,13 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           }
         }
         __syncthreads();
+        HZ_XSTAMP(8)
         int bag = 0;
 #pragma unroll
         for (int t = 0; t < 6; t++) bag += bag_n(ls.misc, t);
         if (npiles_of(ls.piles) == 4 && bag > 21) {
           // one pile per child, random.sample's set method: the wave-parallel form
-          const int cur = turn_end_draws_parallel(L.mt, mtcur[b], ls.misc, nl, lane, L.script);
+          const int cur = turn_end_draws_parallel(L.mt, mtcur[b], ls.misc, nl, lane, L.script, L.acc);
           if (lane == 0) mtcur[b] = cur;
         } else if (lane == 0) {  // fewer piles or the pool method: one lane, serially
           StreamDraw<MT> draw{MT(L.mt, mtcur[b])};
@@ -516,6 +553,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           mtcur[b] = draw.m.cursor();
         }
         __syncthreads();
+        HZ_XSTAMP(9)
         for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];  // stores: no round trip to wait for
         __syncthreads();  // the stream copy is read before the children's states overwrite it
       }
@@ -547,15 +585,12 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           L.flag[c] = 0;
         }
       }
-      for (int s = lane; s < kDedupSlots; s += kWave) {  // empty dedup table (tag 0: no hash has it, see below)
-        L.dtag[s] = 0;
-        L.didx[s] = INT32_MAX;
-      }
       __syncthreads();
       HZ_XSTAMP(3)
       // transpositions (MCTS.py:177-204): a child whose key is already in the
       // tree reuses that node (flag 1), or is skipped if it is the leaf itself
       // (flag 2) ...
+      for (int s = lane; s < kDedupSlots; s += kWave) L.dslot[s] = 0u;  // empty (no entry is 0, see below)
       uint64_t *ht = m.ht + (size_t)b * m.hcap;
       uint64_t hmask = (uint64_t)(m.hcap - 1);
       for (int c = lane; c < kChildSlots; c += kWave) {
@@ -592,12 +627,13 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
       // ... and among the remaining children the first of equal keys creates
       // the node, later siblings reuse it (flag 3: child[c] = that sibling;
       // a target is never itself a duplicate: it has no earlier equal sibling).
-      // Every new child enters its hash tag (hash | 1, so 0 marks an empty
-      // slot) into an LDS open-addressing table whose slot keeps the lowest
-      // child index of that tag (atomicMin).  Equal keys have equal hashes,
-      // so when the slot's lowest index f < c holds c's key, f is the first
-      // of c's equal siblings.  When f's key differs (a 64-bit hash collision
-      // or two hashes differing in bit 0 only) the lane is unresolved and the
+      // Every new child enters its hash into an LDS open-addressing table:
+      // home slot = hash bits 32-38, tag = bits 40-62 with bit 23 set (so no
+      // entry is 0, the empty word); the slot word keeps tag << 8 | the lowest
+      // child index of that tag (atomicMin over words of one tag).  Equal
+      // keys have equal hashes, so when the slot's lowest index f < c holds
+      // c's key, f is the first of c's equal siblings.  When f's key differs
+      // (hashes equal in those 30 bits only) the lane is unresolved and the
       // serial walk below decides it; it runs only if some lane needs it.
       // (The walk alone cost up to ~30k cycles at 60+ children, profiles/r02.)
       {
@@ -605,11 +641,12 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
         const bool new0 = c0 < nl && L.flag[c0] == 0, new1 = c1 < nl && L.flag[c1] == 0;
         const uint64_t h0 = new0 ? L.hash[c0] : 0, h1 = new1 ? L.hash[c1] : 0;
         auto enter = [&](uint64_t h, int c) {
-          const unsigned long long tag = h | 1ull;
+          const uint32_t mine = ((uint32_t)(h >> 40) | 0x800000u) << 8 | (uint32_t)c;
           for (int s = (int)(h >> 32) & (kDedupSlots - 1);; s = (s + 1) & (kDedupSlots - 1)) {
-            const unsigned long long prev = atomicCAS((unsigned long long *)&L.dtag[s], 0ull, tag);
-            if (prev == 0ull || prev == tag) {
-              atomicMin(&L.didx[s], c);
+            const uint32_t prev = atomicCAS(&L.dslot[s], 0u, mine);
+            if (prev == 0u) return s;
+            if ((prev >> 8) == (mine >> 8)) {
+              atomicMin(&L.dslot[s], mine);
               return s;
             }
           }
@@ -626,14 +663,14 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
         int dup0 = -1, dup1 = -1;
         bool open0 = false, open1 = false;  // unresolved lanes
         if (new0) {
-          const int f = L.didx[s0];
+          const int f = (int)(L.dslot[s0] & 0xFFu);
           if (f < c0) {
             if (same_key(f, c0) && !m.dedup_walk) dup0 = f;
             else open0 = true;
           }
         }
         if (new1) {
-          const int f = L.didx[s1];
+          const int f = (int)(L.dslot[s1] & 0xFFu);
           if (f < c1) {
             if (same_key(f, c1) && !m.dedup_walk) dup1 = f;
             else open1 = true;
@@ -739,11 +776,13 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
   // is the leaf's player else -1)
   int d = m.depth[b];
   const int32_t *path = m.path + (size_t)b * m.max_depth;
+  // (the path's edges are distinct: the adds are read-modify-writes done by
+  // the memory side, one round trip less; the f64 add rounds as __dadd_rn)
   for (int i = lane; i < d; i += kWave) {
-    int e = path[i];
-    double dir = m.edge_player[eb + e] == leaf_player ? 1.0 : -1.0;
-    m.edge_n[eb + e] += 1;
-    m.edge_w[eb + e] = __dadd_rn(m.edge_w[eb + e], v * dir);
+    const size_t e = eb + path[i];
+    double dir = m.edge_player[e] == leaf_player ? 1.0 : -1.0;
+    atomicAdd(&m.edge_n[e], 1);
+    unsafeAtomicAdd(&m.edge_w[e], v * dir);
   }
 #ifdef HZ_DIAG
   __builtin_amdgcn_s_waitcnt(0);
@@ -949,11 +988,12 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
                          double eps, int32_t testing, const int32_t *slot) {
   if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
   float ome = (float)(1.0 - eps);
-  // HZ_EXPAND_WAVES=4: registers capped for four waves per SIMD (spills a
-  // little); default three (A/B measurements, profiles/r03)
+  // default: registers capped for four waves per SIMD (38 VGPRs spilled;
+  // with the 9.8 KB LDS, 4096 boards fit the chip in one round): 44.7 vs
+  // 47.3 us per sim step for three waves (HZ_EXPAND_WAVES=3), profiles/r03
   static const int waves = [] {
     const char *e = getenv("HZ_EXPAND_WAVES");
-    return e && atoi(e) == 4 ? 4 : 3;
+    return e && atoi(e) == 3 ? 3 : 4;
   }();
   if (waves == 4)
     hipLaunchKernelGGL(k_expand_backup<4>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),

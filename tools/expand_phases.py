@@ -64,7 +64,22 @@ for kind, sel in (("turn_end", expanded & turn_end), ("other_expand", expanded &
         for i, nm in enumerate(names[:-1]):
             d[nm] = summ(s[:, i + 1] - s[:, i])
         d[names[-1]] = summ(s[:, 7] - s[:, 6])
+    if kind == "turn_end":  # inside legal->chance: stream copy-in, draws, write-back
+        d["copy_in"] = summ(s[:, 8] - s[:, 1])
+        d["draws"] = summ(s[:, 9] - s[:, 8])
+        d["write_back"] = summ(s[:, 2] - s[:, 9])
     res["wave_cycles"][kind] = d
+# s_memtime counters are per XCD (not synchronised across them): spans are
+# taken within an XCD (workgroup b runs on XCD b % 8)
+res["span_cycles_per_xcd"] = [int(st[x::8, 7].max() - st[x::8, 0].min()) for x in range(8)]
+q = (0, 0.25, 0.5, 0.75, 0.95, 1)
+live = st[:, 7] >= st[:, 0]
+res["per_xcd"] = []
+for x in range(8):
+    sx = st[x::8][live[x::8]]
+    t0x = sx[:, 0].min()
+    res["per_xcd"].append({"start": [int(np.quantile(sx[:, 0] - t0x, v)) for v in q],
+                           "end": [int(np.quantile(sx[:, 7] - t0x, v)) for v in q]})
 starts = np.sort(st[:, 0] - t0)
 res["start_quantiles"] = [float(np.quantile(starts, q)) for q in (0, 0.25, 0.5, 0.75, 1)]
 print(json.dumps(res, indent=1))
