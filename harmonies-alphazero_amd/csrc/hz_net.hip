@@ -98,7 +98,7 @@ constexpr int kStage8 = (kRows * 8 + 511) / 512;  // float4 per thread per chunk
 #ifdef HZ_NET_DIAG
 // diagnostic build only (tools/conv_phases.py): per-workgroup phase stamps of
 // waves 0 and 4, written to this buffer alone
-__device__ uint64_t g_conv_stamps[1024][2][10];
+__device__ uint64_t g_conv_stamps[1024][2][16];
 #define HZ_STAMP(k)                                                                   \
   if ((t & 255) == 0 && blockIdx.x < 1024) g_conv_stamps[blockIdx.x][t >> 8][k] = __builtin_amdgcn_s_memtime();
 #else
@@ -364,7 +364,7 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
 // kX6ClassRow: the block's rows as state * 35 + cell (-1: padding row, not
 // stored); kX6ClassTaps: each block's taps (bit t = tap t = (dh + 1) * 3 +
 // dw + 1).  Generated by the grouping in DESIGN.md §3 (k_conv3x3_x6 row).
-__constant__ int16_t kX6ClassRow[18][16] = {
+alignas(16) __constant__ int16_t kX6ClassRow[18][16] = {
     {8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 22, 23, 24, 25, 26, 43},  // MM
     {44, 45, 46, 47, 50, 51, 52, 53, 54, 57, 58, 59, 60, 61, 78, 79},  // MM
     {80, 81, 82, 85, 86, 87, 88, 89, 92, 93, 94, 95, 96, 113, 114, 115},  // MM
@@ -799,6 +799,9 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
 //    program order, so one counted wait per tap (vmcnt 12: the next K-step's
 //    B fragments stay in flight) covers this K-step's B fragments and the
 //    staged chunk.
+#ifndef HZ_KO
+#define HZ_KO 0  // knock-out bits of diagnostic builds (tools/Makefile variants): results are wrong
+#endif
 namespace {
 constexpr int kW4Stg = (kRows * 8 + 255) / 256;  // float4 staged per thread per chunk (9)
 
@@ -816,14 +819,37 @@ constexpr int x6_class_blocks(int h, int tap) {
   return k;
 }
 
+// Block = true: the whole residual block (model.py:287-299, BN folded),
+// out = relu(conv2(relu(conv1(x) + b1)) + b2 + x), in one launch.  The chunk
+// loop runs over NG = 8 chunks (conv1's four, then conv2's); at the switch
+// each wave turns its conv1 accumulators into relu(acc + b1) (the values the
+// layered conv1 stores) and conv2's chunks are staged from them exactly as
+// the layered conv2 stages them from HBM (same split, same planes), so the
+// result is bit-identical to the two layered convs.  Wave (rh, chf) holds
+// output channels 64 chf .. +64 of its row half; at the switch
+//  - chunk 0 (chf = 0, column blocks 0-1) goes into buffer 0 (last read in
+//    conv1's chunk 2) as bf16 planes, chunk 2 (chf = 1, blocks 0-1) into
+//    region E as fp32 rows;
+//  - chunks 1 and 3 (blocks 2-3) go to tmp, the group's slice of a global
+//    scratch ([2][288][32] fp32 per group: L2-resident until read);
+// then conv2's chunks 0, 1, 2 stage chunk 1 (tmp), 2 (E) and 3 (tmp) into
+// the other buffer as the HBM staging does.
+// LDS: two chunk buffers + E (280 rows x 32 fp32) = 162,304 B.
+template <bool Block>
 __global__ void __launch_bounds__(256, 1)
     k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                    const float *__restrict__ res, float *__restrict__ out, int32_t batch,
-                   const int32_t *__restrict__ live) {
-  constexpr int NQ = 4, kRBT = 9, NCB = 4;
+                   const int32_t *__restrict__ live, const bf16x8 *__restrict__ wp2,
+                   const float *__restrict__ bias2, float *__restrict__ tmp) {
+  constexpr int NQ = 4, kRBT = 9, NCB = 4, NG = Block ? 8 : 4;
   constexpr int kZero = kCS * 35 * kX6Cell;  // 62,720 B: 256-B aligned
   constexpr int kBufT = kZero + kX6Zero;
+  constexpr int kE = 2 * kBufT;              // Block: region E, fp32 [280][32]
   static_assert(kZero % 256 == 0, "zero region 256-B aligned");
+  // E has a 281st row and a dummy cell after it: the padding rows of the
+  // switch write there (no branch per value)
+  constexpr int kDummyCell = kE + (kRows + 1) * 128;
+  static_assert(kDummyCell + kX6Cell <= 160 * 1024, "buffers, E and the dummy cell fit the LDS");
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 1, chf = w & 1;
@@ -846,11 +872,42 @@ __global__ void __launch_bounds__(256, 1)
     return f < kRows * 8 ? f : kRows * 8 - 1;
   };
   const int last_row = s0 * 35 + ns * 35 - 1;  // rows past the batch reread its last one
-  auto stage_issue = [&](int q) {
+  // Block: the thread index made opaque per chunk, so the staging addresses
+  // of the three sources are recomputed at each use, not kept in registers
+  auto opaque_t = [&]() __attribute__((always_inline)) {
+    int tt = t;
+    if constexpr (Block) asm volatile("" : "+v"(tt));
+    return tt;
+  };
+  auto stage_issue = [&](int q) __attribute__((always_inline)) {
+    const int tt = opaque_t();
 #pragma unroll
     for (int it = 0; it < kW4Stg; it++) {
-      const int f = stage_f(it), sc = s0 * 35 + (f >> 3);
+      int f = it * 256 + tt;
+      f = f < kRows * 8 ? f : kRows * 8 - 1;
+      const int sc = s0 * 35 + (f >> 3);
       stg[it] = *(const f32x4 *)(x + (size_t)(sc < last_row ? sc : last_row) * 128 + 4 * (f & 7) + 32 * q);
+    }
+  };
+  // Block: conv2's chunk 2 from region E, chunks 1 and 3 from tmp (fp32 rows of 32 channels)
+  constexpr int kTmpRows = 288;  // a group's tmp slice: [2][288][32] (row 280: padding rows' writes)
+  float *const tmpg = Block ? tmp + (size_t)blockIdx.x * 2 * kTmpRows * 32 : nullptr;
+  auto stage_issue_e = [&]() __attribute__((always_inline)) {
+    const int tt = opaque_t();
+#pragma unroll
+    for (int it = 0; it < kW4Stg; it++) {
+      int f = it * 256 + tt;
+      f = f < kRows * 8 ? f : kRows * 8 - 1;
+      stg[it] = *(const f32x4 *)(lds + kE + 16 * f);
+    }
+  };
+  auto stage_issue_tmp = [&](int half) __attribute__((always_inline)) {
+    const int tt = opaque_t();
+#pragma unroll
+    for (int it = 0; it < kW4Stg; it++) {
+      int f = it * 256 + tt;
+      f = f < kRows * 8 ? f : kRows * 8 - 1;
+      stg[it] = *(const f32x4 *)(tmpg + half * kTmpRows * 32 + 4 * f);
     }
   };
   auto stage_put = [&](int it, int buf) {
@@ -863,16 +920,23 @@ __global__ void __launch_bounds__(256, 1)
     *(uint2 *)(d + 128) = l;
   };
   // B fragment of K-step L = q * 9 + tap, plane p, column block cb:
-  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units)
+  // wp[(((tap * NQ + q) * 3 + p) * 128 + co0 + 16 cb) * 4 + kg]   (bf16x8 units);
+  // S = the K-step over all NG chunks (Block: conv2's from S = 36, in wp2)
   const int co0 = 64 * chf + (lane & 15);
   const bf16x8 *wl = wp + co0 * 4 + kg;
-  auto bissue = [&](bf16x8(&dst)[3][NCB], int L) {
-    L = L < 9 * NQ ? L : 9 * NQ - 1;
-    const int q2 = L / 9, t2 = L - 9 * q2;
+  const bf16x8 *wl2 = (Block ? wp2 : wp) + co0 * 4 + kg;
+  auto bissue = [&](bf16x8(&dst)[3][NCB], int S) {
+    S = S < 9 * NG ? S : 9 * NG - 1;
+    const bf16x8 *w = wl;
+    if constexpr (Block) {
+      w = S < 9 * NQ ? wl : wl2;
+      S = S < 9 * NQ ? S : S - 9 * NQ;
+    }
+    const int q2 = S / 9, t2 = S - 9 * q2;
 #pragma unroll
     for (int p = 0; p < 3; p++)
 #pragma unroll
-      for (int cb = 0; cb < NCB; cb++) dst[p][cb] = wl[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
+      for (int cb = 0; cb < NCB; cb++) dst[p][cb] = w[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
   };
   // chunk 0's loads and the first K-step's B fragments first: the rest of
   // the setup runs under their latency
@@ -907,7 +971,6 @@ __global__ void __launch_bounds__(256, 1)
   for (int rb = 0; rb < kRBT; rb++)
 #pragma unroll
     for (int cb = 0; cb < NCB; cb++) acc[rb][cb] = (f32x4){};
-
   HZ_STAMP(1)
 #pragma unroll
   for (int it = 0; it < kW4Stg; it++) stage_put(it, 0);
@@ -924,6 +987,56 @@ __global__ void __launch_bounds__(256, 1)
   // region: a whole tap to land in) and the next chunk's staging (issued in
   // tap 0, split and stored in the plane-1 regions of taps 2-7).  Loads are
   // compiler-tracked, so its counted waits follow them.
+  // Block, between the convs: conv1's outputs relu(acc + b1) (as the layered
+  // conv1's epilogue computes them) to where conv2's chunks are staged from
+  // (above); then the accumulators restart for conv2
+  auto switch_convs = [&]() __attribute__((always_inline)) {
+    float b1v[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; cb++) b1v[cb] = bias[64 * chf + 16 * cb + (lane & 15)];
+    uint2 rows[kRBT];  // the lane's 4 rows of each row block, all loads in flight at once
+#pragma unroll
+    for (int rb = 0; rb < kRBT; rb++) rows[rb] = *(const uint2 *)&kX6ClassRow[rh * kRBT + rb][4 * kg];
+    // chf is wave-uniform: one branch; a padding row (-1) writes to the
+    // dummy cell / row 280, so no value takes a branch of its own
+    auto put_all = [&](auto chfc) __attribute__((always_inline)) {
+      constexpr int C = decltype(chfc)::value;
+      static_for<0, kRBT>([&](auto rbc) {
+        constexpr int rb = decltype(rbc)::value;
+        static_for<0, 4>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int r = (int)(int16_t)((j < 2 ? rows[rb].x : rows[rb].y) >> (16 * (j & 1)));
+          const bool pad = r < 0;
+          static_for<0, NCB>([&](auto cbc) {
+            constexpr int cb = decltype(cbc)::value;
+            float v = acc[rb][cb][j] + b1v[cb];
+            v = v > 0.f ? v : 0.f;
+            const int k = 16 * (cb & 1) + (lane & 15);
+            if constexpr (cb >= 2) {
+              tmpg[C * kTmpRows * 32 + (pad ? kRows : r) * 32 + k] = v;
+            } else if constexpr (C == 0) {
+              const uint32_t h = bf16_bits(v);
+              const float r1 = v - bf16_value(h);
+              const uint32_t m = bf16_bits(r1);
+              const uint32_t l = bf16_bits(r1 - bf16_value(m));
+              char *d = lds + (pad ? kDummyCell : r * kX6Cell) + 2 * k;
+              *(unsigned short *)d = (unsigned short)h;
+              *(unsigned short *)(d + 64) = (unsigned short)m;
+              *(unsigned short *)(d + 128) = (unsigned short)l;
+            } else {
+              *(float *)(lds + kE + (pad ? kRows : r) * 128 + 4 * k) = v;
+            }
+          });
+        });
+        static_for<0, NCB>([&](auto cbc) { acc[rb][decltype(cbc)::value] = (f32x4){}; });
+      });
+    };
+    if (chf == 0)
+      put_all(std::integral_constant<int, 0>{});
+    else
+      put_all(std::integral_constant<int, 1>{});
+    __syncthreads();
+  };
   auto classed = [&](auto half) {
     constexpr int H = decltype(half)::value;
     auto aread = [&](bf16x8(&dst)[kRBT], const char *lb, auto tapc, int pa) {
@@ -940,28 +1053,49 @@ __global__ void __launch_bounds__(256, 1)
         }
       });
     };
-    for (int q = 0; q < NQ; q++) {
+    for (int g = 0; g < NG; g++) {
+      const int q = g & (NQ - 1);  // the chunk of the current conv
+      if constexpr (Block)
+        if (g == NQ) {
+          switch_convs();
+          HZ_STAMP(10)
+        }
       const char *lb = lds + (q & 1) * kBufT;
-      const bool stage = q < NQ - 1;  // workgroup-uniform
+      // workgroup-uniform: the next chunk staged by every thread (from HBM,
+      // or Block: conv2's chunks 2 and 3 from E and tmp)
+      const bool stage = g < NQ - 1 || (Block && g >= NQ && g < NG - 1);
+      const bool sync = g < NQ - 1 || (Block && g >= NQ && g < NG - 1);
       const int nb = (q + 1) & 1;
       bf16x8 a[2][kRBT];  // [plane parity]: the plane in use, the one being read
       aread(a[0], lb, std::integral_constant<int, 0>{}, 0);
       static_for<0, 9>([&](auto tapc) {
         constexpr int tap = decltype(tapc)::value;
-        const int L = q * 9 + tap;
+        const int L = g * 9 + tap;
         static_for<0, 3>([&](auto pac) {
           constexpr int pa = decltype(pac)::value;
           constexpr int cur = (3 * tap + pa) & 1, nxt = cur ^ 1;
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (pa < 2)
+          if constexpr (HZ_KO & 32) {
+          } else if constexpr (pa < 2)
             aread(a[nxt], lb, tapc, pa + 1);
           else if constexpr (tap < 8)
             aread(a[nxt], lb, std::integral_constant<int, tap + 1>{}, 0);
           if constexpr (pa == 0) {
-            bissue(bn, L + 1);
-            if (tap == 0 && stage) stage_issue(q + 1);
+            if constexpr (!(HZ_KO & 16)) bissue(bn, L + 1);  // Block: conv2's first after conv1's last
+            if (tap == 0 && stage && !(HZ_KO & 1)) {
+              if (Block && g == NQ + 1)
+                stage_issue_e();
+              else if (Block && g >= NQ)
+                stage_issue_tmp(g == NQ + 2);
+              else
+                stage_issue(q + 1);
+            }
           }
-          if constexpr (pa == 1) {
+          if constexpr (HZ_KO & 2) {
+            if (tap == 7 && pa == 1 && stage)
+#pragma unroll
+              for (int it = 0; it < kW4Stg; it++) asm volatile("" ::"v"(stg[it]));
+          } else if constexpr (pa == 1 && !(HZ_KO & 1)) {
             if (stage) {
               if constexpr (tap >= 2 && tap <= 4) {
                 stage_put(2 * (tap - 2), nb);
@@ -978,7 +1112,8 @@ __global__ void __launch_bounds__(256, 1)
               if constexpr ((kX6ClassTaps[H][rb] >> tap) & 1) {
 #pragma unroll
                 for (int cb = 0; cb < NCB; cb++)
-                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
+                  acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[(HZ_KO & 32) ? 0 : cur][rb], b[pb][cb],
+                                                                        acc[rb][cb], 0, 0, 0);
               }
             });
           // one filler (VALU, LDS read or write, global load) after each MFMA
@@ -988,14 +1123,20 @@ __global__ void __launch_bounds__(256, 1)
             __builtin_amdgcn_sched_group_barrier(0x322, 1, 0);
           });
         });
+        if constexpr (!(HZ_KO & 16)) {
 #pragma unroll
-        for (int p = 0; p < 3; p++)
+          for (int p = 0; p < 3; p++)
 #pragma unroll
-          for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
+            for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
+        }
       });
       __builtin_amdgcn_sched_barrier(0);
-      if (stage) __syncthreads();
-      HZ_STAMP(3 + q)
+      if (sync) __syncthreads();
+      if (g < NQ) {
+        HZ_STAMP(3 + g)
+      } else {
+        HZ_STAMP(7 + g)  // Block: conv2's chunks in slots 11-14
+      }
     }
   };
   if (rh == 0)
@@ -1020,18 +1161,20 @@ __global__ void __launch_bounds__(256, 1)
     const int row = erow[rb];
     return row >= 0 && row < nrow ? row : -1;
   };
-  // every residual load in flight at once (36 float4 per lane)
+  // every residual load in flight at once (36 float4 per lane); Block: the
+  // skip input is the block input x, the bias conv2's
+  const float *eres = Block ? x : res, *ebias = Block ? bias2 : bias;
   float4 rv[kRBT * NCB];
 #pragma unroll
   for (int k = 0; k < kRBT * NCB; k++) {
     const int rb = k / NCB, cb = k % NCB;
     const int row = orow(rb);
-    rv[k] = res && row >= 0 ? *(const float4 *)(res + gbase + (size_t)row * 128 + cow + 16 * cb)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    rv[k] = eres && row >= 0 ? *(const float4 *)(eres + gbase + (size_t)row * 128 + cow + 16 * cb)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float4 bv[NCB];
 #pragma unroll
-  for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(bias + cow + 16 * cb);
+  for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(ebias + cow + 16 * cb);
 #pragma unroll
   for (int r0 = 0; r0 < kRBT * NCB; r0 += kT) {
 #pragma unroll
@@ -1055,7 +1198,7 @@ __global__ void __launch_bounds__(256, 1)
         v.y = a4[k].y + bv[cb].y;
         v.z = a4[k].z + bv[cb].z;
         v.w = a4[k].w + bv[cb].w;
-        if (res) {
+        if (eres) {
           v.x = v.x + rv[r0 + k].x;
           v.y = v.y + rv[r0 + k].y;
           v.z = v.z + rv[r0 + k].z;
@@ -1065,7 +1208,12 @@ __global__ void __launch_bounds__(256, 1)
         v.y = v.y > 0.f ? v.y : 0.f;
         v.z = v.z > 0.f ? v.z : 0.f;
         v.w = v.w > 0.f ? v.w : 0.f;
-        *(float4 *)(out + gbase + (size_t)row * 128 + cow + 16 * cb) = v;
+        if constexpr (HZ_KO & 4) {
+          int never = 0;
+          asm volatile("" : "+v"(never));
+          if (never) *(float4 *)(out + gbase + (size_t)row * 128 + cow + 16 * cb) = v;
+        } else
+          *(float4 *)(out + gbase + (size_t)row * 128 + cow + 16 * cb) = v;
       }
     }
   }
@@ -1126,21 +1274,41 @@ static bool x6_w4() {
   return v;
 }
 
+template <bool Block>
 static int launch_x6w4(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
-                       int32_t batch, const int32_t *live, void *stream) {
+                       int32_t batch, const int32_t *live, void *stream, const void *wpack6_2 = nullptr,
+                       const float *bias2 = nullptr, float *tmp = nullptr) {
   static std::atomic<uint64_t> init_mask{0};
-  const size_t lds = 2 * (size_t)(kCS * 35 * kX6Cell + kX6Zero);
+  const size_t lds = 2 * (size_t)(kCS * 35 * kX6Cell + kX6Zero) + (Block ? (size_t)(kRows + 1) * 128 + kX6Cell : 0);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3_x6w4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6w4<Block>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
       return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
-  hipLaunchKernelGGL(k_conv3x3_x6w4, dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
-                     (const bf16x8 *)wpack6, bias, res, out, batch, live);
+  hipLaunchKernelGGL(k_conv3x3_x6w4<Block>, dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
+                     (const bf16x8 *)wpack6, bias, res, out, batch, live, (const bf16x8 *)wpack6_2, bias2, tmp);
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// residual blocks run as one launch (k_conv3x3_x6w4<true>) where the tower
+// conv takes the 4-wave form only with HZ_X6_BLOCK=1: measured at parity with
+// the two layered launches (282.2 vs 284.1 us per block at 4096 rows, same
+// process, tools/block_ab.py; profiles/r03/block): under the chip's power
+// limit the cycles the fused form saves (conv1's epilogue, conv2's setup and
+// HBM staging) came back as a higher clock with slower chunks
+static std::atomic<int32_t> g_x6_block{-1};  // -1: from HZ_X6_BLOCK on first use
+static bool x6_block() {
+  int32_t v = g_x6_block.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("HZ_X6_BLOCK");
+    int32_t want = e && atoi(e) == 1 ? 1 : 0, expect = -1;
+    g_x6_block.compare_exchange_strong(expect, want);
+    v = g_x6_block.load(std::memory_order_relaxed);
+  }
+  return v == 1;
 }
 
 template <int NQ, bool Stem>
@@ -1148,7 +1316,7 @@ static int launch_x6(const float *x, const void *wpack6, const float *bias, cons
                      int32_t batch, const int32_t *live, void *stream) {
   if (batch <= x6_tiny_max()) return launch_x6_cs<NQ, Stem, 1, 1>(x, wpack6, bias, res, out, batch, live, stream);
   if constexpr (NQ == 4 && !Stem)
-    if (batch > x6_small_max() && x6_w4()) return launch_x6w4(x, wpack6, bias, res, out, batch, live, stream);
+    if (batch > x6_small_max() && x6_w4()) return launch_x6w4<false>(x, wpack6, bias, res, out, batch, live, stream);
   return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1, 2>(x, wpack6, bias, res, out, batch, live, stream)
                                  : launch_x6_cs<NQ, Stem, 8, 2>(x, wpack6, bias, res, out, batch, live, stream);
 }
@@ -1159,6 +1327,36 @@ extern "C" int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const 
   if (((uintptr_t)x | (uintptr_t)wpack6 | (uintptr_t)out | (uintptr_t)res) & 15) return -1;
   if (batch == 0) return 0;
   return launch_x6<4, false>(x, wpack6, bias, res, out, batch, live, stream);
+}
+
+// One residual block of the tower (model.py:287-299): out = relu(conv2(
+// relu(conv1(x) + b1)) + b2 + x).  Where the tower conv takes the 4-wave form
+// (batch above the one-state forms' limit) it is one launch whose
+// intermediate activation stays on the CU; otherwise the two layered convs
+// through tmp (the same bits either way).
+extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const float *b1, const void *w2,
+                                       const float *b2, float *out, float *tmp, int32_t batch, const int32_t *live,
+                                       void *stream) {
+  if (!x || !w1 || !b1 || !w2 || !b2 || !out || !tmp || batch < 0) return -1;
+  if (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)out | (uintptr_t)tmp) & 15) return -1;
+  if (batch == 0) return 0;
+  if (batch > x6_tiny_max() && batch > x6_small_max() && x6_w4() && x6_block())
+    return launch_x6w4<true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp);
+  const int rc = launch_x6<4, false>(x, w1, b1, nullptr, tmp, batch, live, stream);
+  return rc ? rc : launch_x6<4, false>(tmp, w2, b2, x, out, batch, live, stream);
+}
+
+// 1: residual blocks at the 4-wave conv's batch sizes run as one launch, 0:
+// as the two layered convs (the same bits either way; A/B and tests)
+extern "C" int hz_resblock_x6_set_fused(int32_t on) {
+  if (on != 0 && on != 1) return -1;
+  g_x6_block.store(on, std::memory_order_relaxed);
+  return 0;
+}
+
+// 1 when hz_resblock_x6_bias_act runs batch rows as one launch
+extern "C" int32_t hz_resblock_x6_fused(int32_t batch) {
+  return batch > x6_tiny_max() && batch > x6_small_max() && x6_w4() && x6_block() ? 1 : 0;
 }
 
 extern "C" int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *bias, float *out,

@@ -65,6 +65,9 @@ _SIGS = {
     "hz_heads_fc": ([_vp] * 13 + [_c.c_int32, _vp, _vp], _c.c_int),
     "hz_conv3x3_x6_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_stem3x3_x6_bias_act": ([_vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_resblock_x6_bias_act": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
+    "hz_resblock_x6_fused": ([_c.c_int32], _c.c_int32),
+    "hz_resblock_x6_set_fused": ([_c.c_int32], _c.c_int),
     "hz_tower_x6_resident": ([_vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split_max_batch": ([], _c.c_int32),

@@ -205,6 +205,24 @@ def _conv3x3_x6_act(x, wpack6, b, res=None, live=None):
     return out
 
 
+def _resblock_x6(x, p1, b1, p2, b2, live=None):
+    """One residual block (model.py:376-393, BN folded) on the x6 convs:
+    relu(conv2(relu(conv1(x) + b1)) + b2 + x) through hz_resblock_x6_bias_act
+    (one launch at the 4-wave conv's batch sizes, else the two layered convs;
+    bit-identical either way)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1:] == (128, 5, 7)):
+        raise NativeError("hz_resblock_x6_bias_act needs a CUDA fp32 channels_last [B,128,5,7] activation")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    tmp = torch.empty_like(x, memory_format=torch.channels_last)
+    rc = lib().hz_resblock_x6_bias_act(x.data_ptr(), p1.data_ptr(), b1.data_ptr(), p2.data_ptr(), b2.data_ptr(),
+                                       out.data_ptr(), tmp.data_ptr(), x.shape[0], _live_ptr(live),
+                                       torch.cuda.current_stream(x.device).cuda_stream)
+    if rc != 0:
+        raise NativeError(f"hz_resblock_x6_bias_act failed ({rc})")
+    return out
+
+
 def pack_stem_x6(w):
     """Stem weights [128][38][3][3] in hz_stem3x3_x6_bias_act's layout: bf16
     planes [K-step][q][plane][co][32] over 64 input slots.  Slots 0-37 are
@@ -431,11 +449,13 @@ class FoldedNet(nn.Module):
             x = xs
         elif self.resident is not None and B <= max(self.resident_max, min(self.split_max, 32)):
             x = _tower_resident(x, *self.resident, live)
-        elif self.packed is not None:
-            conv = _conv3x3_x6_act if self.tower == "x6" else _conv3x3_act
+        elif self.packed is not None and self.tower == "x6":
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
-                y = conv(x, p1, b1, None, live)
-                x = conv(y, p2, b2, x, live)
+                x = _resblock_x6(x, p1, b1, p2, b2, live)
+        elif self.packed is not None:
+            for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
+                y = _conv3x3_act(x, p1, b1, None, live)
+                x = _conv3x3_act(y, p2, b2, x, live)
         else:
             for (w1, b1), (w2, b2) in self.blocks:
                 y = ep(F.conv2d(x, w1, None, padding=1), b1)

@@ -245,6 +245,22 @@ int hz_conv3x3_bias_act(const float *x, const float *wpack, const float *bias, c
 int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                            int32_t batch, const int32_t *live, void *stream);
 
+/* One residual block of the tower (model.py:376-393, ResidualBlock.forward
+ * with BN folded): out = relu(conv2(relu(conv1(x) + b1)) + b2 + x), w1/w2
+ * packed as for hz_conv3x3_x6_bias_act; x, out NHWC [batch][5][7][128] (out
+ * must not alias x); tmp = scratch of batch*35*128 floats.  Bit-identical to
+ * hz_conv3x3_x6_bias_act(x, w1, b1, NULL, tmp) followed by
+ * hz_conv3x3_x6_bias_act(tmp, w2, b2, x, out); in its one-launch form
+ * (hz_resblock_x6_fused(batch) == 1) the intermediate activation stays on
+ * the CU (tmp holds half of it, briefly). */
+int hz_resblock_x6_bias_act(const float *x, const void *w1, const float *b1, const void *w2, const float *b2,
+                            float *out, float *tmp, int32_t batch, const int32_t *live, void *stream);
+int32_t hz_resblock_x6_fused(int32_t batch);
+/* on = 1: hz_resblock_x6_bias_act takes the one-launch form where it applies;
+ * 0 (the default, unless HZ_X6_BLOCK=1): the two layered convs.  Measured at
+ * parity with each other; results are bit-identical. */
+int hz_resblock_x6_set_fused(int32_t on);
+
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the
  * encoder writes it, out NHWC [batch][5][7][128], wpack = w with the input

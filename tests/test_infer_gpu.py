@@ -403,6 +403,48 @@ def test_x6_eight_state_form_live_rows_and_accuracy():
     assert torch.equal(part[:517], full[:517])
 
 
+@pytest.mark.parametrize("batch", [769, 803, 4096])
+def test_resblock_x6_fused_equals_two_layered_convs(batch):
+    """hz_resblock_x6_bias_act as one launch (the 4-wave conv's batch sizes:
+    conv1's output relu(acc + b1) staged for conv2 on the CU, through LDS and
+    half of it through tmp) gives the bits of the two layered convs,
+    with a partly filled last workgroup (803 = 100 x 8 + 3), a live-row bound
+    inside a workgroup, and a NaN tail past the input (nothing read past the
+    batch); and stays within fp32 rounding of a float64 block."""
+    from hzamd._native import lib
+    from hzamd.infer import _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6
+    assert lib().hz_resblock_x6_set_fused(1) == 0
+    try:
+        _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6)
+    finally:
+        lib().hz_resblock_x6_set_fused(0)
+
+
+def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):
+    assert lib().hz_resblock_x6_fused(batch) == 1
+    g = torch.Generator().manual_seed(batch)
+    cl = torch.channels_last
+    x = torch.randn(batch, 128, 5, 7, generator=g).relu()
+    w1 = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+    w2 = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+    b1 = torch.randn(128, generator=g) * 0.1
+    b2 = torch.randn(128, generator=g) * 0.1
+    buf = torch.full((batch + 9, 128, 5, 7), float("nan"), device="cuda").contiguous(memory_format=cl)
+    buf[:batch] = x.cuda()
+    xc = buf[:batch]
+    p1, p2 = pack_conv3x3_x6(w1).cuda(), pack_conv3x3_x6(w2).cuda()
+    b1c, b2c = b1.cuda(), b2.cuda()
+    fused = _resblock_x6(xc, p1, b1c, p2, b2c)
+    layered = _conv3x3_x6_act(_conv3x3_x6_act(xc, p1, b1c), p2, b2c, xc)
+    assert torch.equal(fused, layered)
+    live = torch.tensor([batch - 4], dtype=torch.int32, device="cuda")
+    part = _resblock_x6(xc, p1, b1c, p2, b2c, live)
+    assert torch.equal(part[:batch - 4], fused[:batch - 4])
+    k = 48
+    want = _conv_ref(_conv_ref(x[:k], w1, b1, None).float(), w2, b2, x[:k])
+    assert (fused[:k].cpu().double() - want).abs().max().item() <= 2e-5
+
+
 @pytest.mark.parametrize("batch", [1, 5, 64, 256, 1024])
 def test_resident_tower_matches_layered_tower(batch):
     """hz_tower_x6_resident (small batches: the whole tower in one launch,

@@ -31,7 +31,7 @@ out = torch.empty_like(x)
 for _ in range(200):  # ~70 ms of back-to-back launches so the clock settles
     assert fn(x.data_ptr(), w.data_ptr(), b.data_ptr(), None if NORES else r.data_ptr(), out.data_ptr(), B,
                                    None, torch.cuda.current_stream().cuda_stream) == 0
-st = np.zeros((1024, 2, 10), dtype=np.uint64)
+st = np.zeros((1024, 2, 16), dtype=np.uint64)
 assert lib.hz_net_diag_stamps(st.ctypes.data) == 0
 nwg = (B + 7) // 8
 s = st[:nwg].astype(np.int64)

@@ -32,7 +32,7 @@ args = [x, glob, *fn.heads, *fn.fc]
 for _ in range(300):
     assert lib.hz_heads_fc(*(t.data_ptr() for t in args), None, probs.data_ptr(), value.data_ptr(), B, None,
                            torch.cuda.current_stream().cuda_stream) == 0
-st = np.zeros((1024, 2, 10), dtype=np.uint64)
+st = np.zeros((1024, 2, 16), dtype=np.uint64)
 assert lib.hz_net_diag_stamps(st.ctypes.data) == 0
 nwg = min(1024, (B + 7) // 8)
 s = st[:nwg, 0].astype(np.int64)
