@@ -337,19 +337,31 @@ __device__ __forceinline__ uint32_t bf16_bits(float v) {
 }
 __device__ __forceinline__ float bf16_value(uint32_t b) { return __uint_as_float(b << 16); }
 
-// the three bf16 planes of four consecutive channels: 8 B per plane
+// two floats rounded to bf16 (nearest-even) in one v_cvt_pk_bf16_f32: a in
+// the low half, b in the high half
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_v;
+typedef __attribute__((ext_vector_type(2))) float f32x2_v;
+__device__ __forceinline__ uint32_t bf16_pair(float a, float b) {
+  const f32x2_v f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_v));
+}
+__device__ __forceinline__ float bf16_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+// the three bf16 planes of four consecutive channels: 8 B per plane; each
+// plane's pairs come out of one paired conversion already packed (22 VALU
+// per float4 instead of ~38 for per-element conversions and packing; the
+// same roundings, so the same bits)
 __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 &l) {
-  uint32_t hb[4], mb[4], lb[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    hb[j] = bf16_bits(v[j]);
-    const float r1 = v[j] - bf16_value(hb[j]);
-    mb[j] = bf16_bits(r1);
-    lb[j] = bf16_bits(r1 - bf16_value(mb[j]));
-  }
-  h = make_uint2(hb[0] | hb[1] << 16, hb[2] | hb[3] << 16);
-  m = make_uint2(mb[0] | mb[1] << 16, mb[2] | mb[3] << 16);
-  l = make_uint2(lb[0] | lb[1] << 16, lb[2] | lb[3] << 16);
+  const uint32_t h01 = bf16_pair(v[0], v[1]), h23 = bf16_pair(v[2], v[3]);
+  const float r0 = v[0] - bf16_lo(h01), r1 = v[1] - bf16_hi(h01);
+  const float r2 = v[2] - bf16_lo(h23), r3 = v[3] - bf16_hi(h23);
+  const uint32_t m01 = bf16_pair(r0, r1), m23 = bf16_pair(r2, r3);
+  const float s0 = r0 - bf16_lo(m01), s1 = r1 - bf16_hi(m01);
+  const float s2 = r2 - bf16_lo(m23), s3 = r3 - bf16_hi(m23);
+  h = make_uint2(h01, h23);
+  m = make_uint2(m01, m23);
+  l = make_uint2(bf16_pair(s0, s1), bf16_pair(s2, s3));
 }
 
 // Tap classes (8-state tower conv).  On the 5x7 board with zero padding a
