@@ -535,7 +535,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   // lane keeps the LDS banks its row would use).
   // valid[rb] bit tap = the neighbour is on the board.
   // the 8-state tower groups its rows by tap class (above)
-  constexpr bool kClassed = CS == 8 && !Stem && NCB == 2;
+  constexpr bool kClassed = CS == 8 && NCB == 2;  // the 8-state forms: tower conv and stem
   int cbase[kRBT];
   uint32_t valid[kRBT];
 #pragma unroll
@@ -611,12 +611,13 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
     for (int cb = 0; cb < NCB; cb++) b[p][cb] = bload(0, p, cb);
 
   // classed main loop: the chunk loop rolled, the taps unrolled, one copy
-  // per row half (its blocks' tap sets are compile-time constants)
+  // per row half (its blocks' tap sets are compile-time constants).  The
+  // stem (two chunks, unrolled): its second chunk is tap-packed (a K-step
+  // holds 4 taps), where every block issues all 3 K-steps as in the
+  // unclassed loop
   auto classed = [&](auto half) {
     constexpr int H = decltype(half)::value;
-    for (int q = 0; q < NQ; q++) {
-      const char *lb = lds + (q & 1) * kBufT;
-      if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
+    auto taps = [&](int q, const char *lb) __attribute__((always_inline)) {
 #pragma unroll
       for (int tap = 0; tap < 9; tap++) {
         const int L = q * 9 + tap, Ln = L + 1 < 9 * NQ ? L + 1 : 9 * NQ - 1;
@@ -626,6 +627,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
           for (int cb = 0; cb < NCB; cb++) bn[p][cb] = bload(Ln, p, cb);
 #pragma unroll
         for (int pa = 0; pa < 3; pa++) {
+          if (Stem && pa >= npa) break;  // the chunk's A pieces m, l are zero (stem on encoder boards)
           bf16x8 a[kRBT];
 #pragma unroll
           for (int rb = 0; rb < kRBT; rb++) {
@@ -653,11 +655,54 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
           for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
         __builtin_amdgcn_sched_barrier(0);  // taps stay in order (registers: no hoisting across)
       }
-      if (q < NQ - 1) {
-        HZ_X6_STORE((q + 1) & 1)
-        HZ_X6_SYNC(npa_next)
+    };
+    if constexpr (Stem) {
+      static_assert(NQ == 2, "the stem has two chunks");
+      HZ_X6_LOAD(1)
+      taps(0, lds);
+      HZ_X6_STORE(1)
+      HZ_X6_SYNC(npa_next)
+      npa = npa_next ? 3 : 1;
+      HZ_STAMP(3)
+      const char *lb = lds + kBufT;
+#pragma unroll
+      for (int st = 0; st < 3; st++) {
+        const int L = 9 + st, Ln = L + 1;
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+          for (int cb = 0; cb < NCB; cb++) bn[p][cb] = bload(Ln, p, cb);
+#pragma unroll
+        for (int pa = 0; pa < 3; pa++) {
+          if (pa >= npa) break;
+          bf16x8 a[kRBT];
+#pragma unroll
+          for (int rb = 0; rb < kRBT; rb++) a[rb] = *(const bf16x8 *)(lb + aoff_tp(rb, st) + 64 * pa);
+#pragma unroll
+          for (int pb = 0; pb < 3 - pa; pb++)
+#pragma unroll
+            for (int rb = 0; rb < kRBT; rb++)
+#pragma unroll
+              for (int cb = 0; cb < NCB; cb++)
+                acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[pb][cb], acc[rb][cb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+          for (int cb = 0; cb < NCB; cb++) b[p][cb] = bn[p][cb];
       }
-      HZ_STAMP(3 + q)
+      HZ_STAMP(4)
+    } else {
+      for (int q = 0; q < NQ; q++) {
+        const char *lb = lds + (q & 1) * kBufT;
+        if (q < NQ - 1) { HZ_X6_LOAD(q + 1) }
+        taps(q, lb);
+        if (q < NQ - 1) {
+          HZ_X6_STORE((q + 1) & 1)
+          HZ_X6_SYNC(npa_next)
+        }
+        HZ_STAMP(3 + q)
+      }
     }
   };
   if constexpr (kClassed) {

@@ -228,12 +228,14 @@ def test_folded_small_batches_match_large_batch():
         assert torch.allclose(l1, l0[:k], atol=1e-5) and torch.allclose(v1, v0[:k], atol=1e-5), k
 
 
-def test_stem_x6_fp32_accuracy_vs_fp64():
+@pytest.mark.parametrize("n", [200, 1000])
+def test_stem_x6_fp32_accuracy_vs_fp64(n):
     """Encoder-like boards (0, 1/3, 2/3, 1, bag fractions: not bf16 values):
-    the bf16x6 stem's error vs a float64 conv is at the f32 stem's level."""
+    the bf16x6 stem's error vs a float64 conv is at the f32 stem's level, in
+    the one-state form (200 rows) and the eight-state form with tap classes
+    (1000 rows: all six products, the packed second chunk for every block)."""
     from hzamd.infer import _stem_act, _stem_x6_act, pack_stem, pack_stem_x6
     g = torch.Generator().manual_seed(4)
-    n = 200
     board = torch.randint(0, 4, (n, 38, 5, 7), generator=g).float() / 3.0
     w = torch.randn(128, 38, 3, 3, generator=g) * 0.1
     b = torch.randn(128, generator=g) * 0.1
@@ -264,7 +266,7 @@ def test_heads_match_torch(batch):
 
 
 @pytest.mark.parametrize("kind", ["f32", "x6"])
-@pytest.mark.parametrize("batch", [1, 13, 64])
+@pytest.mark.parametrize("batch", [1, 13, 64, 1000])
 def test_stem_exact_on_integer_data(batch, kind):
     """hz_stem3x3_bias_act / hz_stem3x3_x6_bias_act on small-integer data
     equal the fp64 conv exactly (NCHW board in, NHWC out; channel padding
