@@ -311,14 +311,21 @@ def bench_loop(args, dev, rank, world):
 
 class TimedEvaluator:
     """Wraps the leaf evaluator: HIP events around every call (the current
-    stream, where the network's kernels run) and the rows it computed."""
+    stream, where the network's kernels run); `rows` = the rows it computed
+    since reset(), read from the search's own device counter (k_gather adds
+    each simulation's live-row count; one add per search), so the timed
+    region holds no counting kernel of the benchmark's."""
 
     device_rows = True
 
     def __init__(self, pred, dev):
         self.pred = pred
         self.events = []
-        self.rows = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.mcts = None  # attach(): the BatchedMCTS whose searches call this evaluator
+        self._base = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def attach(self, mcts):
+        self.mcts = mcts
 
     def __call__(self, board, glob, rows=None, count=None):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -326,13 +333,16 @@ class TimedEvaluator:
         out = self.pred(board, glob, rows, count)
         b.record()
         self.events.append((a, b))
-        self.rows += count if count is not None else board.shape[0]
         return out
+
+    @property
+    def rows(self):
+        return self.mcts.eval_rows_total - self._base
 
     def reset(self):
         torch.cuda.synchronize()
         self.events.clear()
-        self.rows.zero_()
+        self._base = self.mcts.eval_rows_total.clone()
 
     def ms(self):
         return sum(a.elapsed_time(b) for a, b in self.events)
@@ -388,6 +398,7 @@ def _selfplay_setup(args, dev, rank, sims, n):
     ev = TimedEvaluator(BatchedPredictor(net, dtype=dtype), dev)
     ev.network = what
     sp = SelfPlay(n, ev, cfg, seed_base=args.seed_base + rank * n, device=dev)
+    ev.attach(sp.mcts)
     return sp, ev
 
 

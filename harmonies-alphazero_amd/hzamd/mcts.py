@@ -49,6 +49,7 @@ class BatchedMCTS:
         self.rows = torch.zeros(self.n, dtype=torch.int32, device=d)
         self.count = torch.zeros(1, dtype=torch.int32, device=d)
         self.eval_rows = torch.zeros(1, dtype=torch.int64, device=d)  # leaves evaluated, last search
+        self.eval_rows_total = torch.zeros(1, dtype=torch.int64, device=d)  # ... all searches (one add each)
         # k_gather adds each simulation's gathered row count to it (no extra kernel)
         nat.check(L.hz_mcts_set_eval_counter(self._h, nat.ptr(self.eval_rows)), "hz_mcts_set_eval_counter")
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
@@ -222,6 +223,7 @@ class BatchedMCTS:
         evaluation of it went through a timed-out split-tower hand-off (whose
         NaN priors would have steered PUCT silently): NativeError if one did."""
         from .infer import check_split_timeouts
+        self.eval_rows_total += self.eval_rows
         visits = self.result()
         check_split_timeouts(self.device)
         return visits
