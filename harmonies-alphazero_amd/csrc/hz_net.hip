@@ -2128,6 +2128,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   __shared__ float4 vin[kVIn][kHS / 4];
   __shared__ float lg[kHS][kAct + 1];
   __shared__ float vpart[4][kHS];
+  __shared__ float hpart[kHS * 35 * 8][3];  // the 1x1 convs' partial sums per 16-channel group
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (live) batch = *live < batch ? *live : batch;
   const int s0 = blockIdx.x * kHS;
@@ -2145,39 +2146,60 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   __syncthreads();
   HZ_HSTAMP(1)
 
-  // 1. heads' 1x1 convs (rows past the batch reread its last state)
+  // 1. heads' 1x1 convs (rows past the batch reread its last state).  Work
+  // item = (state, cell, 16-channel group): every lane busy and every load of
+  // the thread issued before any is used (one memory round trip instead of
+  // four); the group's three partial sums go to LDS and each (state, cell)
+  // adds its eight in group order: k_heads_fc1's split and order, the same
+  // bits
+  {
+    constexpr int kItems = kHS * 35 * 8, kIt = (kItems + 255) / 256;
+    f32x4 u[kIt][4];
 #pragma unroll
-  for (int pr = 0; pr < kHS / 8; pr++) {
-    if (lane >= 35) break;
-    const int sa = w + 8 * pr, sb = sa + 4;
-    const float4 *xa = (const float4 *)(x + ((size_t)(s0 + (sa < ns ? sa : ns - 1)) * 35 + lane) * 128);
-    const float4 *xb = (const float4 *)(x + ((size_t)(s0 + (sb < ns ? sb : ns - 1)) * 35 + lane) * 128);
-    // eight partial sums of 16 channels added in order (k_heads_fc1's split)
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
-#pragma unroll 2
-    for (int kk = 0; kk < 8; kk++) {
-      float e0 = 0.f, e1 = 0.f, e2 = 0.f, f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    for (int it = 0; it < kIt; it++) {
+      int i = it * 256 + t;
+      i = i < kItems ? i : kItems - 1;
+      const int sl = i / 280, rem = i - 280 * sl, cell = rem >> 3, kk = rem & 7;
+      const f32x4 *xr = (const f32x4 *)(x + ((size_t)(s0 + (sl < ns ? sl : ns - 1)) * 35 + cell) * 128) + 4 * kk;
 #pragma unroll
-      for (int k4 = 0; k4 < 4; k4++) {
-        const int k = 4 * kk + k4;
-        const float4 u = xa[k], v = xb[k], p = w4[0][k], q = w4[1][k], r = w4[2][k];
-        e0 += u.x * p.x + u.y * p.y + u.z * p.z + u.w * p.w;
-        e1 += u.x * q.x + u.y * q.y + u.z * q.z + u.w * q.w;
-        e2 += u.x * r.x + u.y * r.y + u.z * r.z + u.w * r.w;
-        f0 += v.x * p.x + v.y * p.y + v.z * p.z + v.w * p.w;
-        f1 += v.x * q.x + v.y * q.y + v.z * q.z + v.w * q.w;
-        f2 += v.x * r.x + v.y * r.y + v.z * r.z + v.w * r.w;
-      }
-      a0 += e0, a1 += e1, a2 += e2, c0 += f0, c1 += f1, c2 += f2;
+      for (int k4 = 0; k4 < 4; k4++) u[it][k4] = xr[k4];
     }
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+      const int i = it * 256 + t;
+      if (i < kItems) {
+        const int kk = i & 7;
+        float e0 = 0.f, e1 = 0.f, e2 = 0.f;
+#pragma unroll
+        for (int k4 = 0; k4 < 4; k4++) {
+          const int k = 4 * kk + k4;
+          const f32x4 v = u[it][k4];
+          const float4 p = w4[0][k], q = w4[1][k], r = w4[2][k];
+          e0 += v[0] * p.x + v[1] * p.y + v[2] * p.z + v[3] * p.w;
+          e1 += v[0] * q.x + v[1] * q.y + v[2] * q.z + v[3] * q.w;
+          e2 += v[0] * r.x + v[1] * r.y + v[2] * r.z + v[3] * r.w;
+        }
+        hpart[i][0] = e0;
+        hpart[i][1] = e1;
+        hpart[i][2] = e2;
+      }
+    }
+    __syncthreads();
     const float h0 = hb[0], h1 = hb[1], h2 = hb[2];
-    a0 += h0, a1 += h1, a2 += h2, c0 += h0, c1 += h1, c2 += h2;
-    ((float *)pin[lane])[sa] = a0 > 0.f ? a0 : 0.f;
-    ((float *)pin[35 + lane])[sa] = a1 > 0.f ? a1 : 0.f;
-    ((float *)vin[lane])[sa] = a2 > 0.f ? a2 : 0.f;
-    ((float *)pin[lane])[sb] = c0 > 0.f ? c0 : 0.f;
-    ((float *)pin[35 + lane])[sb] = c1 > 0.f ? c1 : 0.f;
-    ((float *)vin[lane])[sb] = c2 > 0.f ? c2 : 0.f;
+    for (int i = t; i < kHS * 35; i += 256) {
+      const int sl = i / 35, cell = i - 35 * sl;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 8; kk++) {
+        a0 += hpart[8 * i + kk][0];
+        a1 += hpart[8 * i + kk][1];
+        a2 += hpart[8 * i + kk][2];
+      }
+      a0 += h0, a1 += h1, a2 += h2;
+      ((float *)pin[cell])[sl] = a0 > 0.f ? a0 : 0.f;
+      ((float *)pin[35 + cell])[sl] = a1 > 0.f ? a1 : 0.f;
+      ((float *)vin[cell])[sl] = a2 > 0.f ? a2 : 0.f;
+    }
   }
   __syncthreads();
   HZ_HSTAMP(2)
