@@ -2077,34 +2077,50 @@ __device__ __forceinline__ float wave_max(float v) {
 // the workgroup.  The blocks are k_heads_fc1's input chunks (policy 7 x 16,
 // value 4 x 20 with the last cut at 17) and every sum runs in its order, so
 // the two head kernels give bit-identical rows: a board's priors do not
-// depend on the size of the batch it was evaluated in.
+// depend on the size of the batch it was evaluated in.  The next block's
+// weight loads are in flight while the current block is summed (one exposed
+// L2 round trip instead of NB).
 template <int J, int NB, int JB = J / NB>
-__device__ __forceinline__ void fcn(const float *__restrict__ w, int ld, int col, const float4 (*in)[kHS / 4],
-                                    float (&out)[kHS]) {
+__device__ __forceinline__ void fcn_pipe(const float *__restrict__ w, int ld, int col,
+                                         const float4 (*in)[kHS / 4], float (&out)[kHS]) {
   static_assert(NB * JB >= J && (NB - 1) * JB < J, "NB blocks of JB rows cover J");
   constexpr bool ragged = NB * JB != J;
   float part[NB][kHS];
   const int r0 = blockIdx.x % NB;
-  for (int bi = 0; bi < NB; bi++) {
-    int blk = r0 + bi;
-    blk -= blk >= NB ? NB : 0;
+  auto block_of = [&](int bi) {
+    const int blk = r0 + bi;
+    return blk >= NB ? blk - NB : blk;
+  };
+  auto load = [&](float(&dst)[JB], int blk) {
     const float *wb = w + blk * JB * ld + col;
+#pragma unroll
+    for (int j = 0; j < JB; j++) dst[j] = ragged && blk * JB + j >= J ? 0.f : wb[(ragged && blk * JB + j >= J ? 0 : j) * ld];
+  };
+  float wc[JB], wn[JB];
+  load(wc, block_of(0));
+  for (int bi = 0; bi < NB; bi++) {
+    const int blk = block_of(bi);
+    if (bi + 1 < NB) load(wn, block_of(bi + 1));
     const float4(*ib)[kHS / 4] = in + blk * JB;
+    const int jn = ragged && J - blk * JB < JB ? J - blk * JB : JB;  // block-uniform
     float p[kHS] = {};
 #pragma unroll
-    for (int j = 0; j < JB; j++) {  // the block's weight loads all in flight
-      if (ragged && blk * JB + j >= J) break;
-      const float wv = wb[j * ld];
+    for (int j = 0; j < JB; j++) {
+      if (!ragged || j < jn) {  // (rows past J are not read: they are not in the input)
+        const float wv = wc[j];
 #pragma unroll
-      for (int q = 0; q < kHS / 4; q++) {
-        const float4 v = ib[j][q];
-        p[4 * q] += wv * v.x, p[4 * q + 1] += wv * v.y, p[4 * q + 2] += wv * v.z, p[4 * q + 3] += wv * v.w;
+        for (int q = 0; q < kHS / 4; q++) {
+          const float4 v = ib[j][q];
+          p[4 * q] += wv * v.x, p[4 * q + 1] += wv * v.y, p[4 * q + 2] += wv * v.z, p[4 * q + 3] += wv * v.w;
+        }
       }
     }
 #pragma unroll
     for (int b = 0; b < NB; b++)
 #pragma unroll
       for (int s = 0; s < kHS; s++) part[b][s] = b == blk ? p[s] : part[b][s];
+#pragma unroll
+    for (int j = 0; j < JB; j++) wc[j] = wn[j];
   }
 #pragma unroll
   for (int s = 0; s < kHS; s++) {
@@ -2207,7 +2223,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   // 2. policy logits
   if (t < kAct) {
     float acc[kHS];
-    fcn<kPIn, 7>(wpT, kAct, t, pin, acc);
+    fcn_pipe<kPIn, 7>(wpT, kAct, t, pin, acc);
     const float bb = bp[t];
 #pragma unroll
     for (int s = 0; s < kHS; s++) lg[s][t] = acc[s] + bb;
@@ -2217,7 +2233,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   // 3. value: hidden unit t, relu, times w2[t], summed over the units
   {
     float acc[kHS];
-    fcn<kVIn, 4, 20>(w1T, kHid, t, vin, acc);
+    fcn_pipe<kVIn, 4, 20>(w1T, kHid, t, vin, acc);
     const float bb = b1[t], wo = w2[t];
 #pragma unroll
     for (int s = 0; s < kHS; s++) {
