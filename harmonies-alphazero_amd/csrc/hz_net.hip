@@ -398,13 +398,31 @@ alignas(16) __constant__ int16_t kX6ClassRow[18][16] = {
 };
 // kX6ClassSel: the block taps some of whose rows (the corner cells) read
 // off the board: only those need the zero-region redirect
-constexpr uint32_t kX6ClassSel[2][9] = {
+constexpr uint32_t kX6ClassSel[3][9] = {
     {0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000, 0x000},
     {0x000, 0x000, 0x000, 0x000, 0x048, 0x000, 0x024, 0x180, 0x003},
+    {0x000, 0x000, 0x000, 0x1c0, 0x000, 0x168, 0x000, 0x180, 0x0c0},  // 4-state groups (kX6C4Row)
 };
-constexpr uint32_t kX6ClassTaps[2][9] = {
+constexpr uint32_t kX6ClassTaps[3][9] = {
     {0x1ff, 0x1ff, 0x1ff, 0x1ff, 0x1f8, 0x1f8, 0x03f, 0x1b6, 0x0db},
     {0x1ff, 0x1ff, 0x1ff, 0x1ff, 0x1f8, 0x03f, 0x03f, 0x1b6, 0x0db},
+    {0x1ff, 0x1ff, 0x1ff, 0x1ff, 0x1f8, 0x1f8, 0x03f, 0x1b6, 0x0db},  // 4-state groups (kX6C4Row)
+};
+// The same grouping for 4 states (140 rows, 9 blocks; class index 2 of the
+// tables above): 4 nine-tap blocks (the 60 interior cells and 4 BM cells),
+// TM (+ the TL, TR corners: two blocks, 4 padding rows), BM, ML (+ BL), MR
+// (+ BR): 66 block-taps, half of the 8-state groups' 132 (tools: the
+// generator in DESIGN.md §3, k_conv3x3_x6 CS = 4 row)
+alignas(16) __constant__ int16_t kX6C4Row[9][16] = {
+    {8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 22, 23, 24, 25, 26, 43},
+    {44, 45, 46, 47, 50, 51, 52, 53, 54, 57, 58, 59, 60, 61, 78, 79},
+    {80, 81, 82, 85, 86, 87, 88, 89, 92, 93, 94, 95, 96, 113, 114, 115},
+    {116, 117, 120, 121, 122, 123, 124, 127, 128, 129, 130, 131, 135, 136, 137, 138},
+    {1, 2, 3, 4, 5, 36, 37, 38, 39, 40, 71, 72, 73, 74, 75, 106},
+    {107, 108, 109, 110, 0, 35, 70, 105, 6, 41, 76, 111, -1, -1, -1, -1},
+    {29, 30, 31, 32, 33, 64, 65, 66, 67, 68, 99, 100, 101, 102, 103, 134},
+    {7, 14, 21, 42, 49, 56, 77, 84, 91, 112, 119, 126, 28, 63, 98, 133},
+    {13, 20, 27, 48, 55, 62, 83, 90, 97, 118, 125, 132, 34, 69, 104, 139},
 };
 
 // NQ chunks of 32 input channels.  Stem: x is the encoder's NCHW board
@@ -417,14 +435,14 @@ constexpr uint32_t kX6ClassTaps[2][9] = {
 // the arena's batches of a few dozen boards fill only a few CUs; one state
 // per group cuts each wave's chain to a third at 48/35 rows of waste.
 template <int NQ, bool Stem, int CS, int NCB>
-__global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
+__global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, CS == 4 ? 2 : 1)
     k_conv3x3_x6(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                  const float *__restrict__ res, float *__restrict__ out, int32_t batch,
                  const int32_t *__restrict__ live) {
-  static_assert(CS == 8 || CS == 1, "8 or 1 states per workgroup");
+  static_assert(CS == 8 || CS == 4 || CS == 1, "8, 4 or 1 states per workgroup");
   static_assert(NCB == 2 || NCB == 1, "column blocks of 16 output channels per wave");
   constexpr int kRowsT = CS * 35;                  // output rows of the group
-  constexpr int kRBT = CS == 8 ? 9 : 3;            // row blocks of 16 per wave
+  constexpr int kRBT = CS == 1 ? 3 : 9;            // row blocks of 16 per wave
   constexpr int kCG = 8 / NCB;                     // column groups (waves per row group)
   constexpr int kThreads = (CS == 8 ? 2 : 1) * kCG * 64;
   constexpr int kStg = (kRowsT * 8 + kThreads - 1) / kThreads;  // float4 staged per thread per chunk
@@ -535,15 +553,17 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   // lane keeps the LDS banks its row would use).
   // valid[rb] bit tap = the neighbour is on the board.
   // the 8-state tower groups its rows by tap class (above)
-  constexpr bool kClassed = CS == 8 && NCB == 2;  // the 8-state forms: tower conv and stem
+  constexpr bool kClassed = CS != 1 && NCB == 2;  // the 8-state forms (tower conv, stem), the 4-state one
+  // the class table's row of block idx (CS = 4: its own 9-block table, class index 2)
+  auto class_row = [&](int idx, int i) -> int { return CS == 4 ? kX6C4Row[idx][i] : kX6ClassRow[idx][i]; };
   int cbase[kRBT];
   uint32_t valid[kRBT];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
     int r = (rh * kRBT + rb) * 16 + (lane & 15);
     if constexpr (kClassed) {
-      r = kX6ClassRow[rh * kRBT + rb][lane & 15];
-      r = r >= 0 ? r : kX6ClassRow[rh * kRBT + rb][0];  // padding rows read a real row (not stored)
+      r = class_row(rh * kRBT + rb, lane & 15);
+      r = r >= 0 ? r : class_row(rh * kRBT + rb, 0);  // padding rows read a real row (not stored)
     }
     r = r < kRowsT ? r : kRowsT - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
@@ -561,7 +581,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
   int erow[kClassed ? kRBT : 1];
   if constexpr (kClassed) {
 #pragma unroll
-    for (int rb = 0; rb < kRBT; rb++) erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
+    for (int rb = 0; rb < kRBT; rb++) erow[rb] = class_row(rh * kRBT + rb, lane >> 2);
   }
   auto aoff = [&](int rb, int tap) -> int {
     const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
@@ -705,7 +725,9 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, 1)
       }
     }
   };
-  if constexpr (kClassed) {
+  if constexpr (kClassed && CS == 4) {
+    classed(std::integral_constant<int, 2>{});
+  } else if constexpr (kClassed) {
     if (rh == 0)
       classed(std::integral_constant<int, 0>{});
     else
@@ -1368,10 +1390,24 @@ static bool x6_block() {
   return v == 1;
 }
 
+// HZ_X6_CS4=1: the tower conv above the one-state forms' limit as the
+// 4-state form (k_conv3x3_x6<4, false, 4, 2>: two 4-wave workgroups per CU,
+// each one's epilogue and staging free to overlap the other's MFMAs;
+// A/B measurements)
+static bool x6_cs4() {
+  static const bool v = [] {
+    const char *e = getenv("HZ_X6_CS4");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 template <int NQ, bool Stem>
 static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                      int32_t batch, const int32_t *live, void *stream) {
   if (batch <= x6_tiny_max()) return launch_x6_cs<NQ, Stem, 1, 1>(x, wpack6, bias, res, out, batch, live, stream);
+  if constexpr (NQ == 4 && !Stem)
+    if (batch > x6_small_max() && x6_cs4()) return launch_x6_cs<NQ, Stem, 4, 2>(x, wpack6, bias, res, out, batch, live, stream);
   if constexpr (NQ == 4 && !Stem)
     if (batch > x6_small_max() && x6_w4()) return launch_x6w4<false>(x, wpack6, bias, res, out, batch, live, stream);
   return batch <= x6_small_max() ? launch_x6_cs<NQ, Stem, 1, 2>(x, wpack6, bias, res, out, batch, live, stream)
