@@ -447,6 +447,40 @@ def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):
     assert (fused[:k].cpu().double() - want).abs().max().item() <= 2e-5
 
 
+_CS4_SCRIPT = """
+import sys, torch
+sys.path[:0] = [sys.argv[2]]
+from hzamd.infer import _conv3x3_x6_act, pack_conv3x3_x6
+g = torch.Generator().manual_seed(77)
+x = torch.randn(1003, 128, 5, 7, generator=g).relu()
+w = torch.randn(128, 128, 3, 3, generator=g) * 0.03
+b = torch.randn(128, generator=g) * 0.1
+r = torch.randn(1003, 128, 5, 7, generator=g)
+cl = torch.channels_last
+xc, rc = x.cuda().contiguous(memory_format=cl), r.cuda().contiguous(memory_format=cl)
+y = _conv3x3_x6_act(xc, pack_conv3x3_x6(w).cuda(), b.cuda(), rc)
+torch.save(y.cpu(), sys.argv[1])
+"""
+
+
+def test_x6_four_state_form_matches_default(tmp_path):
+    """The opt-in 4-state tower conv (HZ_X6_CS4=1: two 4-wave workgroups per
+    CU, its own tap-class table) gives the default 4-wave form's bits, with a
+    partly filled last workgroup (1003 = 250 x 4 + 3); the form is chosen
+    once per process, so each runs in a process of its own."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "harmonies-alphazero_amd")
+    outs = []
+    for flag in ("0", "1"):
+        path = str(tmp_path / f"cs4_{flag}.pt")
+        env = dict(os.environ, HZ_X6_CS4=flag)
+        subprocess.run([sys.executable, "-c", _CS4_SCRIPT, path, pkg], env=env, check=True, timeout=300)
+        outs.append(torch.load(path, weights_only=True))
+    assert torch.isfinite(outs[0]).all() and torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("batch", [1, 5, 64, 256, 1024])
 def test_resident_tower_matches_layered_tower(batch):
     """hz_tower_x6_resident (small batches: the whole tower in one launch,
