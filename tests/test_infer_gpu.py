@@ -447,6 +447,34 @@ def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):
     assert (fused[:k].cpu().double() - want).abs().max().item() <= 2e-5
 
 
+def test_folded_net_fused_blocks_same_bits():
+    """The whole folded forward with every residual block as one launch
+    (hz_resblock_x6_set_fused(1)) gives the layered forward's logits and
+    values bit for bit (1,100 encoder-like boards: above the resident
+    tower's 1,024, so the layered blocks run; live bound inside a
+    workgroup)."""
+    from hzamd._native import lib
+    g = torch.Generator().manual_seed(12)
+    torch.manual_seed(12)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    n = 1100
+    board = (torch.rand(n, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    board[:, 37] = 2.0 / 3.0
+    glob = torch.rand(n, 42, generator=g).cuda()
+    fnet = FoldedNet(net.cuda())
+    assert n > fnet.resident_max
+    live = torch.tensor([n - 5], dtype=torch.int32, device="cuda")
+    l0, v0 = fnet(board, glob, live=live)
+    assert lib().hz_resblock_x6_set_fused(1) == 0
+    try:
+        assert lib().hz_resblock_x6_fused(n) == 1
+        l1, v1 = fnet(board, glob, live=live)
+    finally:
+        lib().hz_resblock_x6_set_fused(0)
+    assert torch.equal(l0[:n - 5], l1[:n - 5]) and torch.equal(v0[:n - 5], v1[:n - 5])
+
+
 _CS4_SCRIPT = """
 import sys, torch
 sys.path[:0] = [sys.argv[2]]
