@@ -1373,17 +1373,18 @@ static int launch_x6w4(const float *x, const void *wpack6, const float *bias, co
 }
 
 // residual blocks run as one launch (k_conv3x3_x6w4<true>) where the tower
-// conv takes the 4-wave form only with HZ_X6_BLOCK=1: measured at parity with
-// the two layered launches (282.2 vs 284.1 us per block at 4096 rows, same
-// process, tools/block_ab.py; profiles/r03/block): under the chip's power
-// limit the cycles the fused form saves (conv1's epilogue, conv2's setup and
-// HBM staging) came back as a higher clock with slower chunks
+// conv takes the 4-wave form, unless HZ_X6_BLOCK=0: one block alone measures
+// at parity with the two layered launches (282.2 vs 284.1 us, tools/block_ab.py,
+// whose layered convs re-read a cached input), but in the forward chain the
+// intermediate activation's write and re-read are gone: 2.29 vs 2.41 ms per
+// 4096-row forward, 138.4-138.8 vs 132.9-133.6 complete self-play games/s
+// on one box (profiles/r03/block)
 static std::atomic<int32_t> g_x6_block{-1};  // -1: from HZ_X6_BLOCK on first use
 static bool x6_block() {
   int32_t v = g_x6_block.load(std::memory_order_relaxed);
   if (v < 0) {
     const char *e = getenv("HZ_X6_BLOCK");
-    int32_t want = e && atoi(e) == 1 ? 1 : 0, expect = -1;
+    int32_t want = e && atoi(e) == 0 ? 0 : 1, expect = -1;
     g_x6_block.compare_exchange_strong(expect, want);
     v = g_x6_block.load(std::memory_order_relaxed);
   }

@@ -256,9 +256,9 @@ int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias
 int hz_resblock_x6_bias_act(const float *x, const void *w1, const float *b1, const void *w2, const float *b2,
                             float *out, float *tmp, int32_t batch, const int32_t *live, void *stream);
 int32_t hz_resblock_x6_fused(int32_t batch);
-/* on = 1: hz_resblock_x6_bias_act takes the one-launch form where it applies;
- * 0 (the default, unless HZ_X6_BLOCK=1): the two layered convs.  Measured at
- * parity with each other; results are bit-identical. */
+/* on = 1 (the default, unless HZ_X6_BLOCK=0): hz_resblock_x6_bias_act takes
+ * the one-launch form where it applies; 0: the two layered convs (A/B
+ * measurements); results are bit-identical. */
 int hz_resblock_x6_set_fused(int32_t on);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,

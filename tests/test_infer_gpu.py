@@ -415,11 +415,12 @@ def test_resblock_x6_fused_equals_two_layered_convs(batch):
     batch); and stays within fp32 rounding of a float64 block."""
     from hzamd._native import lib
     from hzamd.infer import _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6
+    prev = lib().hz_resblock_x6_fused(4096)
     assert lib().hz_resblock_x6_set_fused(1) == 0
     try:
         _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6)
     finally:
-        lib().hz_resblock_x6_set_fused(0)
+        lib().hz_resblock_x6_set_fused(prev)
 
 
 def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):
@@ -449,8 +450,8 @@ def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):
 
 def test_folded_net_fused_blocks_same_bits():
     """The whole folded forward with every residual block as one launch
-    (hz_resblock_x6_set_fused(1)) gives the layered forward's logits and
-    values bit for bit (1,100 encoder-like boards: above the resident
+    (hz_resblock_x6_set_fused(1), the default) gives the layered forward's
+    logits and values bit for bit (1,100 encoder-like boards: above the resident
     tower's 1,024, so the layered blocks run; live bound inside a
     workgroup)."""
     from hzamd._native import lib
@@ -465,13 +466,15 @@ def test_folded_net_fused_blocks_same_bits():
     fnet = FoldedNet(net.cuda())
     assert n > fnet.resident_max
     live = torch.tensor([n - 5], dtype=torch.int32, device="cuda")
-    l0, v0 = fnet(board, glob, live=live)
-    assert lib().hz_resblock_x6_set_fused(1) == 0
+    prev = lib().hz_resblock_x6_fused(4096)
     try:
+        assert lib().hz_resblock_x6_set_fused(0) == 0
+        l0, v0 = fnet(board, glob, live=live)
+        assert lib().hz_resblock_x6_set_fused(1) == 0
         assert lib().hz_resblock_x6_fused(n) == 1
         l1, v1 = fnet(board, glob, live=live)
     finally:
-        lib().hz_resblock_x6_set_fused(0)
+        lib().hz_resblock_x6_set_fused(prev)
     assert torch.equal(l0[:n - 5], l1[:n - 5]) and torch.equal(v0[:n - 5], v1[:n - 5])
 
 

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from hzamd._native import lib  # noqa: E402
 from hzamd.infer import _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6  # noqa: E402
 
-assert lib().hz_resblock_x6_set_fused(1) == 0  # _resblock_x6 = the one-launch form
+assert lib().hz_resblock_x6_set_fused(1) == 0  # _resblock_x6 = the one-launch form (the default)
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 cl = torch.channels_last
