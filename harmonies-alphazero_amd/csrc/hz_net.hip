@@ -1017,8 +1017,15 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
       for (int cb = 0; cb < NCB; cb++) dst[p][cb] = w[((t2 * NQ + q2) * 3 + p) * 512 + 64 * cb];
   };
-  // chunk 0's loads and the first K-step's B fragments first: the rest of
-  // the setup runs under their latency
+  // the class table's rows first (vmcnt counts loads in issue order: the
+  // setup's wait for them then covers them alone), then chunk 0's loads and
+  // the first K-step's B fragments, under whose latency the setup runs
+  int rtab[kRBT], rtab0[kRBT];
+#pragma unroll
+  for (int rb = 0; rb < kRBT; rb++) {
+    rtab[rb] = kX6ClassRow[rh * kRBT + rb][lane & 15];
+    rtab0[rb] = kX6ClassRow[rh * kRBT + rb][0];
+  }
   stage_issue(0);
   bf16x8 b[3][NCB], bn[3][NCB];
   bissue(b, 0);
@@ -1027,8 +1034,8 @@ __global__ void __launch_bounds__(256, 1)
   uint32_t valid[kRBT];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    int r = kX6ClassRow[rh * kRBT + rb][lane & 15];
-    r = r >= 0 ? r : kX6ClassRow[rh * kRBT + rb][0];  // padding rows read a real row (not stored)
+    int r = rtab[rb];
+    r = r >= 0 ? r : rtab0[rb];  // padding rows read a real row (not stored)
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
     cbase[rb] = r * kX6Cell + 16 * kg;
     uint32_t v = 0;
