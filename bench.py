@@ -59,7 +59,11 @@ MEAN_SELFPLAY_PLIES = 62.4  # mean game length
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher, N > 1 starts N ranks itself. Must equal "
+                         "WORLD_SIZE when a launcher set it")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (RCCL) even at one rank, so the N > 1 collectives run")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--boards", type=int, default=4096)
@@ -104,7 +108,7 @@ def parse():
                     help="self-play network: a model.py-format checkpoint (default: synthesize best_model.pth.tar "
                          "from the torch.manual_seed(0) default net and load it through load_checkpoint)")
     ap.add_argument("--stub", action="store_true",
-                    help="config 4: the deterministic stub evaluator instead of the network (oracle-replay tests)")
+                    help="config 4 only: the deterministic stub evaluator instead of the network (oracle-replay tests)")
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     ap.add_argument("--full-game", action="store_true",
                     help="config 3: time one complete game on every board (games/s measured, not estimated)")
@@ -256,7 +260,7 @@ def bench_loop(args, dev, rank, world):
     tr.execute_self_play_phase(tr.best_model_manager)
     tr.execute_training_phase()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     t0 = time.perf_counter()
     phases = {"self_play": 0.0, "training": 0.0, "evaluation": 0.0}
@@ -286,10 +290,10 @@ def bench_loop(args, dev, rank, world):
         print(f"[config5] iteration {it}: self-play {b - a:.1f}s training {c - b:.1f}s eval {d - c:.1f}s",
               file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     if rank == 0:
         ref = (sims == 400 and args.eval_sims == 200 and args.eval_games == 30 and args.eval_every == 5)
@@ -307,6 +311,8 @@ def bench_loop(args, dev, rank, world):
                        "reference_config": ref, "parallelism": f"shard{world}"},
             "phase_seconds": phases, "games": games, "evaluations": evals,
         }))
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)  # the run's checkpoints and buffer files
 
 
 class TimedEvaluator:
@@ -323,9 +329,14 @@ class TimedEvaluator:
         self.events = []
         self.mcts = None  # attach(): the BatchedMCTS whose searches call this evaluator
         self._base = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._ebase = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.calls = 0
+        self.snap_at = None  # call index whose leaf batch + outputs are kept (device copies) for nn_guard
+        self.snap = None
 
     def attach(self, mcts):
         self.mcts = mcts
+        mcts.count_edges = True  # expansion env steps counted on the device (edges_total)
 
     def __call__(self, board, glob, rows=None, count=None):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -333,16 +344,26 @@ class TimedEvaluator:
         out = self.pred(board, glob, rows, count)
         b.record()
         self.events.append((a, b))
+        if self.calls == self.snap_at:  # after the event pair: not part of the forward's time
+            self.snap = (board.clone(), glob.clone(), None if count is None else count.clone(),
+                         out[0].clone(), out[1].clone())
+        self.calls += 1
         return out
 
     @property
     def rows(self):
         return self.mcts.eval_rows_total - self._base
 
+    @property
+    def edges(self):
+        """Expansion env steps (apply_move per legal child) since reset()."""
+        return self.mcts.edges_total - self._ebase
+
     def reset(self):
         torch.cuda.synchronize()
         self.events.clear()
         self._base = self.mcts.eval_rows_total.clone()
+        self._ebase = self.mcts.edges_total.clone()
 
     def ms(self):
         return sum(a.elapsed_time(b) for a, b in self.events)
@@ -365,20 +386,23 @@ def load_selfplay_model(args, dev):
     from hzamd.manager import ModelManager
     from hzamd.net import DEFAULT
     cfg = dict(REF_TRAIN_CFG, device=str(dev))
-    path = args.checkpoint
-    if path is None:
-        folder = tempfile.mkdtemp(prefix="hz_ckpt_")
-        torch.manual_seed(0)
-        ModelManager(dict(DEFAULT, board_size=(5, 7)), cfg).save_checkpoint(folder=folder,
-                                                                            filename="best_model.pth.tar")
-        path, what = os.path.join(folder, "best_model.pth.tar"), "synthesized best_model.pth.tar " \
-            "(torch.manual_seed(0) default net, model.py:161-182 format)"
-    else:
-        what = f"checkpoint {path}"
     mm = ModelManager(dict(DEFAULT, board_size=(5, 7)), cfg)
-    ok, _ = mm.load_checkpoint(folder=os.path.dirname(os.path.abspath(path)), filename=os.path.basename(path))
-    if not ok:
-        raise SystemExit(f"could not load {path} with ModelManager.load_checkpoint")
+
+    def load(path):
+        ok, _ = mm.load_checkpoint(folder=os.path.dirname(os.path.abspath(path)), filename=os.path.basename(path))
+        if not ok:
+            raise SystemExit(f"could not load {path} with ModelManager.load_checkpoint")
+
+    if args.checkpoint is None:
+        with tempfile.TemporaryDirectory(prefix="hz_ckpt_") as folder:  # removed after the load
+            torch.manual_seed(0)
+            ModelManager(dict(DEFAULT, board_size=(5, 7)), cfg).save_checkpoint(folder=folder,
+                                                                                filename="best_model.pth.tar")
+            load(os.path.join(folder, "best_model.pth.tar"))
+        what = "synthesized best_model.pth.tar (torch.manual_seed(0) default net, model.py:161-182 format)"
+    else:
+        load(args.checkpoint)
+        what = f"checkpoint {args.checkpoint}"
     return mm.model.eval(), what + " loaded by ModelManager.load_checkpoint"
 
 
@@ -416,22 +440,22 @@ def bench_selfplay(args, dev, rank, world):
     for w in range(args.warmup):
         sp.move(w)
     ev.reset()
-    edges = 0
-    if world > 1:
+    if dd():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    moves = []
     for k in range(args.steps):
-        _, v, active = sp.move(args.warmup + k)
-        edges += int(sp.mcts.stats()[:, 1].sum().item())
+        moves.append(sp.move(args.warmup + k)[2].sum())
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     nn_ms = ev.ms()
     rows = int(ev.rows.item())
+    env_steps = int(ev.edges.item()) + int(sum(int(m) for m in moves))  # expansion children + real moves
     sims_done = n * sims * args.steps
-    if world > 1:
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     sims_all = sims_done * world
     per_move = elapsed / args.steps
@@ -446,7 +470,7 @@ def bench_selfplay(args, dev, rank, world):
             "config": {"workload": f"config3: {n} boards x {sims} sims/move, default 128fx8 net",
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
             "games_per_s_est": world * n / (per_move * MEAN_SELFPLAY_PLIES),
-            "env_steps_per_s": (edges + n * args.steps) * world / elapsed,
+            "env_steps_per_s": env_steps * world / elapsed,
             "nn_rows_evaluated": rows, "nn_ms_per_move": nn_ms / args.steps,
             "tree_ms_per_move": per_move * 1e3 - nn_ms / args.steps,
             "nn_tflops": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
@@ -474,7 +498,7 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
         return out
 
     sp.move = move
-    if world > 1:
+    if dd():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -485,7 +509,8 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
     moves = int(rec["valid"].sum().item())
     nn_ms = ev.ms()
     rows = int(ev.rows.item())
-    if world > 1:
+    env_steps = int(ev.edges.item()) + moves
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
     if rank == 0:
         print(json.dumps({
@@ -497,6 +522,7 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
             "config": {"workload": f"config3: {n} boards x {sims} sims/move, one whole game per board",
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
             "plies": rec["plies"], "moves": moves, "sims_per_s": world * moves * sims / elapsed,
+            "env_steps_per_s": world * env_steps / elapsed,
             "nn_rows_evaluated": rows, "nn_rows_skipped": moves * sims - rows, "nn_s": nn_ms * 1e-3,
             "nn_tflops": flops_per_eval() * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
         }))
@@ -534,32 +560,37 @@ def selfplay_probe(args, dev, rank, world):
     sp.keep_noise = True
     sp.noise_log.clear()
     ev.reset()
+    ev.calls, ev.snap_at, ev.snap = 0, sims // 2, None  # the NN guard's leaf batch: mid first timed move
     # -- leg 1: per move at the full leaf batch
     recs = []
-    if world > 1:
+    if dd():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.sp_moves):
         recs.append(sp.move(args.sp_warmup + k))
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     nn_ms = ev.ms()
     rows = int(ev.rows.item())
     board_moves = int(sum(int(a.sum().item()) for _, _, a in recs))
+    env_steps = int(ev.edges.item()) + board_moves  # expansion children + real moves
     noise0 = sp.noise_log[0][0].clone()
     sp.keep_noise = False
     sp.noise_log.clear()
     sims_done = board_moves * sims
-    if world > 1:
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
-        sims_all, rows_all = (int(x) for x in all_reduce([sims_done, rows], dist.ReduceOp.SUM))
+        sims_all, rows_all, env_all = (int(x) for x in all_reduce([sims_done, rows, env_steps], dist.ReduceOp.SUM))
     else:
-        sims_all, rows_all = sims_done, rows
+        sims_all, rows_all, env_all = sims_done, rows, env_steps
     per_move = elapsed / args.sp_moves
     nn_tf = fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None
+    # the network's numerics in the measured run: rows of a timed leaf batch
+    # against the checkpoint's network in float64 on the CPU
+    nn_parity = nn_guard(ev, dev)
     # -- leg 2: complete games (+ config 4's exchange at N > 1)
     game = selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl) if args.sp_games > 0 else None
     # -- leg 3: the parity guard (every rank), with the CPU twin's timing
@@ -573,6 +604,7 @@ def selfplay_probe(args, dev, rank, world):
                            f"per move: {args.sp_warmup} warm-up + {args.sp_moves} timed moves from the game start; "
                            f"complete games: {args.sp_games} whole game(s) on every board",
                "sims_per_s": sims_all / elapsed, "nn_evals_per_s": rows_all / elapsed,
+               "env_steps_per_s_per_move_leg": env_all / elapsed,
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
                "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
                "nn_rows_evaluated": rows, "sims": sims_done,
@@ -588,13 +620,20 @@ def selfplay_probe(args, dev, rank, world):
                                         f"{emu_peak:.1f} TFLOP/s; fp32_mfma_frac is the same figure against the "
                                         f"f32 MFMA's dense peak ({FP32_MFMA_PEAK_TFLOPS} TFLOP/s), which this path "
                                         "does not use"},
-               "dtype": "fp32", "n_gpus": world, "network": ev.network, "parity": guard["parity"]}
+               "dtype": "fp32", "n_gpus": world, "network": ev.network, "parity": guard["parity"],
+               "nn_parity": nn_parity}
         if game is not None:
             out.update({"games_per_s": game["games_per_s"], "games_per_s_basis": game["basis"],
+                        "env_steps_per_s": game["env_steps_per_s"],
+                        "env_steps_basis": "complete-games leg: expansion children (one apply_move per legal "
+                                           "child, MCTS.py:171-177, counted on the device) + real moves, all "
+                                           "ranks, over the slowest rank's time",
                         "game": game})
             out["exchange"] = game.get("exchange")
         else:
-            out.update({"games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
+            out.update({"env_steps_per_s": env_all / elapsed,
+                        "env_steps_basis": "per-move leg: expansion children + real moves",
+                        "games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
                         "games_per_s_basis": f"estimate: ms per move x mean game length {MEAN_SELFPLAY_PLIES} "
                                              "plies (--sp-games 0)", "exchange": None})
         if guard.get("cpu_baseline") is not None:
@@ -626,7 +665,7 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
     plies, moves, t_play, packed = [], 0, 0.0, []
     try:
         for _ in range(args.sp_games):
-            if world > 1:
+            if dd():
                 dist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -635,17 +674,18 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
             t_play += time.perf_counter() - t0
             plies.append(rec["plies"])
             moves += int(rec["valid"].sum().item())
-            if world > 1:
+            if dd():
                 comp = sp.compact(rec)
                 packed.append(hd.pack_records(comp["states"], comp["visits"], comp["z"], comp["player"]))
             del rec
     finally:
         sp.move = orig_move
     nn_ms, rows = ev.ms(), int(ev.rows.item())
+    env_steps = int(ev.edges.item()) + moves  # expansion children + real moves
     exchange = None
-    if world > 1:
+    if dd():
         t_play = all_reduce([t_play], dist.ReduceOp.MAX)[0]
-        moves_all, rows_all = (int(x) for x in all_reduce([moves, rows], dist.ReduceOp.SUM))
+        moves_all, rows_all, env_all = (int(x) for x in all_reduce([moves, rows, env_steps], dist.ReduceOp.SUM))
         own = torch.cat(packed)
         buf = hd.ReplayBuffer(max(1, own.shape[0]) * world, dev)
         torch.cuda.synchronize(dev)
@@ -662,7 +702,7 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
                     "bytes_per_rank_received": nbytes, "ms": xdt * 1e3, "GBps": nbytes / xdt / 1e9,
                     "note": "the complete games' (s, pi, z) records, 336 B each (config 4's exchange)"}
     else:
-        moves_all, rows_all = moves, rows
+        moves_all, rows_all, env_all = moves, rows, env_steps
     if rank != 0:
         return None
     games = world * n * args.sp_games
@@ -670,7 +710,8 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
             "basis": f"complete games: {args.sp_games} whole game(s) on each of the {world} x {n} boards, timed "
                      "end to end (slowest rank)",
             "seconds": t_play, "games": games, "plies_per_game_batch": plies, "moves": moves_all,
-            "sims_per_s": moves_all * sims / t_play, "nn_rows_evaluated": rows_all,
+            "sims_per_s": moves_all * sims / t_play, "env_steps": env_all, "env_steps_per_s": env_all / t_play,
+            "nn_rows_evaluated": rows_all,
             "nn_rows_skipped": moves_all * sims - rows_all, "nn_s_rank0": nn_ms * 1e-3,
             "nn_tflops_rank0": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
             "exchange": exchange}
@@ -729,7 +770,7 @@ def selfplay_guard(roots, active, noise, sims, dev, rank, world, cpu_sample=Fals
         bad = sum(pool.map(check, boards, chunksize=8))
     cpu_dt = time.perf_counter() - t0
     checked = len(boards)
-    if world > 1:
+    if dd():
         bad, checked = (int(x) for x in all_reduce([bad, checked], dist.ReduceOp.SUM))
     assert bad == 0, f"selfplay parity: {bad} of {checked} boards' searches differ from the C twin"
     out = {"parity": f"{checked}/{checked} boards bit-exact vs C twin (first timed move's roots, streams and root "
@@ -771,6 +812,48 @@ def selfplay_guard(roots, active, noise, sims, dev, rank, world, cpu_sample=Fals
     return out
 
 
+NN_GUARD_TOL = 1e-4  # tests/test_infer_gpu.py:38's bound against the float64 network
+
+
+def nn_guard(ev, dev, rows_each=256):
+    """The leaf evaluator's numerics inside the measured run (model.py:81-110):
+    the first and the last `rows_each` live rows of one timed leaf batch
+    (TimedEvaluator.snap: the batch the kernels saw and the probabilities and
+    values they returned) evaluated again by the checkpoint's own network in
+    float64 on the host CPU (softmax over all 143 logits, tanh value, as
+    ModelManager.predict); max |diff| of probabilities and values must be
+    within NN_GUARD_TOL on every rank (all-reduced)."""
+    import copy
+    if ev.snap is None:
+        raise RuntimeError("nn_guard: no leaf batch was kept")
+    board, glob, count, pol, val = ev.snap
+    ev.snap = None
+    k = int(count.item()) if count is not None else board.shape[0]
+    idx = sorted(set(range(min(rows_each, k))) | set(range(max(0, k - rows_each), k)))
+    it = torch.tensor(idx, dtype=torch.long, device=board.device)
+    b64, g64 = board.index_select(0, it).cpu().double(), glob.index_select(0, it).cpu().double()
+    p_gpu, v_gpu = pol.index_select(0, it).cpu().double(), val.reshape(-1).index_select(0, it).cpu().double()
+    net64 = copy.deepcopy(ev.pred.model).cpu().double().eval()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))))
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        logits, v64 = net64(b64, g64)
+    cpu_s = time.perf_counter() - t0
+    torch.set_num_threads(prev)
+    dp = (p_gpu - torch.softmax(logits, 1)).abs().max().item() if idx else 0.0
+    dv = (v_gpu - v64.reshape(-1)).abs().max().item() if idx else 0.0
+    checked = len(idx)
+    if dd():
+        dp, dv = all_reduce([dp, dv], dist.ReduceOp.MAX)
+        checked = int(all_reduce([checked], dist.ReduceOp.SUM)[0])
+    assert dp <= NN_GUARD_TOL and dv <= NN_GUARD_TOL, f"nn guard: max |dp| {dp:.3g}, |dv| {dv:.3g} > {NN_GUARD_TOL}"
+    return {"rows_checked": checked, "live_rows_in_batch": k, "max_abs_dpolicy": dp, "max_abs_dvalue": dv,
+            "tol": NN_GUARD_TOL, "cpu_s": cpu_s,
+            "basis": f"the first and last {rows_each} live rows of one timed leaf batch (mid first timed move) "
+                     "against the loaded network in float64 on the CPU: softmax probabilities and tanh values"}
+
+
 def bench_exchange(args, dev, rank, world):
     """BASELINE config 4: every rank plays `iterations` self-play iterations
     (SelfPlay.iteration: one whole game on each of its 4096 boards, seeded by
@@ -786,7 +869,7 @@ def bench_exchange(args, dev, rank, world):
     sp.env.reset()
     for w in range(min(2, args.warmup)):
         sp.move(w)
-    if world > 1:
+    if dd():
         hd.all_gather_records(torch.zeros(1, hd.RECORD_WORDS, dtype=torch.int64, device=dev))
     torch.cuda.synchronize(dev)
     own, plies = [], []
@@ -796,7 +879,7 @@ def bench_exchange(args, dev, rank, world):
     # test can replay the records with the C twin (tests/test_bench_gpu.py)
     sp.keep_noise = bool(args.records_out)
     sp.noise_log.clear()
-    if world > 1:
+    if dd():
         dist.barrier()
     t0 = time.perf_counter()
     for it in range(args.iterations):
@@ -812,10 +895,10 @@ def bench_exchange(args, dev, rank, world):
         print(f"[config4] iteration {it}: self-play {tm['play_s']:.1f}s exchange {tm['exchange_s'] * 1e3:.1f} ms "
               f"({int(gathered.shape[0])} records)", file=sys.stderr, flush=True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dd():
         elapsed, t_play, t_x = all_reduce([elapsed, t_play, t_x], dist.ReduceOp.MAX)
     if args.records_out:
         log = sp.noise_log
@@ -840,16 +923,54 @@ def bench_exchange(args, dev, rank, world):
                        "boards_per_gpu": n, "sims": sims, "parallelism": f"shard{world}"},
             "self_play_s": t_play, "exchange": {"ms": t_x * 1e3, "records": examples,
                                                 "bytes_per_rank_received": nbytes,
-                                                "GBps": nbytes / t_x / 1e9 if t_x > 0 and world > 1 else None,
+                                                "GBps": nbytes / t_x / 1e9 if t_x > 0 and dd() else None,
                                                 "collective": "all_gather (counts) + all_gather_into_tensor"
-                                                if world > 1 else "none (one rank)"},
+                                                if dd() else "none (one rank)"},
             "examples_per_iteration": examples / args.iterations,
         }))
 
 
+def dd():
+    """True when torch.distributed carries this run's collectives (N > 1, or
+    --dist at N = 1)."""
+    return dist.is_available() and dist.is_initialized()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per
+    GPU) as `torch.distributed.run` children on 127.0.0.1 and exit with their
+    status.  The parent touches no GPU (torch.cuda.device_count() does not
+    initialise one on this image); it only checks that N GPUs are visible."""
+    import subprocess
+    rehearsal = os.environ.get("HZ_BENCH_REHEARSAL") == "1"
+    if not rehearsal and torch.cuda.device_count() < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {torch.cuda.device_count()} GPU(s) visible")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] spawning {n} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd)
+    if r.returncode != 0:
+        print(f"[bench] a rank failed (exit {r.returncode})", file=sys.stderr, flush=True)
+    sys.exit(r.returncode)
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.stub and args.config != 4:
+        raise SystemExit("--stub is config 4's evaluator (oracle-replay runs); pass --config 4")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        spawn_ranks(args.gpus)  # exits
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # HZ_BENCH_REHEARSAL=1 (tests only): ranks share the visible GPUs
@@ -858,15 +979,25 @@ def main():
     rehearsal = os.environ.get("HZ_BENCH_REHEARSAL") == "1"
     if rehearsal:
         local = local % max(1, torch.cuda.device_count())
+    elif world > 1 and local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     global _RED_DEV
     _RED_DEV = "cpu" if rehearsal else dev
-    if world > 1:
+    if world > 1 or args.dist:
+        # --dist at N = 1: a one-rank process group, so the RCCL collectives
+        # of the N > 1 path (records all-gather, parity all-reduce) run
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if rehearsal:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        print(f"[bench] rank {rank}/{world}: process group backend {dist.get_backend()}", file=sys.stderr,
+              flush=True)
     if args.config == 1:
         if world > 1:
             raise SystemExit("config 1 is one game at a time on one GPU")
@@ -874,12 +1005,12 @@ def main():
         return
     if args.config == 5:
         bench_loop(args, dev, rank, world)
-        if world > 1:
+        if dd():
             dist.destroy_process_group()
         return
     if args.config in (3, 4):
         (bench_selfplay if args.config == 3 else bench_exchange)(args, dev, rank, world)
-        if world > 1:
+        if dd():
             dist.destroy_process_group()
         return
 
@@ -917,7 +1048,7 @@ def main():
     steps_t = torch.zeros(T, n, dtype=torch.int32, device=dev)
     first_ep = launches[0]
     first_state = torch.empty(6, n, dtype=torch.int64, device=dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -926,7 +1057,7 @@ def main():
         if i == 0:  # the first timed batch's final states, for the oracle check (a 196 KB copy)
             first_state.copy_(env.export_state())
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     last_ep = launches[0] - 1
@@ -946,7 +1077,7 @@ def main():
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
     longest = int(steps_t.max())
-    if world > 1:
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
         c = all_reduce([timed_steps, timed_games], dist.ReduceOp.SUM)
         env_steps_all, games_all = int(c[0]), int(c[1])
@@ -1001,7 +1132,7 @@ def main():
         if bad:
             print(f"[parity] rank {rank} episode {ep}: boards {bad[:8]} differ from the C oracle", file=sys.stderr)
         bad_boards += len(bad)
-    if world > 1:
+    if dd():
         bad_steps, bad_boards = (int(x) for x in all_reduce([bad_steps, bad_boards], dist.ReduceOp.SUM))
     assert bad_steps == 0 and bad_boards == 0, (bad_steps, bad_boards)
     parity = (f"first batch: {first_steps} env steps == C oracle ({ref_total}); final states of the first and "
@@ -1018,7 +1149,9 @@ def main():
             "metric": "self-play env-steps/sec + games/sec @4096 boards, 1/2/4/8 GPUs; bit-exact vs CPU",
             "value": value,
             "unit": "env-steps/s",
-            "games_per_s": games_per_s,
+            "env_games_per_s": games_per_s,
+            "env_games_basis": "rule-driven env games (config 2, no MCTS) per second; the self-play games/s "
+                               "is selfplay.games_per_s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -1057,7 +1190,7 @@ def main():
         print(json.dumps(out))
     if args.no_selfplay:
         env.close()
-    if world > 1:
+    if dd():
         dist.destroy_process_group()
 
 
@@ -1095,7 +1228,7 @@ def off_compare(env, one_launch, games, args, dev, world):
     for _ in range(2):
         one_launch()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     T = args.steps * args.launches_per_step
     steps_o = torch.zeros(T, env.n, dtype=torch.int32, device=dev)
@@ -1103,11 +1236,11 @@ def off_compare(env, one_launch, games, args, dev, world):
     for i in range(T):
         one_launch(None, games, steps_o[i])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t1
     total = int(steps_o.sum(dtype=torch.int64))
-    if world > 1:
+    if dd():
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
         total = int(all_reduce([total], dist.ReduceOp.SUM)[0])
     env.set_seed_ahead(True)

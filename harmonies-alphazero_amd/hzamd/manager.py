@@ -25,8 +25,11 @@ from .net import HarmoniesNet
 
 
 def _net_cfg(model_config):
+    """The AlphaZeroModel arguments ModelManager passes (model.py:20-29): the
+    head conv filter counts are never passed, so the heads are always 2 / 1
+    filters whatever the config says (model.py:287-288 defaults)."""
     keys = ("input_channels", "cnn_filters", "board_size", "action_size", "global_feature_size",
-            "value_head_hidden_dim", "num_res_blocks", "policy_head_conv_filters", "value_head_conv_filters")
+            "value_head_hidden_dim", "num_res_blocks")
     return {k: model_config[k] for k in keys if k in model_config}
 
 

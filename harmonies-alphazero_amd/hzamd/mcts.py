@@ -52,6 +52,12 @@ class BatchedMCTS:
         self.eval_rows_total = torch.zeros(1, dtype=torch.int64, device=d)  # ... all searches (one add each)
         # k_gather adds each simulation's gathered row count to it (no extra kernel)
         nat.check(L.hz_mcts_set_eval_counter(self._h, nat.ptr(self.eval_rows)), "hz_mcts_set_eval_counter")
+        # count_edges: after each search, its edges (one apply_move per legal
+        # child of every expanded leaf, MCTS.py:171-177; the skipped self-loop
+        # children of :189-194 are not edges) are added on the device to
+        # edges_total (two small launches per search, no host read)
+        self.count_edges = False
+        self.edges_total = torch.zeros(1, dtype=torch.int64, device=d)
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
         self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
 
@@ -224,6 +230,8 @@ class BatchedMCTS:
         NaN priors would have steered PUCT silently): NativeError if one did."""
         from .infer import check_split_timeouts
         self.eval_rows_total += self.eval_rows
+        if self.count_edges:
+            self.edges_total += self.stats()[:, 1].sum(dtype=torch.int64)
         visits = self.result()
         check_split_timeouts(self.device)
         return visits

@@ -1,6 +1,7 @@
 """World-N rehearsal of the training loop (hzamd.trainer.Trainer, BASELINE
 config 5) for tests/test_multirank_gpu.py: launched by torch.distributed.run
-with gloo, every rank on cuda:0 (a one-GPU box).  Each rank writes what it
+with gloo, every rank on cuda:0 (a one-GPU box), or with RCCL at one rank
+(HZ_DIST_BACKEND=nccl).  Each rank writes what it
 ended with: model and best-model weights, replay buffer, history."""
 import os
 import sys
@@ -20,9 +21,13 @@ def main(out, folder):
     from hzamd.trainer import Trainer
     from test_manager_cpu import MODEL_CFG
     from test_trainer_gpu import EVAL, MCTS, TRAIN
-    dist.init_process_group("gloo")
-    rank = dist.get_rank()
     torch.cuda.set_device(0)
+    backend = os.environ.get("HZ_DIST_BACKEND", "gloo")  # "nccl" (RCCL): one rank only on a one-GPU box
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend)
+    rank = dist.get_rank()
     torch.manual_seed(100 + rank)  # ranks start from different weights: the broadcast must fix that
     cfg = {"num_iterations": 2, "num_games_per_iter": 6, "epochs_per_iter": 1, "replay_buffer_size": 1000,
            "checkpoint_folder": os.path.join(folder, "ck"), "replay_buffer_folder": os.path.join(folder, "buf"),
@@ -35,7 +40,7 @@ def main(out, folder):
     torch.save({"model": flat(tr.model_manager.model), "best": flat(tr.best_model_manager.model),
                 "buffer": tr.replay_buffer.records().cpu(),
                 "evals": [h["evaluation"] for h in hist], "examples": [h["self_play"]["examples"] for h in hist],
-                "world": dist.get_world_size()}, f"{out}.rank{rank}.pt")
+                "world": dist.get_world_size(), "backend": dist.get_backend()}, f"{out}.rank{rank}.pt")
     dist.barrier()
     dist.destroy_process_group()
 

@@ -34,11 +34,56 @@ def _torchrun(args, port, timeout=600):
     return r
 
 
-def _single(args, timeout=600):
+def _single(args, timeout=600, env=None):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=timeout, cwd=ROOT)
+                       timeout=timeout, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return r
+
+
+def test_bench_gpus_n_spawns_its_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (the form
+    the driver uses for its N-GPU runs); on this one-GPU box they share it
+    over gloo (HZ_BENCH_REHEARSAL=1)."""
+    env = dict(os.environ, HZ_BENCH_REHEARSAL="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = _single(["--gpus", "2", "--steps", "2", "--warmup", "1", "--launches-per-step", "4", "--no-off-compare",
+                 "--no-selfplay"], env=env)
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "shard2"
+    assert "8192/8192 boards bit-exact vs C oracle" in d["parity"]
+    assert "spawning 2 ranks" in r.stderr
+
+
+def test_bench_rccl_one_rank():
+    """--dist at one rank: the process group is RCCL ("nccl") and the N > 1
+    collectives run on device tensors: the parity all-reduces, and the
+    complete games' records all-gathered (all_gather_into_tensor) into the
+    replay buffer; with one rank the gathered records are the rank's own."""
+    r = _single(["--dist", "--steps", "2", "--warmup", "1", "--launches-per-step", "4", "--no-off-compare",
+                 "--no-cpu-baseline", "--sp-cpu-seconds", "0"] + SMALL_SP)
+    assert "backend nccl" in r.stderr, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 1 and "4096/4096 boards bit-exact" in d["parity"]
+    sp = d["selfplay"]
+    x = sp["exchange"]
+    assert x is not None and x["records"] == x["records_own"] == sp["game"]["moves"]
+    assert x["bytes_per_rank_received"] == x["records"] * 336
+    assert sp["parity"].startswith("256/256 boards bit-exact vs C twin")
+    assert sp["nn_parity"]["rows_checked"] >= 256
+
+
+def test_config4_rccl_one_rank_equals_plain(tmp_path):
+    """Config 4 with the records all-gathered over RCCL at one rank
+    (SelfPlay.iteration -> all_gather_records on device tensors) fills the
+    replay buffer with exactly the records of the run without a process
+    group."""
+    _single(CFG4 + ["--dist", "--records-out", str(tmp_path / "rccl")])
+    _single(CFG4 + ["--records-out", str(tmp_path / "plain")])
+    a = torch.load(tmp_path / "rccl.rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "plain.rank0.pt", weights_only=True)
+    assert a["buffer"].shape[0] > 0 and torch.equal(a["buffer"], b["buffer"]) and torch.equal(a["own"], b["own"])
 
 
 def test_bench_two_ranks_rehearsal():
@@ -74,10 +119,17 @@ def test_bench_single_rank_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in d["cpu_baseline"], k
     assert "4096/4096 boards bit-exact" in d["parity"]
+    assert d["env_games_per_s"] > 0 and "games_per_s" not in d
     sp = d["selfplay"]
-    for k in ("sims_per_s", "games_per_s", "nn_roofline", "tree_ms_per_move", "cpu_baseline", "exchange"):
+    for k in ("sims_per_s", "games_per_s", "nn_roofline", "tree_ms_per_move", "cpu_baseline", "exchange",
+              "env_steps_per_s", "nn_parity"):
         assert k in sp, k
     assert sp["exchange"] is None
+    # env steps: every expansion child plus every real move of the complete games
+    g = sp["game"]
+    assert g["env_steps"] > 5 * g["moves"] and sp["env_steps_per_s"] == g["env_steps_per_s"]
+    assert sp["nn_parity"]["rows_checked"] >= 256 and sp["nn_parity"]["max_abs_dpolicy"] <= 1e-4
+    assert sp["nn_parity"]["max_abs_dvalue"] <= 1e-4
     assert sp["sims"] == 256 * 16 * 2 and 0 < sp["nn_rows_evaluated"] <= sp["sims"]
     assert 0 < sp["nn_roofline"]["frac"] < 1 and sp["nn_roofline"]["fp32_mfma_frac"] > 0
     assert sp["parity"].startswith("256/256 boards bit-exact vs C twin")

@@ -106,3 +106,15 @@ def test_checkpoint_round_trip(tmp_path):
     p0, v0 = a.predict(b[0], g[0])
     p1, v1 = c.predict(b[0], g[0])
     assert p0.shape == (143,) and np.array_equal(p0, p1) and v0 == v1
+
+
+def test_head_filters_in_config_are_ignored_like_the_reference():
+    """The reference's ModelManager never passes the head conv filter counts
+    to AlphaZeroModel (model.py:20-29), so its heads are always 2 / 1 filters
+    (model.py:287-288): a config naming other counts builds the same network
+    and state dict."""
+    mm = ModelManager(dict(MODEL_CFG, policy_head_conv_filters=4, value_head_conv_filters=3), TRAIN_CFG)
+    ref = ModelManager(MODEL_CFG, TRAIN_CFG)
+    a, b = mm.model.state_dict(), ref.model.state_dict()
+    assert list(a) == list(b) and all(a[k].shape == b[k].shape for k in a)
+    assert a["policy_conv.weight"].shape[0] == 2 and a["value_conv.weight"].shape[0] == 1

@@ -15,13 +15,35 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def test_training_loop_two_ranks(tmp_path):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29523",
-           os.path.join(ROOT, "tests", "dist_loop_rehearsal.py"), str(tmp_path / "out"), str(tmp_path / "run")]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+def _loop(tmp_path, tag, nproc, port, backend="gloo"):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tests", "dist_loop_rehearsal.py"), str(tmp_path / tag), str(tmp_path / f"run_{tag}")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, HZ_DIST_BACKEND=backend))
     assert r.returncode == 0, r.stderr[-3000:]
-    a, b = (torch.load(tmp_path / f"out.rank{k}.pt", weights_only=True) for k in (0, 1))
+    return [torch.load(tmp_path / f"{tag}.rank{k}.pt", weights_only=True) for k in range(nproc)]
+
+
+def test_training_loop_rccl_one_rank_equals_gloo(tmp_path):
+    """The loop's collectives on RCCL (one rank: records all-gather on device
+    tensors, weight broadcast, arena all-reduce) end with the same weights,
+    replay buffer and decisions as the same loop over gloo."""
+    (a,) = _loop(tmp_path, "rccl", 1, 29527, "nccl")
+    (b,) = _loop(tmp_path, "gloo", 1, 29529, "gloo")
+    assert a["backend"] == "nccl" and b["backend"] == "gloo"
+    # self-play of both iterations uses the initial best weights: bit-exact
+    assert torch.equal(a["buffer"], b["buffer"]) and a["examples"] == b["examples"]
+    # training runs MIOpen's backward, whose summation order is not fixed run
+    # to run (Adam's steps then move the weights apart by up to ~0.03): the
+    # weights are only checked to be trained and finite
+    for k in ("model", "best"):
+        assert torch.isfinite(a[k]).all() and torch.isfinite(b[k]).all(), k
+    assert a["evals"][1] is not None and b["evals"][1] is not None
+
+
+def test_training_loop_two_ranks(tmp_path):
+    a, b = _loop(tmp_path, "out", 2, 29523)
     assert a["world"] == b["world"] == 2
     assert torch.equal(a["model"], b["model"])
     assert torch.equal(a["best"], b["best"])
