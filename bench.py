@@ -368,6 +368,18 @@ class TimedEvaluator:
     def ms(self):
         return sum(a.elapsed_time(b) for a, b in self.events)
 
+    def call_stats(self):
+        """Per-call forward durations (HIP events, no profiler): the tail of
+        the distribution shows whether slow launches exist outside rocprof."""
+        import numpy as np
+        t = np.array([a.elapsed_time(b) for a, b in self.events])
+        if not t.size:
+            return None
+        q = np.percentile(t, [50, 90, 99, 99.9])
+        return {"calls": int(t.size), "mean_ms": float(t.mean()), "std_ms": float(t.std()), "p50_ms": float(q[0]),
+                "p90_ms": float(q[1]), "p99_ms": float(q[2]), "p999_ms": float(q[3]), "max_ms": float(t.max()),
+                "calls_over_2x_p50": int((t > 2 * q[0]).sum())}
+
 
 REF_TRAIN_CFG = {"optimizer_type": "Adam", "learning_rate": 0.001, "weight_decay": 0.0001,
                  "value_loss_weight": 1.0, "policy_loss_weight": 1.0, "batch_size": 64, "momentum": 0.9,
@@ -681,6 +693,7 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
     finally:
         sp.move = orig_move
     nn_ms, rows = ev.ms(), int(ev.rows.item())
+    nn_calls = ev.call_stats()
     env_steps = int(ev.edges.item()) + moves  # expansion children + real moves
     exchange = None
     if dd():
@@ -714,7 +727,7 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
             "nn_rows_evaluated": rows_all,
             "nn_rows_skipped": moves_all * sims - rows_all, "nn_s_rank0": nn_ms * 1e-3,
             "nn_tflops_rank0": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
-            "exchange": exchange}
+            "nn_call_ms_rank0": nn_calls, "exchange": exchange}
 
 
 def selfplay_guard(roots, active, noise, sims, dev, rank, world, cpu_sample=False, one_core_s=2.0):

@@ -329,6 +329,12 @@ constexpr int kBoardC = 38;                           // encoder board channels 
 constexpr int kX6Zero = 512;                          // bytes of zeros after the cells
 constexpr int kX6Buf = kCS * 35 * kX6Cell + kX6Zero;  // one chunk of 8 states + the zero region
 static_assert(kCS * 35 * kX6Cell % 256 == 0 && kX6Buf % 256 == 0, "zero region and buffers 256-B aligned");
+// padding rows of the class tables read at kX6PadBase + 32 k (+ tap offsets
+// of at most 8 cells either way, + 3 planes): a 256-B-aligned point in the
+// middle of a chunk buffer, in bounds for every form
+constexpr int kX6PadBase = (4 * 35 * kX6Cell) & ~255;
+static_assert(kX6PadBase >= 8 * kX6Cell && kX6PadBase + 256 + 64 * 3 + 8 * kX6Cell <= 8 * 35 * kX6Cell,
+              "padding reads stay inside an 8-state chunk buffer");
 constexpr int kX6SmallMax = 768;                      // batches up to this run one state per workgroup
 constexpr int kX6TinyMax = 256;                       // ... and up to this, 8 waves of 16 channels each
 
@@ -373,28 +379,40 @@ __device__ __forceinline__ void split4(const f32x4 v, uint2 &h, uint2 &m, uint2 
 // (-18.5 % MFMA work).  Blocks 0-8 are row half 0, 9-17 row half 1, each
 // 66 block-taps: 4 interior blocks (9 taps) and 5 edge blocks (6 taps; the
 // corner cells ride in edge blocks whose taps cover theirs).
-// kX6ClassRow: the block's rows as state * 35 + cell (-1: padding row, not
-// stored); kX6ClassTaps: each block's taps (bit t = tap t = (dh + 1) * 3 +
-// dw + 1).  Generated by the grouping in DESIGN.md §3 (k_conv3x3_x6 row).
+// kX6ClassRow: the block's rows as state * 35 + cell (-1 - k: padding row,
+// not stored, that reads LDS bank slot 2k: see kX6PadBase); kX6ClassTaps:
+// each block's taps (bit t = tap t = (dh + 1) * 3 + dw + 1).
+// Bank-conflict-free A reads (round 4): a cell's 224-B stride puts row r's
+// 16-B K slice kg in bank slot (14 r + kg) mod 16, and a ds_read_b128 serves
+// 16 lanes per LDS cycle, lanes {0-3, 12-15} of K slice 2j with lanes {4-11}
+// of K slice 2j + 1 (and the reverse): all 16 slots differ exactly when the
+// block's positions {0-3, 12-15} hold one row of every residue r mod 8 and
+// positions {4-11} another.  Every class has every residue equally often
+// (state s adds 35 s = 3 s mod 8), so each block takes two rows per residue;
+// the corner rows (one per residue) ride in one block of their class with
+// one row per residue of the class (as before), and the 8 padding rows (one
+// per residue) in one interior block.  tools/class_table.py generates this
+// table and checks it (1,584 LDS cycles per chunk and row half pair for the
+// A reads against 3,456 for the round-3 table).
 alignas(16) __constant__ int16_t kX6ClassRow[18][16] = {
-    {8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 22, 23, 24, 25, 26, 43},  // MM
-    {44, 45, 46, 47, 50, 51, 52, 53, 54, 57, 58, 59, 60, 61, 78, 79},  // MM
-    {80, 81, 82, 85, 86, 87, 88, 89, 92, 93, 94, 95, 96, 113, 114, 115},  // MM
-    {116, 117, 120, 121, 122, 123, 124, 127, 128, 129, 130, 131, 148, 149, 150, 151},  // MM
-    {1, 2, 3, 4, 5, 36, 37, 38, 39, 40, 71, 72, 73, 74, 75, 106},  // TM
-    {107, 108, 109, 110, 141, 142, 143, 144, 145, 176, 177, 178, 179, 180, 211, 212},  // TM
-    {29, 30, 31, 32, 33, 64, 65, 66, 67, 68, 99, 100, 101, 102, 103, 134},  // BM
-    {7, 14, 21, 42, 49, 56, 77, 84, 91, 112, 119, 126, 147, 154, 161, 182},  // ML
-    {13, 20, 27, 48, 55, 62, 83, 90, 97, 118, 125, 132, 153, 160, 167, 188},  // MR
-    {152, 155, 156, 157, 158, 159, 162, 163, 164, 165, 166, 183, 184, 185, 186, 187},  // MM
-    {190, 191, 192, 193, 194, 197, 198, 199, 200, 201, 218, 219, 220, 221, 222, 225},  // MM
-    {226, 227, 228, 229, 232, 233, 234, 235, 236, 253, 254, 255, 256, 257, 260, 261},  // MM
-    {262, 263, 264, 267, 268, 269, 270, 271, -1, -1, -1, -1, -1, -1, -1, -1},  // MM
-    {213, 214, 215, 246, 247, 248, 249, 250, 0, 35, 70, 105, 140, 175, 210, 245},  // TM
-    {135, 136, 137, 138, 169, 170, 171, 172, 173, 204, 205, 206, 207, 208, 239, 240},  // BM
-    {241, 242, 243, 274, 275, 276, 277, 278, 34, 69, 104, 139, 174, 209, 244, 279},  // BM
-    {189, 196, 217, 224, 231, 252, 259, 266, 28, 63, 98, 133, 168, 203, 238, 273},  // ML
-    {195, 202, 223, 230, 237, 258, 265, 272, 6, 41, 76, 111, 146, 181, 216, 251},  // MR
+    {8, 9, 10, 11, 16, 17, 18, 19, 44, 53, 46, 23, 12, 45, 22, 15},  // MM
+    {24, 25, 26, 43, 80, 57, 50, 51, 60, 85, 78, 79, 52, 61, 54, 47},  // MM
+    {88, 81, 58, 59, 96, 89, 82, 115, 116, 117, 94, 95, 92, 93, 86, 87},  // MM
+    {120, 113, 114, 123, 128, 121, 122, 131, 148, 157, 158, 151, 124, 149, 150, 127},  // MM
+    {40, 1, 2, 3, 72, 73, 74, 75, 36, 37, 110, 71, 4, 5, 38, 39},  // TM
+    {144, 145, 106, 107, 176, 177, 178, 179, 180, 141, 214, 215, 108, 109, 142, 143},  // TM
+    {32, 33, 66, 67, 64, 65, 138, 99, 100, 101, 102, 103, 68, 29, 30, 31},  // BM
+    {56, 49, 42, 91, 112, 161, 154, 147, 196, 77, 126, 119, 84, 21, 14, 7},  // ML
+    {48, 97, 90, 27, 160, 153, 202, 83, 132, 125, 118, 167, 20, 13, 62, 55},  // MR
+    {152, 129, 130, 155, 184, 185, 162, 163, 164, 197, 190, 183, 156, 165, 166, 159},  // MM
+    {192, 193, 186, 187, 200, 201, 194, 219, 228, 229, 222, 199, 220, 221, 198, 191},  // MM
+    {232, 225, 218, 227, 256, 233, 226, 235, 260, 261, 262, 263, 236, 253, 254, 255},  // MM
+    {264, 257, 234, 267, -1, -2, -3, -4, -5, -6, -7, -8, 268, 269, 270, 271},  // MM
+    {0, 105, 210, 35, 248, 249, 250, 211, 212, 245, 246, 247, 140, 213, 70, 175},  // TM+TL
+    {136, 137, 170, 171, 208, 169, 242, 243, 204, 205, 206, 207, 172, 173, 134, 135},  // BM
+    {104, 209, 34, 139, 240, 241, 274, 275, 276, 277, 278, 279, 244, 69, 174, 239},  // BM+BR
+    {168, 217, 98, 203, 224, 273, 266, 259, 252, 189, 238, 231, 28, 133, 182, 63},  // ML+BL
+    {216, 41, 146, 195, 272, 265, 258, 251, 188, 237, 230, 223, 76, 181, 6, 111},  // MR+TR
 };
 // kX6ClassSel: the block taps some of whose rows (the corner cells) read
 // off the board: only those need the zero-region redirect
@@ -464,14 +482,19 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, CS == 4 ? 
     *(float4 *)(lds + b * kBufT + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..)
+  // staging: float4 f of a chunk = (row sc, channels 4 (f & 7) ..), sc = f >> 3
+  // with bits 0 and 1 swapped: the 16 lanes of an LDS store cycle cover rows
+  // r and r + 2, whose plane slices fall in disjoint bank halves (as
+  // k_conv3x3_x6w4's srow; rows stay within their group of four, so every
+  // row index stays below kRowsT)
   f32x4 stg[kStg];
   int gsrc[kStg], ldst[kStg];
 #pragma unroll
   for (int it = 0; it < kStg; it++) {
     int f = it * kThreads + t;
     f = f < kRowsT * 8 ? f : kRowsT * 8 - 1;
-    const int sc = f >> 3, part = f & 7, s = sc / 35, cell = sc - 35 * s;
+    const int r0 = f >> 3;
+    const int sc = (r0 & ~3) | ((r0 & 1) << 1) | ((r0 >> 1) & 1), part = f & 7, s = sc / 35, cell = sc - 35 * s;
     if constexpr (Stem)  // board element (state, channel 4 part, cell); channel offset added per chunk
       gsrc[it] = (s < ns ? s0 + s : s0 + ns - 1) * (kBoardC * 35) + 4 * part * 35 + cell;
     else
@@ -561,20 +584,26 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, CS == 4 ? 
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
     int r = (rh * kRBT + rb) * 16 + (lane & 15);
+    int pad = -1;  // CS = 8: a padding row (-1 - k) reads anything in bounds at bank slot 2k (kX6ClassRow)
     if constexpr (kClassed) {
       r = class_row(rh * kRBT + rb, lane & 15);
-      r = r >= 0 ? r : class_row(rh * kRBT + rb, 0);  // padding rows read a real row (not stored)
+      if constexpr (CS == 8) {
+        pad = r >= 0 ? -1 : -1 - r;
+        r = r >= 0 ? r : 0;
+      } else {
+        r = r >= 0 ? r : class_row(rh * kRBT + rb, 0);  // CS = 4: padding rows read a real row (not stored)
+      }
     }
     r = r < kRowsT ? r : kRowsT - 1;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
-    cbase[rb] = r * kX6Cell + 16 * kg;
+    cbase[rb] = (pad < 0 ? r * kX6Cell : kX6PadBase + 32 * pad) + 16 * kg;
     uint32_t v = 0;
 #pragma unroll
     for (int tap = 0; tap < 9; tap++) {
       const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
       v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
     }
-    valid[rb] = v;
+    valid[rb] = pad < 0 ? v : 0x1ffu;
   }
   // classed: the epilogue's rows (transposed tiles: lane -> row lane >> 2),
   // read from the table now so that their latency is long hidden
@@ -943,12 +972,21 @@ __global__ void __launch_bounds__(256, 1)
     const int b = t / (kX6Zero / 16), k = t - b * (kX6Zero / 16);
     *(float4 *)(lds + b * kBufT + kZero + 16 * k) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // staging: float4 f of a chunk = (row sc = f >> 3, channels 4 (f & 7) ..);
-  // the addresses are recomputed per use (registers are the constraint here)
+  // staging: float4 f of a chunk = (row sc = srow(f), channels 4 (f & 7) ..);
+  // srow swaps bits 0 and 1 of f >> 3, so that the 16 lanes of each LDS
+  // store cycle (ds_write_b64: 16 contiguous lanes, 32 banks) cover rows r
+  // and r + 2, whose 64-B plane slices fall in disjoint bank halves (rows r,
+  // r + 1 at the 224-B cell stride share a quarter: 2-way conflicts; tools/
+  // class_table.py); the addresses are recomputed per use (registers are the
+  // constraint here)
   f32x4 stg[kW4Stg];
   auto stage_f = [&](int it) {
     const int f = it * 256 + t;
     return f < kRows * 8 ? f : kRows * 8 - 1;
+  };
+  auto srow = [](int f) {
+    const int r = f >> 3;
+    return (r & ~3) | ((r & 1) << 1) | ((r >> 1) & 1);
   };
   const int last_row = s0 * 35 + ns * 35 - 1;  // rows past the batch reread its last one
   // Block: the thread index made opaque per chunk, so the staging addresses
@@ -964,7 +1002,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int it = 0; it < kW4Stg; it++) {
       int f = it * 256 + tt;
       f = f < kRows * 8 ? f : kRows * 8 - 1;
-      const int sc = s0 * 35 + (f >> 3);
+      const int sc = s0 * 35 + srow(f);
       stg[it] = *(const f32x4 *)(x + (size_t)(sc < last_row ? sc : last_row) * 128 + 4 * (f & 7) + 32 * q);
     }
   };
@@ -977,7 +1015,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int it = 0; it < kW4Stg; it++) {
       int f = it * 256 + tt;
       f = f < kRows * 8 ? f : kRows * 8 - 1;
-      stg[it] = *(const f32x4 *)(lds + kE + 16 * f);
+      stg[it] = *(const f32x4 *)(lds + kE + 128 * srow(f) + 16 * (f & 7));
     }
   };
   auto stage_issue_tmp = [&](int half) __attribute__((always_inline)) {
@@ -986,14 +1024,14 @@ __global__ void __launch_bounds__(256, 1)
     for (int it = 0; it < kW4Stg; it++) {
       int f = it * 256 + tt;
       f = f < kRows * 8 ? f : kRows * 8 - 1;
-      stg[it] = *(const f32x4 *)(tmpg + half * kTmpRows * 32 + 4 * f);
+      stg[it] = *(const f32x4 *)(tmpg + half * kTmpRows * 32 + 32 * srow(f) + 4 * (f & 7));
     }
   };
   auto stage_put = [&](int it, int buf) {
     uint2 h, m, l;
     split4(stg[it], h, m, l);
     const int f = stage_f(it);
-    char *d = lds + buf * kBufT + (f >> 3) * kX6Cell + 8 * (f & 7);
+    char *d = lds + buf * kBufT + srow(f) * kX6Cell + 8 * (f & 7);
     *(uint2 *)d = h;
     *(uint2 *)(d + 64) = m;
     *(uint2 *)(d + 128) = l;
@@ -1020,12 +1058,9 @@ __global__ void __launch_bounds__(256, 1)
   // the class table's rows first (vmcnt counts loads in issue order: the
   // setup's wait for them then covers them alone), then chunk 0's loads and
   // the first K-step's B fragments, under whose latency the setup runs
-  int rtab[kRBT], rtab0[kRBT];
+  int rtab[kRBT];
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) {
-    rtab[rb] = kX6ClassRow[rh * kRBT + rb][lane & 15];
-    rtab0[rb] = kX6ClassRow[rh * kRBT + rb][0];
-  }
+  for (int rb = 0; rb < kRBT; rb++) rtab[rb] = kX6ClassRow[rh * kRBT + rb][lane & 15];
   stage_issue(0);
   bf16x8 b[3][NCB], bn[3][NCB];
   bissue(b, 0);
@@ -1034,17 +1069,18 @@ __global__ void __launch_bounds__(256, 1)
   uint32_t valid[kRBT];
 #pragma unroll
   for (int rb = 0; rb < kRBT; rb++) {
-    int r = rtab[rb];
-    r = r >= 0 ? r : rtab0[rb];  // padding rows read a real row (not stored)
+    const int r = rtab[rb] >= 0 ? rtab[rb] : 0;
     const int s = r / 35, cell = r - 35 * s, ch = cell / 7, cw = cell - 7 * ch;
-    cbase[rb] = r * kX6Cell + 16 * kg;
     uint32_t v = 0;
 #pragma unroll
     for (int tap = 0; tap < 9; tap++) {
       const int hh = ch + tap / 3 - 1, ww = cw + tap % 3 - 1;
       v |= (uint32_t)(hh >= 0 && hh < 5 && ww >= 0 && ww < 7) << tap;
     }
-    valid[rb] = v;
+    // a padding row (-1 - k, not stored) reads anything in bounds at bank
+    // slot 2k (its residue in the class table)
+    cbase[rb] = (rtab[rb] >= 0 ? r * kX6Cell : kX6PadBase + 32 * (-1 - rtab[rb])) + 16 * kg;
+    valid[rb] = rtab[rb] >= 0 ? v : 0x1ffu;
   }
   auto aoff = [&](int rb, int tap) -> int {
     const int d = ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
@@ -1441,7 +1477,7 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
   if (!x || !w1 || !b1 || !w2 || !b2 || !out || !tmp || batch < 0) return -1;
   if (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)out | (uintptr_t)tmp) & 15) return -1;
   if (batch == 0) return 0;
-  if (batch > x6_tiny_max() && batch > x6_small_max() && x6_w4() && x6_block())
+  if (hz_resblock_x6_fused(batch))
     return launch_x6w4<true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp);
   const int rc = launch_x6<4, false>(x, w1, b1, nullptr, tmp, batch, live, stream);
   return rc ? rc : launch_x6<4, false>(tmp, w2, b2, x, out, batch, live, stream);
@@ -1455,9 +1491,13 @@ extern "C" int hz_resblock_x6_set_fused(int32_t on) {
   return 0;
 }
 
-// 1 when hz_resblock_x6_bias_act runs batch rows as one launch
+// 1 when hz_resblock_x6_bias_act runs batch rows as one launch.  The fused
+// kernel's scratch is a [2][288][32]-float slice per 8-state group in tmp,
+// which the ABI sizes batch x 35 x 128 floats: the fused form is taken only
+// when the slices fit (any batch > 4; the default routing needs > 768)
 extern "C" int32_t hz_resblock_x6_fused(int32_t batch) {
-  return batch > x6_tiny_max() && batch > x6_small_max() && x6_w4() && x6_block() ? 1 : 0;
+  const bool fits = (int64_t)((batch + kCS - 1) / kCS) * 2 * 288 * 32 <= (int64_t)batch * 35 * 128;
+  return fits && batch > x6_tiny_max() && batch > x6_small_max() && x6_w4() && x6_block() ? 1 : 0;
 }
 
 extern "C" int hz_stem3x3_x6_bias_act(const float *board, const void *wpack6, const float *bias, float *out,

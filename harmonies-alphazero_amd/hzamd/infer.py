@@ -134,7 +134,9 @@ def check_split_timeouts(device=None):
     if device is not None:
         device = torch.device(device)
         if device.index is None:
-            device = torch.device("cuda", torch.cuda.current_device())
+            # "cuda" without an index (a ModelManager's training_config device)
+            # may name a model on any GPU: check every device with launches
+            device = None
     if not _SPLIT_PENDING or (device is not None and device not in _SPLIT_PENDING):
         return
     if device is None:

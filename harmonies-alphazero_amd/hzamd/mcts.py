@@ -139,7 +139,15 @@ class BatchedMCTS:
         the evaluator's kernels, expand + backup): replaying it costs one
         launch instead of ~60.  Noise is passed as NULL: the kernel reads it
         only when it expands the root, which the first (eager) simulation does
-        (hz_mcts.hip k_expand_backup: noisy = leaf == 0 && !testing && noise)."""
+        (hz_mcts.hip k_expand_backup: noisy = leaf == 0 && !testing && noise).
+
+        Replay constraint: the graph bakes in the split tower's counter block
+        of its capture stream, and capture streams come from PyTorch's stream
+        pool, so two handles may share one block.  Replays of captured
+        simulations must therefore run one at a time (search() replays on the
+        caller's stream, in order); replaying two handles' graphs
+        concurrently on different streams would corrupt the hand-off
+        counters."""
         g = torch.cuda.CUDAGraph()
         if self._capture_stream is None:
             self._capture_stream = torch.cuda.Stream(self.device)

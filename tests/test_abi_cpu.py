@@ -57,3 +57,17 @@ def test_object_roundtrip():
     for v in f["states"][::37]:
         g = apply_ref_to_object(v, G())
         assert (ref_from_object(g) == v).all()
+
+
+def test_tower_class_table_is_bank_conflict_free():
+    """csrc/hz_net.hip's kX6ClassRow equals tools/class_table.py's generated
+    table, whose A-fragment ds_read_b128s (every tap, plane and row block of
+    a chunk, the corner rows' zero-region redirects and the padding rows'
+    wildcard reads included) and staging stores take exactly the
+    conflict-free LDS cycles (MI355X_MICROARCH.md's lane groups and banks)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "class_table.py")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "source table equals it" in r.stdout and "(1584, 1584)" in r.stdout
