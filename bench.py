@@ -47,7 +47,9 @@ BYTES_PER_RESET = 2564     # 624x4 B MT init + idx + 64 B state
 BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
-PIPELINE_DEPTH = 4         # hz_play launches until every board replays a fully prepared episode
+# hz_play launches until every board replays a fully prepared episode, by
+# pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's seven stages)
+PIPELINE_DEPTH = {1: 4, 2: 7}
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 X6_PRODUCTS = 6                # bf16 MFMAs per fp32 product block in the x6 kernels
@@ -67,6 +69,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--boards", type=int, default=4096)
+    ap.add_argument("--pipeline", type=int, choices=(1, 2), default=1,
+                    help="config 2: hz_play's pipeline (1 = chance-ahead k_rollout, 2 = k_play2's seven stages; "
+                         "identical results)")
     ap.add_argument("--launches-per-step", type=int, default=256,
                     help="config 2: hz_play launches (4096-board batches) per bench step")
     ap.add_argument("--seed-base", type=int, default=0)
@@ -1032,6 +1037,8 @@ def main():
 
     n, L = args.boards, args.launches_per_step
     env = BatchedEnv(n, seed_base=args.seed_base + rank * n, device=dev)
+    env.set_pipeline(args.pipeline)
+    kname = "k_play2" if args.pipeline == 2 else "k_rollout"
     games = torch.zeros(n, dtype=torch.int32, device=dev)
     steps = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -1050,7 +1057,7 @@ def main():
     first_steps = int(steps.sum().item())
     # the chance-ahead pipeline (seed -> draw1 -> draw2 -> play) is primed
     # after three launches; warm-up is at least that many
-    prime = max(0, PIPELINE_DEPTH - args.warmup * L)
+    prime = max(0, PIPELINE_DEPTH[args.pipeline] - args.warmup * L)
     for _ in range(max(0, args.warmup * L - 1) + prime):
         one_launch()
     torch.cuda.synchronize(dev)
@@ -1101,7 +1108,8 @@ def main():
     games_per_s = games_all / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
 
-    # roofline of the dominant kernel (hz_play = k_rollout with reset), per launch
+    # roofline of the dominant kernel (hz_play = k_rollout with reset, or
+    # k_play2), per launch
     alg_bytes = (timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET) / T
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
@@ -1181,15 +1189,20 @@ def main():
                        "games_per_step": timed_games / args.steps, "parallelism": f"shard{world}"},
             "roofline": {"bound": "latency (per-lane chains)", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "kernel_ms": kern_ms, "kernel_ms_launches": K,
+                         "kernel": kname, "kernel_ms": kern_ms, "kernel_ms_launches": K,
                          "alg_bytes_per_launch": alg_bytes, "issue_bound": issue,
                          "bound_note": "priced against HBM (peak 8 TB/s), but the launch is bound by its serial "
                                        "per-lane chains (a board's whole game, a stream's seeding): counter "
                                        "traffic is below the algorithmic bytes, see issue_bound and DESIGN.md §3"},
-            "chance_ahead": {"on": True, "note": "each hz_play also prepares every board's next three episodes "
-                                                 "as a pipeline on the other CUs (stream seeding, pile draws and "
-                                                 "rule hashes, none of which depends on moves); steady state: one "
-                                                 "preparation per game in the timed region",
+            "chance_ahead": {"on": True, "pipeline": args.pipeline,
+                             "note": ("each hz_play also prepares every board's next three episodes as a pipeline "
+                                      "on the other CUs (stream seeding, pile draws and rule hashes, none of which "
+                                      "depends on moves); steady state: one preparation per game in the timed region"
+                                      if args.pipeline == 1 else
+                                      "k_play2: each hz_play runs seven stages on seven consecutive episodes of every "
+                                      "board (seeding pass 1, pass 2, draws 0-7, 8-15, 16-23 + rule hashes, plies "
+                                      "0-39, the rest + scoring); steady state: one episode's worth of every stage per "
+                                      "call, i.e. one game per board per call"),
                              "pipeline_prime": prime,
                              "value_off": (off_steps / off_elapsed) if off_steps else None,
                              "ms_per_step_off": (off_elapsed * 1000.0 / args.steps) if off_steps else None},
@@ -1236,8 +1249,9 @@ def encoder_roofline(dev, n, seed_base):
 
 def off_compare(env, one_launch, games, args, dev, world):
     """Time the same workload with chance-ahead off (every launch seeds and
-    draws in-kernel); returns (env steps of all ranks, max elapsed)."""
+    draws in-kernel; pipeline 1); returns (env steps of all ranks, max elapsed)."""
     env.set_seed_ahead(False)
+    env.set_pipeline(1)
     for _ in range(2):
         one_launch()
     torch.cuda.synchronize(dev)
@@ -1257,6 +1271,9 @@ def off_compare(env, one_launch, games, args, dev, world):
         elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
         total = int(all_reduce([total], dist.ReduceOp.SUM)[0])
     env.set_seed_ahead(True)
+    env.set_pipeline(args.pipeline)
+    for _ in range(PIPELINE_DEPTH[args.pipeline]):  # (refill before anything else times this env)
+        one_launch()
     return total, elapsed
 
 

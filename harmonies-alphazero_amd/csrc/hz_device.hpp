@@ -598,6 +598,98 @@ __device__ __forceinline__ void mt_seed_tab(uint32_t *w, const uint32_t *tab, ui
   w[0] = 0x80000000U;
 }
 
+// init_by_array (random.seed) split at its pass boundary, the stream word-
+// major in global memory (word i of the board at w[i * ns]), so that the
+// chain's wave issues no LDS operation (hz_play's second pipeline, hz_env.hip
+// "pipeline 2"): pass 1 leaves mt[1] (the 624th iteration's value) and
+// mt[2..623] as pass 2 reads them; pass 2 finishes the array (cursor
+// kMTSeeded).  The two together write exactly mt_seed's words.
+__device__ __forceinline__ void mt_seed_pass1_g(uint32_t* __restrict__ w, size_t ns, uint64_t seed) {
+  const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  const uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
+  uint32_t prev = 19650218u, m1 = 0;
+  for (int g = 1; g < kMT - 7; g += 8) {  // i = 1..616
+    uint32_t iv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[g + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      if (u || g > 1) w[(size_t)(g + u) * ns] = v;
+      else m1 = v;
+      prev = v;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // i = 617..623
+    const uint32_t v = (kInitGen.v[617 + u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(size_t)(617 + u) * ns] = v;
+    prev = v;
+  }
+  // mt[0] = mt[623]; the 624th iteration at i = 1 (key j = 623 % keylen -> kB)
+  w[ns] = (m1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+}
+template <int PF = 16>
+__device__ __forceinline__ void mt_seed_pass2_g(uint32_t* __restrict__ w, size_t ns) {
+  const uint32_t first1 = w[ns];
+  uint32_t prev = first1;
+  uint32_t ring[PF];  // pass-1 words PF iterations ahead
+#pragma unroll
+  for (int u = 0; u < PF; u++) ring[u] = w[(size_t)(2 + u) * ns];
+  constexpr int kFull = 2 + ((kMT - 2) / PF) * PF;
+  for (int g = 2; g < kFull; g += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      const uint32_t cur = ring[u];
+      const int nx = g + PF + u;
+      ring[u] = nx < kMT ? w[(size_t)nx * ns] : 0u;
+      const uint32_t v = (cur ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
+      w[(size_t)(g + u) * ns] = v;
+      prev = v;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < (kMT - 2) % PF; u++) {
+    const uint32_t v = (ring[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(kFull + u);
+    w[(size_t)(kFull + u) * ns] = v;
+    prev = v;
+  }
+  w[ns] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
+  w[0] = 0x80000000U;
+}
+// rows [0, rows) of a seeded stream (rows <= 227: every source still old)
+// twisted in place, the next generation's start: the stream afterwards has
+// cursor 0 | rows << 16 (kMTAhead for rows = kAheadTwist)
+__device__ __forceinline__ void mt_pretwist_g(uint32_t* __restrict__ w, size_t ns, int rows) {
+  constexpr int B = 8;
+  for (int i0 = 0; i0 < rows; i0 += B) {
+    uint32_t cur[B + 1], far[B];
+#pragma unroll
+    for (int j = 0; j <= B; j++) cur[j] = w[(size_t)(i0 + j) * ns];
+#pragma unroll
+    for (int j = 0; j < B; j++) far[j] = w[(size_t)(i0 + j + 397) * ns];
+#pragma unroll
+    for (int j = 0; j < B; j++)
+      if (i0 + j < rows) w[(size_t)(i0 + j) * ns] = twist_word(cur[j], cur[j + 1], far[j]);
+  }
+}
+
+// A board's stream in global memory with a runtime word stride (a pipeline-2
+// stream slot, word-major: stride = the slot's row length).  As MTS.
+struct MTR {
+  uint32_t* w;
+  int stride, pos, tw;
+  __device__ __forceinline__ MTR(uint32_t* words, int s, int cursor)
+      : w(words), stride(s), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
+  __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
+  __device__ __forceinline__ void prefetch() {}
+  __device__ __forceinline__ uint32_t next() {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    if (pos >= tw) tw += twist_block(w, stride, tw);
+    return temper(w[(size_t)(pos++) * stride]);
+  }
+};
+
 template <class M>
 __device__ __forceinline__ uint32_t randbelow(M& m, uint32_t n) {
   if (!n) return 0;
@@ -761,6 +853,37 @@ __device__ __forceinline__ void sample3_raw(LdsMT& m, uint32_t n, int k, uint32_
   }
   j[0] = j0; j[1] = j1; j[2] = j2;
   if (got < k) sample3_serial(m, n, k, j, got);  // window exhausted (rare)
+}
+
+// A window of a pre-twisted stream in LDS: rows [0, lim) only (hz_env.hip's
+// pipeline-2 draw stages, three windows side by side).  Reads never twist:
+// past the window next() returns 0, and the caller discards any draw whose
+// cursor ends past lim (its picks depend only on the words it consumed, all
+// below the cursor).  The scan reads rows up to pos + 23, in bounds while
+// pos <= lim.
+struct WinMT : LdsMT {
+  int lim;
+  __device__ __forceinline__ WinMT(int l, int cursor, int rows) : LdsMT(l, cursor), lim(rows) {}
+  __device__ __forceinline__ void prefetch() {}
+  __device__ __forceinline__ uint32_t next() {
+    const int i = pos++;
+    return i < lim ? temper(hz_lds[i * kLdsStride + lane]) : 0u;
+  }
+};
+__device__ __forceinline__ void sample3_raw(WinMT& m, uint32_t n, int k, uint32_t j[3]) {
+  if (k != 3) {
+    sample3_serial(m, n, k, j, 0);
+    return;
+  }
+  uint32_t j0, j1, j2;
+  int got;
+  LdsMT& lm = m;
+  if (__all(n > 21)) got = scan3<false, false>(lm, n, j0, j1, j2);
+  else if (__all(n <= 21)) got = scan3<false, true>(lm, n, j0, j1, j2);
+  else if (n > 21) got = scan3<false, false>(lm, n, j0, j1, j2);
+  else got = scan3<false, true>(lm, n, j0, j1, j2);
+  j[0] = j0; j[1] = j1; j[2] = j2;
+  if (got < k) sample3_serial(m, n, k, j, got);
 }
 
 // _draw_tiles(3) (harmonies_engine.py:120-130): flat_bag follows the bag's

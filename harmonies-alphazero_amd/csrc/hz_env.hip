@@ -49,6 +49,24 @@ struct hz_env {
   // materialize(), before any other entry point that reads streams)
   int32_t *mt_src;           // [n]
   int lazy;                  // some board may have mt_src >= 0
+  // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
+  // spread over seven consecutive hz_play calls, one stage per call
+  int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
+  int calls2, primed2;
+  uint32_t *p2_s[8];         // [624][nrow] streams: seeded (pass 1, then 2), rows [0, 224) pre-twisted
+  int32_t *p2_s_tag[8];      // [nrow] episode * 4 + 1 (pass 1 done) / + 2 (seeded, pre-twisted)
+  int32_t *p2_d_tag[7];      // draw hand-offs AB[2], BC[2], PL[3]: [nrow] episode * 4 + stage
+  int32_t *p2_d_k[7];        // [nrow] draws done
+  uint64_t *p2_d_q[7];       // [4][nrow] the script so far
+  uint64_t *p2_d_bag[7];     // [nrow] bag fields after those draws
+  int32_t *p2_d_cur[7];      // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
+  int32_t *p2_m_tag[2];      // playA -> playB: [nrow] episode
+  uint64_t *p2_m_st[2];      // [6][nrow] state after the first kP2Half plies
+  uint64_t *p2_m_q[2];       // [4][nrow] the rest of the script
+  int32_t *p2_m_i[2];        // [3][nrow] script entries used, plies played, stream cursor if fell (else -1)
+  uint32_t *p2_h[3];         // [kRulePlies][nrow] rule hashes
+  int32_t *p2_h_tag[3];      // [nrow] episode
+  int32_t *p2_ep[2];         // [n] episode counter each board ended the call with
 };
 
 #ifdef HZ_DIAG
@@ -1058,6 +1076,566 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #endif
 }
 
+// ============================================================= pipeline 2
+// hz_play's second pipeline (hz_env_set_pipeline(e, 2)).  Each of
+// k_rollout's roles runs one serial per-board chain of ~60 k cycles (a whole
+// game, a whole seeding, 16 pile draws), and a launch lasts as long as its
+// longest chain.  Here every board's episode is cut into seven stages of
+// about half that, one per consecutive hz_play call, and one launch runs all
+// seven stages at once, each on a different episode of the board:
+//   seed blocks [2 nblk, 3 nblk): wave 0 P1 (init_by_array's pass 1,
+//     episode ep + 6), wave 1 P2 (pass 2 and the next generation's first 224
+//     words twisted, episode ep + 5), straight into the episode's stream slot
+//     in HBM (word-major: no LDS operation in either chain);
+//   draw blocks [nblk, 2 nblk): waves 0-2 the draw stages A (draws 0-7,
+//     episode ep + 4), B (8-15, ep + 3), C (16-23, ep + 2), each on its own
+//     LDS window of its episode's pre-twisted stream (rows [0, 192)); wave 3
+//     the rule hashes of episode ep + 2;
+//   play blocks [0, nblk): wave 1 playA (plies [0, 40) of episode ep + 1
+//     from its pile script), wave 0 playB (the rest of episode ep, final
+//     scoring, the board's state, cursor and counters).
+// ep = the episode counter the previous call left (p2_ep).  A stage uses an
+// input only when its tag names the stage's episode, so a wrong prediction
+// costs time, never results: the stages skip the board and playB plays its
+// whole game from scratch (seeding and drawing in LDS, like k_rollout's
+// unprepared boards).  In steady state a call seeds, draws and plays one
+// episode's worth per board: the work of one call is one game per board,
+// spread over seven episodes.  The results are k_rollout's: the board ends
+// the call with episode ep's final state, cursor and counters, and
+// games_done / steps_done count that game (its first plies ran one call
+// earlier, in playA).
+constexpr int kP2Win = 192;   // draw stages' LDS window rows (a draw reads <= 24 words past its cursor)
+constexpr int kP2Half = 40;   // playA's plies: five turn pairs
+constexpr int kP2Stream = 8;  // stream slots: written at call c (P1), used through c + 6, read by materialize
+constexpr int kP2MinPlies = 96;  // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
+// the windows fit the block's LDS, and a scan from a cursor <= kP2Win (rows
+// up to kP2Win + 23 past the last window's base) stays inside it
+static_assert(kP2Win <= kAheadTwist && (2 * kP2Win + kP2Win + 24) * kLdsStride * 4 <= (int)kResetLds, "windows fit");
+
+struct P2Draw {        // a draw stage's output / the play stages' pile script, per board
+  int32_t *tag;        // [nrow] episode * 4 + stage (1 A, 2 B, 3 C)
+  int32_t *k;          // [nrow] draws done
+  uint64_t *q;         // [4][nrow] the script: draw i at bits 9 i ..
+  uint64_t *bag;       // [nrow] bag fields (misc layout) after the draws
+  int32_t *cur;        // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
+};
+
+struct P2Args {
+  uint64_t *st;
+  uint32_t *mt;
+  int32_t *pos, *ply, *episode;
+  uint64_t *seed;
+  int n, max_plies, draws;
+  uint64_t seed_base;
+  long nrow;
+  int32_t *games_done, *steps_done, *mt_src;
+  const int32_t *ep_in;
+  int32_t *ep_out;
+  uint32_t *s_mt[7];   // stream slot of stage s (0 P1, 1 P2, 2-4 draws A-C, 5 playA, 6 playB)
+  int32_t *s_tag[7];
+  int s_idx6;          // playB's slot index (materialize: mt_src = 2 + index)
+  P2Draw ab_w, ab_r, bc_w, bc_r, pl_w, pl_a, pl_b;
+  int32_t *m_tag_w, *m_i_w;
+  const int32_t *m_tag_r, *m_i_r;
+  uint64_t *m_st_w, *m_q_w;
+  const uint64_t *m_st_r, *m_q_r;
+  uint32_t *h_w;
+  const uint32_t *h_a, *h_b;
+  int32_t *h_tag_w;
+  const int32_t *h_tag_a, *h_tag_b;
+};
+
+// PlayDraw for the prepared stages: the pile script in registers, then (a
+// script shorter than the game needs) the episode's stream slot in HBM
+struct PlayDraw2 {
+  uint64_t q0, q1, q2, q3;
+  int d, nd;
+  bool fell;
+  MTR gm;
+  __device__ __forceinline__ uint32_t pop() {
+    uint32_t p9 = (uint32_t)q0 & 0x1FFu;
+    q0 = (q0 >> 9) | (q1 << 55);
+    q1 = (q1 >> 9) | (q2 << 55);
+    q2 = (q2 >> 9) | (q3 << 55);
+    q3 >>= 9;
+    d++;
+    return p9;
+  }
+  __device__ __forceinline__ bool pair_pops() const { return d + 2 <= nd; }
+  __device__ __forceinline__ uint32_t draw_one(uint64_t misc) {
+    if (d < nd) return pop();
+    fell = true;
+    uint32_t p9;
+    return draw_pile(misc, gm, p9) ? p9 : 0x1FFu;
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t misc) { return take(misc, true); }
+  __device__ __forceinline__ uint32_t take(uint64_t misc, bool want) {
+    if (__all(!want || d < nd)) {
+      uint32_t p9 = want ? (uint32_t)q0 & 0x1FFu : 0x1FFu;
+      uint64_t n0 = (q0 >> 9) | (q1 << 55), n1 = (q1 >> 9) | (q2 << 55), n2 = (q2 >> 9) | (q3 << 55);
+      q0 = want ? n0 : q0;
+      q1 = want ? n1 : q1;
+      q2 = want ? n2 : q2;
+      q3 = want ? q3 >> 9 : q3;
+      d += want ? 1 : 0;
+      return p9;
+    }
+    return want ? draw_one(misc) : 0x1FFu;
+  }
+  __device__ __forceinline__ void scripted_reset(State &s) {  // >= 5 entries: the opening piles
+    s.pl[0] = s.pl[1] = s.pl[2] = s.pl[3] = 0;
+    uint64_t open = q0 & ((1ull << 45) - 1);
+    s.piles = open | (5ull << 45);
+    uint64_t misc = 0x1FF;
+#pragma unroll
+    for (int t = 0; t < 6; t++) misc = set_bits(misc, 11 + 5 * t, 5, (uint64_t)initial_count(t));
+#pragma unroll
+    for (int i = 0; i < 5; i++) apply_pile_fast(misc, (uint32_t)(open >> (9 * i)) & 0x1FFu);
+    s.misc = misc;
+    q0 = (q0 >> 45) | (q1 << 19);
+    q1 = (q1 >> 45) | (q2 << 19);
+    q2 = (q2 >> 45) | (q3 << 19);
+    q3 >>= 45;
+    d = 5;
+  }
+};
+
+// the rule policy's plies [g, g_end) of one board (k_rollout's ply loop, no
+// reset, no recording): turn pairs while the wave allows, single plies
+// otherwise; hashes from a pipeline slot when `hs` (row stride nr) holds the
+// episode's, else computed.  Returns the plies played.
+template <class Draw>
+__device__ __forceinline__ int p2_plies(State &s, Draw &draw, int g, int g_end, uint64_t rkey, const uint32_t *hs,
+                                        size_t nr) {
+  const int g0 = g;
+  auto hash = [&](int ply) -> uint32_t { return hs && ply < kRulePlies ? hs[(size_t)ply * nr] : rule_h32(rkey, ply); };
+  while (g < g_end) {
+    if (phase_of(s.misc) == PH_OVER) break;
+    if (__all(g + 8 <= g_end && turn_pair_safe(s))) {
+      uint32_t h[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) h[j] = hash(g + j);
+      int done = 4;
+      if (__all(draw.pair_pops())) {
+        play_turn_h<0, Draw, true>(s, draw, h[0], h[1], h[2], h[3]);
+        if (phase_of(s.misc) != PH_OVER) {
+          play_turn_h<1, Draw, true>(s, draw, h[4], h[5], h[6], h[7]);
+          done = 8;
+        }
+      } else {
+        play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
+        if (phase_of(s.misc) != PH_OVER) {
+          play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
+          done = 8;
+        }
+      }
+      g += done;
+      continue;
+    }
+    const int a = rule_action(s, hash(g));
+    if (a < 0) break;  // stuck board (unreachable from HarmoniesGameState())
+    step_trusted<true>(s, a, draw);
+    g++;
+  }
+  return g - g0;
+}
+
+// P2 in LDS: pass 2 is a serial chain whose every step reads the next
+// pass-1 word, too close ahead for an HBM round trip (pass 2 straight from
+// the slot took ~100 k cycles), so the seed block's LDS holds the 64 streams
+// ([624][65]): wave 2 stages the pass-1 words in row order ahead of the
+// chain (s_in: rows [0, s_in) present), wave 1 runs pass 2 and the
+// pre-twist in LDS (s_out: rows [2, s_out) final; kMT + 1 once all are),
+// wave 3 stores the final rows [kAheadTwist, kMT) back as they come, and
+// after the pre-twist waves 2 and 3 store rows [0, kAheadTwist).  A wave's
+// LDS operations execute in order, so a counter stored after its rows is
+// seen after them (SeedProgress's reasoning); readers load with acquire.
+struct P2Flags {
+  int in, out;
+};
+__device__ __forceinline__ int p2_wait(int *flag, int need) {
+  int v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // every publisher reaches kMT + 1 (or kMT rows); the bound only guards
+  // against a hang should that ever change
+  for (int spin = 0; v < need && spin < (1 << 22); spin++) {
+    __builtin_amdgcn_s_sleep(1);
+    v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return v;
+}
+__device__ __forceinline__ void p2_publish(int *flag, int v) {
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// rows [r0, r1) of the block's 64 boards between LDS [row][65] and the slot
+// (16-B accesses, four boards of a row per lane: a wave covers four rows)
+template <bool ToLds>
+__device__ __forceinline__ void p2_rows(uint32_t *__restrict__ slot, size_t nr, int b0, int lane, int r0, int r1) {
+  constexpr int U = 16;
+  const int c4 = (lane & 15) * 4;
+  for (int q0 = r0; q0 < r1; q0 += 4 * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int r = q0 + 4 * u + (lane >> 4);
+      if (r < r1) {
+        if (ToLds) {
+          v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+        } else {
+          const uint32_t *d = hz_lds + r * kLdsStride + c4;
+          v[u] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int r = q0 + 4 * u + (lane >> 4);
+      if (r < r1) {
+        if (ToLds) {
+          uint32_t *d = hz_lds + r * kLdsStride + c4;
+          d[0] = v[u].x;
+          d[1] = v[u].y;
+          d[2] = v[u].z;
+          d[3] = v[u].w;
+        } else {
+          *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v[u];
+        }
+      }
+    }
+  }
+}
+
+// pass 2 of init_by_array on the lane's LDS column, waiting for staged rows
+// (f.in) and publishing final ones (f.out every 32 rows); then the pre-twist
+__device__ __forceinline__ void p2_pass2_lds(int lane, P2Flags &f) {
+  uint32_t *w = hz_lds + lane;
+  constexpr int S = kLdsStride;
+  int have = p2_wait(&f.in, 18);
+  const uint32_t first1 = w[1 * S];
+  uint32_t prev = first1;
+  uint32_t cur[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) cur[u] = w[(2 + u) * S];
+  for (int g = 2; g < kMT - 6; g += 8) {  // i = 2..617
+    if (g + 16 > have) have = p2_wait(&f.in, g + 16 < kMT ? g + 16 : kMT);
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = w[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
+      w[(g + u) * S] = v;
+      prev = v;
+    }
+    if (((g + 8) & 31) == 2) p2_publish(&f.out, g + 8);
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 6; u++) {  // i = 618..623
+    const uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(618 + u);
+    w[(618 + u) * S] = v;
+    prev = v;
+  }
+  w[1 * S] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
+  w[0] = 0x80000000U;
+  p2_publish(&f.out, kMT);  // rows [kAheadTwist, kMT) final (the pre-twist rewrites only rows below)
+  mt_pretwist_g(w, (size_t)S, kAheadTwist);
+  p2_publish(&f.out, kMT + 1);
+}
+
+__device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
+  __shared__ P2Flags f;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock, b = b0 + lane;
+  const bool act = b < a.n;
+  const size_t nr = (size_t)a.nrow;
+  if (tid == 0) {
+    f.in = 0;
+    f.out = 0;
+  }
+  __syncthreads();
+  if (w == 0) {  // P1: pass 1 of episode ep + 6 into its fresh slot
+    if (act) {
+      const int e = a.ep_in[b] + 6;
+      mt_seed_pass1_g(a.s_mt[0] + b, nr, episode_seed(a.seed_base, b, e));
+      a.s_tag[0][b] = e * 4 + 1;
+    }
+    return;
+  }
+  // P2: episode ep + 5, whose pass 1 ran in the previous call.  Every lane
+  // runs the chain (lockstep); only boards whose pass 1 was this episode's
+  // get the tag.
+  uint32_t *slot = a.s_mt[1];
+  if (w == 1) {
+    const int e = act ? a.ep_in[b] + 5 : 0;
+    const bool ok = act && a.s_tag[1][b] == e * 4 + 1;
+    p2_pass2_lds(lane, f);
+    if (ok) a.s_tag[1][b] = e * 4 + 2;
+  } else if (w == 2) {  // stage rows [0, kMT) in chunks, publishing as they land
+    constexpr int kChunk = 64;
+    for (int r0 = 0; r0 < kMT; r0 += kChunk) {
+      const int r1 = r0 + kChunk < kMT ? r0 + kChunk : kMT;
+      p2_rows<true>(slot, nr, b0, lane, r0, r1);
+      p2_publish(&f.in, r1);
+    }
+    p2_wait(&f.out, kMT + 1);
+    p2_rows<false>(slot, nr, b0, lane, 0, kAheadTwist / 2);
+  } else {  // w == 3: final rows back as pass 2 publishes them
+    int done = kAheadTwist;
+    while (done < kMT) {
+      const int upto = p2_wait(&f.out, done + 32 < kMT ? done + 32 : kMT);
+      const int r1 = upto < kMT ? upto : kMT;
+      if (r1 > done) p2_rows<false>(slot, nr, b0, lane, done, r1);
+      done = r1 > done ? r1 : done;
+    }
+    p2_wait(&f.out, kMT + 1);
+    p2_rows<false>(slot, nr, b0, lane, kAheadTwist / 2, kAheadTwist);
+  }
+}
+
+__device__ __forceinline__ void p2_draw(const P2Args &a, int blk) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock, b = b0 + lane;
+  const bool act = b < a.n;
+  const size_t nr = (size_t)a.nrow;
+  if (w == 3) {  // the rule hashes of episode ep + 2
+    if (!act) return;
+    const int e = a.ep_in[b] + 2;
+    const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
+#pragma unroll 1
+    for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
+    a.h_tag_w[b] = e;
+    return;
+  }
+  // stage w: draws [lo, hi) of episode ep + 4 - w, on stream slot s_mt[2 + w]
+  const int lo = 8 * w, hi = w == 2 ? a.draws : min(a.draws, lo + 8);
+  const int e = act ? a.ep_in[b] + 4 - w : 0;
+  const uint32_t *slot = a.s_mt[2 + w];
+  const P2Draw &in = w == 1 ? a.ab_r : a.bc_r;
+  const P2Draw &out = w == 0 ? a.ab_w : w == 1 ? a.bc_w : a.pl_w;
+  bool ok = act && a.s_tag[2 + w][b] == e * 4 + 2;
+  if (w > 0) ok = ok && in.tag[b] == e * 4 + w;
+  // the window: rows [0, kP2Win) of the wave's 64 boards into LDS rows of
+  // stride 65 (16-B loads, four boards of a row per lane, half the window's
+  // loads in flight at once)
+  const int base = w * kP2Win * kLdsStride;
+  if (__any(ok)) {
+    constexpr int U = 24;
+    static_assert(kP2Win % (4 * U) == 0, "window rows per pass");
+    const int c4 = (lane & 15) * 4;
+#pragma unroll 1
+    for (int r0 = 0; r0 < kP2Win; r0 += 4 * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int r = r0 + 4 * u + (lane >> 4);
+        v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint32_t *dd = hz_lds + base + (r0 + 4 * u + (lane >> 4)) * kLdsStride + c4;
+        dd[0] = v[u].x;
+        dd[1] = v[u].y;
+        dd[2] = v[u].z;
+        dd[3] = v[u].w;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!act) return;
+  if (!ok) {
+    out.tag[b] = -1;
+    return;
+  }
+  int k0 = 0, c0 = kMTAhead;
+  uint64_t bag = initial_bag(), q[kAheadWords] = {0, 0, 0, 0};
+  if (w > 0) {
+    k0 = in.k[b];
+    bag = in.bag[b];
+#pragma unroll
+    for (int i = 0; i < kAheadWords; i++) q[i] = in.q[(size_t)i * nr + b];
+    int32_t cv[kAheadDraws + 1];  // the cursors so far, forwarded (all loads first)
+#pragma unroll
+    for (int i = 0; i <= kAheadDraws; i++) cv[i] = i <= 8 * w ? in.cur[(size_t)i * nr + b] : 0;
+#pragma unroll
+    for (int i = 0; i <= kAheadDraws; i++)
+      if (i <= 8 * w && i <= k0) out.cur[(size_t)i * nr + b] = cv[i];
+    c0 = in.cur[(size_t)k0 * nr + b];
+  } else {
+    out.cur[b] = kMTAhead;
+  }
+  int k = k0;
+  if (k0 >= lo) {  // every earlier draw is done: continue in the window
+    StreamDraw<WinMT> d{WinMT(base + lane, c0, kP2Win)};
+#pragma unroll 1
+    for (int i = lo; i < hi; i++) {
+      if (d.m.pos >= kP2Win) break;
+      const uint32_t p9 = d(bag);
+      // a draw that consumed words past the window is discarded: the play
+      // stages redo it from the stream slot (from the last cursor kept)
+      if (d.m.pos > kP2Win) break;
+      apply_pile_fast(bag, p9);
+      const int bit = 9 * i, wd = bit >> 6, off = bit & 63;
+      const uint64_t lo9 = (uint64_t)p9 << off, hi9 = off > 55 ? (uint64_t)p9 >> (64 - off) : 0ull;
+      q[0] |= wd == 0 ? lo9 : 0ull;
+      q[1] |= wd == 1 ? lo9 : wd == 0 ? hi9 : 0ull;
+      q[2] |= wd == 2 ? lo9 : wd == 1 ? hi9 : 0ull;
+      q[3] |= wd == 3 ? lo9 : wd == 2 ? hi9 : 0ull;
+      out.cur[(size_t)(i + 1) * nr + b] = d.m.cursor();
+      k = i + 1;
+    }
+  }
+  out.k[b] = k;
+  out.bag[b] = bag;
+#pragma unroll
+  for (int i = 0; i < kAheadWords; i++) out.q[(size_t)i * nr + b] = q[i];
+  out.tag[b] = e * 4 + w + 1;
+}
+
+__device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
+  __shared__ uint64_t s_lds_mask;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock, b = b0 + lane;
+  const bool act = b < a.n;
+  const uint64_t actmask = __ballot(act);
+  const int nb = a.n - b0 < kBlock ? a.n - b0 : kBlock;
+  const size_t nr = (size_t)a.nrow;
+#ifdef HZ_DIAG
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (w == 1) {  // playA: plies [0, kP2Half) of episode ep + 1
+    if (act) {
+      const int e = a.ep_in[b] + 1;
+      const P2Draw &pl = a.pl_a;
+      if (pl.tag[b] == e * 4 + 3) {
+        const int nd = pl.k[b];
+        PlayDraw2 draw{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
+                       MTR(a.s_mt[5] + b, (int)nr, pl.cur[(size_t)nd * nr + b])};
+        State s;
+        if (__all(nd >= 5)) draw.scripted_reset(s);
+        else reset_state(s, draw);
+        const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
+        const uint32_t *hs = a.h_tag_a[b] == e ? a.h_a + b : nullptr;
+        const int lim = kP2Half < a.max_plies ? kP2Half : a.max_plies;
+        const int steps = p2_plies(s, draw, 0, lim, rk, hs, nr);
+#pragma unroll
+        for (int k = 0; k < 4; k++) a.m_st_w[(size_t)k * nr + b] = s.pl[k];
+        a.m_st_w[4 * nr + b] = s.piles;
+        a.m_st_w[5 * nr + b] = s.misc;
+        a.m_q_w[b] = draw.q0;
+        a.m_q_w[nr + b] = draw.q1;
+        a.m_q_w[2 * nr + b] = draw.q2;
+        a.m_q_w[3 * nr + b] = draw.q3;
+        a.m_i_w[b] = draw.d;
+        a.m_i_w[nr + b] = steps;
+        a.m_i_w[2 * nr + b] = draw.fell ? draw.gm.cursor() : -1;
+        a.m_tag_w[b] = e;
+      } else {
+        a.m_tag_w[b] = -1;
+      }
+#ifdef HZ_DIAG
+      if (g_stamps) g_stamps[(size_t)b * 16 + 9] = __builtin_amdgcn_s_memtime() - t0;  // playA alone
+#endif
+    }
+  }
+  if (w == 0) {  // playB: the rest of episode ep (or all of it)
+    bool lds_used = false;
+    if (act) {
+      const int e = a.episode[b];
+      const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
+      a.episode[b] = e + 1;
+      State s;
+      int g = 0, cursor = 0, src = -1;
+      const P2Draw &pl = a.pl_b;
+      if (a.m_tag_r[b] == e && pl.tag[b] == e * 4 + 3) {  // continue after playA
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.pl[k] = a.m_st_r[(size_t)k * nr + b];
+        s.piles = a.m_st_r[4 * nr + b];
+        s.misc = a.m_st_r[5 * nr + b];
+        const int d = a.m_i_r[b], fc = a.m_i_r[2 * nr + b], nd = pl.k[b];
+        g = a.m_i_r[nr + b];
+        PlayDraw2 draw{a.m_q_r[b], a.m_q_r[nr + b], a.m_q_r[2 * nr + b], a.m_q_r[3 * nr + b], d, nd, fc >= 0,
+                       MTR(a.s_mt[6] + b, (int)nr, fc >= 0 ? fc : pl.cur[(size_t)nd * nr + b])};
+        const uint32_t *hs = a.h_tag_b[b] == e ? a.h_b + b : nullptr;
+        g += p2_plies(s, draw, g, a.max_plies, rk, hs, nr);
+        cursor = draw.fell ? draw.gm.cursor() : pl.cur[(size_t)draw.d * nr + b];
+        src = 2 + a.s_idx6;
+      } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
+        mt_seed(hz_lds + lane, kLdsStride, sd);
+        PlayDraw draw{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
+        reset_state(s, draw);
+        g = p2_plies(s, draw, 0, a.max_plies, rk, nullptr, nr);
+        cursor = draw.m.cursor();
+        lds_used = true;
+      }
+      if (score_pending(s.misc)) finish_game(s);
+      store_state(a.st, a.n, b, s);
+      a.pos[b] = cursor;
+      a.mt_src[b] = src;
+      a.ply[b] = g;
+      a.seed[b] = sd;
+      a.ep_out[b] = e + 1;
+      // the game this call completes, as hz_play's other pipeline counts it
+      // (its first plies ran one call earlier, in playA)
+      if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
+      if (a.steps_done) a.steps_done[b] = g;
+#ifdef HZ_DIAG
+      if (g_stamps) g_stamps[(size_t)b * 16 + 8] = __builtin_amdgcn_s_memtime() - t0;  // playB alone
+#endif
+    }
+    const uint64_t lm = __ballot(lds_used);
+    if (lane == 0) s_lds_mask = lm;
+  }
+  if (w == 0 && actmask == 0 && lane == 0) s_lds_mask = 0;
+  __syncthreads();
+  const uint64_t lds_mask = s_lds_mask & actmask;
+  if (lds_mask) stage_mt(a.mt + (size_t)b0 * kMT, nb, tid, lds_mask, false);
+}
+
+__global__ void __launch_bounds__(kStageThreads) k_play2(P2Args a, int nblk) {
+  const int blk = (int)blockIdx.x;
+  const int role = blk < nblk ? 0 : blk < 2 * nblk ? 1 : 2;  // play, draw, seed blocks
+#ifdef HZ_DIAG
+  if (g_role_only >= 0 && g_role_only != role) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (role == 0) p2_play(a, blk);
+  else if (role == 1) p2_draw(a, blk - nblk);
+  else p2_seed(a, blk - 2 * nblk);
+#ifdef HZ_DIAG
+  {  // stage durations, per board: 0 playB, 1 playA, 2-4 draws A-C, 5 hashes, 6 P1, 7 P2
+    const int w = threadIdx.x >> 6, bb = (blk - role * nblk) * kBlock + (threadIdx.x & 63);
+    const int slot = role == 0 ? w : role == 1 ? 2 + w : 6 + w;
+    if (g_stamps && bb < a.n && slot < 8 && (role != 0 || w < 2))
+      g_stamps[(size_t)bb * 16 + slot] = __builtin_amdgcn_s_memtime() - t0;
+  }
+#endif
+}
+
+// boards whose stream lives in a pipeline-2 slot (mt_src = 2 + slot): the
+// slot's column (word-major) into the board's own stream, one wave per board
+struct P2Slots {
+  uint32_t *s[kP2Stream];
+};
+__global__ void __launch_bounds__(64) k_mt_materialize2(uint32_t *__restrict__ mt, P2Slots slots,
+                                                       int32_t *__restrict__ mt_src, int n, long nrow) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int src = mt_src[b];
+  if (src < 2 || src >= 2 + kP2Stream) return;
+  const uint32_t *from = slots.s[src - 2] + b;
+  uint32_t *to = mt + (size_t)b * kMT;
+  uint32_t v[(kMT + 63) / 64];
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++) v[k] = lane + 64 * k < kMT ? from[(size_t)(lane + 64 * k) * nrow] : 0u;
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++)
+    if (lane + 64 * k < kMT) to[lane + 64 * k] = v[k];
+  if (lane == 0) mt_src[b] = -1;
+}
+
 // ---------------------------------------------------------- greedy agent
 // evaluation.py:137-196 choose_move_greedy, one wave per board: lane l scores
 // legal moves l, l+64 (canonical ascending order) by applying the placement
@@ -1148,7 +1726,7 @@ __global__ void __launch_bounds__(64) k_mt_materialize(uint32_t *__restrict__ mt
                                                       int n) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int src = mt_src[b];
-  if (src < 0) return;
+  if (src < 0 || src > 1) return;  // (pipeline-2 slots: k_mt_materialize2)
   const uint32_t *from = (src ? a1 : a0) + (size_t)b * kMT;
   uint32_t *to = mt + (size_t)b * kMT;
   uint32_t v[(kMT + 63) / 64];
@@ -1164,8 +1742,159 @@ static int materialize(hz_env *e) {
   if (!e->lazy) return 0;
   hipLaunchKernelGGL(k_mt_materialize, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ahead_mt[0], e->ahead_mt[1],
                      e->mt_src, e->n);
+  if (e->p2_s[0]) {
+    P2Slots sl;
+    for (int k = 0; k < kP2Stream; k++) sl.s[k] = e->p2_s[k];
+    hipLaunchKernelGGL(k_mt_materialize2, dim3(e->n), dim3(64), 0, e->stream, e->mt, sl, e->mt_src, e->n,
+                       (long)e->nrow);
+  }
   e->lazy = 0;
   return launch_err();
+}
+
+// ---------------------------------------------------------- pipeline 2 host
+static void free_p2(hz_env *e) {
+  auto f = [](void *p) {
+    if (p) (void)hipFree(p);
+  };
+  for (int k = 0; k < kP2Stream; k++) {
+    f(e->p2_s[k]);
+    f(e->p2_s_tag[k]);
+    e->p2_s[k] = nullptr;
+    e->p2_s_tag[k] = nullptr;
+  }
+  for (int k = 0; k < 7; k++) {
+    f(e->p2_d_tag[k]);
+    f(e->p2_d_k[k]);
+    f(e->p2_d_q[k]);
+    f(e->p2_d_bag[k]);
+    f(e->p2_d_cur[k]);
+    e->p2_d_tag[k] = e->p2_d_k[k] = e->p2_d_cur[k] = nullptr;
+    e->p2_d_q[k] = e->p2_d_bag[k] = nullptr;
+  }
+  for (int k = 0; k < 2; k++) {
+    f(e->p2_m_tag[k]);
+    f(e->p2_m_st[k]);
+    f(e->p2_m_q[k]);
+    f(e->p2_m_i[k]);
+    f(e->p2_ep[k]);
+    e->p2_m_tag[k] = e->p2_m_i[k] = e->p2_ep[k] = nullptr;
+    e->p2_m_st[k] = e->p2_m_q[k] = nullptr;
+  }
+  for (int k = 0; k < 3; k++) {
+    f(e->p2_h[k]);
+    f(e->p2_h_tag[k]);
+    e->p2_h[k] = nullptr;
+    e->p2_h_tag[k] = nullptr;
+  }
+}
+
+// every hand-off tag to "none" (a tag names the episode its slot holds, and a
+// slot's contents depend only on (board, episode), so this is never needed
+// for correctness; it keeps a fresh pipeline from trusting freshly allocated
+// memory)
+static int p2_clear_tags(hz_env *e) {
+  const size_t bytes = e->nrow * sizeof(int32_t);
+  for (int k = 0; k < kP2Stream; k++)
+    if (hipMemsetAsync(e->p2_s_tag[k], 0xff, bytes, e->stream)) return 1;
+  for (int k = 0; k < 7; k++)
+    if (hipMemsetAsync(e->p2_d_tag[k], 0xff, bytes, e->stream)) return 1;
+  for (int k = 0; k < 2; k++)
+    if (hipMemsetAsync(e->p2_m_tag[k], 0xff, bytes, e->stream)) return 1;
+  for (int k = 0; k < 3; k++)
+    if (hipMemsetAsync(e->p2_h_tag[k], 0xff, bytes, e->stream)) return 1;
+  return 0;
+}
+
+// allocated on first use: 8 stream slots of 2.5 KB per board plus ~1.5 KB of
+// hand-offs per board
+static int alloc_p2(hz_env *e) {
+  if (e->p2_s[0]) return 0;
+  const size_t nr = e->nrow;
+  auto m = [](auto **p, size_t bytes) { return hipMalloc((void **)p, bytes) == hipSuccess; };
+  bool ok = true;
+  for (int k = 0; ok && k < kP2Stream; k++) ok = m(&e->p2_s[k], nr * kMT * 4) && m(&e->p2_s_tag[k], nr * 4);
+  for (int k = 0; ok && k < 7; k++)
+    ok = m(&e->p2_d_tag[k], nr * 4) && m(&e->p2_d_k[k], nr * 4) && m(&e->p2_d_q[k], kAheadWords * nr * 8) &&
+         m(&e->p2_d_bag[k], nr * 8) && m(&e->p2_d_cur[k], (kAheadDraws + 1) * nr * 4);
+  for (int k = 0; ok && k < 2; k++)
+    ok = m(&e->p2_m_tag[k], nr * 4) && m(&e->p2_m_st[k], 6 * nr * 8) && m(&e->p2_m_q[k], 4 * nr * 8) &&
+         m(&e->p2_m_i[k], 3 * nr * 4) && m(&e->p2_ep[k], nr * 4);
+  for (int k = 0; ok && k < 3; k++) ok = m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
+  if (!ok || p2_clear_tags(e)) {
+    free_p2(e);
+    return 1;
+  }
+  e->primed2 = 0;
+  return 0;
+}
+
+// one hz_play call of pipeline 2 (k_play2).  Call c uses stream slot
+// (c - s) % 8 for stage s (0 P1 .. 6 playB), draw hand-offs AB / BC by call
+// parity, the pile scripts and rule hashes in rings of three, playA -> playB
+// by parity; every slot written by call c is read by call c + 1 or later, so
+// launch order on the stream is the only synchronisation.
+static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32_t *steps_done) {
+  if (alloc_p2(e)) return 1;
+  const int c = e->calls2, r = c & 1, w = r ^ 1;
+  if (!e->primed2) {
+    if (hipMemcpyAsync(e->p2_ep[w], e->episode, (size_t)e->n * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                       e->stream))
+      return 1;
+    e->primed2 = 1;
+  }
+  P2Args a{};
+  a.st = e->state;
+  a.mt = e->mt;
+  a.pos = e->pos;
+  a.ply = e->ply;
+  a.episode = e->episode;
+  a.seed = e->seed;
+  a.n = e->n;
+  a.max_plies = max_plies;
+  a.draws = e->seed_ahead;
+  a.seed_base = e->seed_base;
+  a.nrow = (long)e->nrow;
+  a.games_done = games_done;
+  a.steps_done = steps_done;
+  a.mt_src = e->mt_src;
+  a.ep_in = e->p2_ep[w];
+  a.ep_out = e->p2_ep[r];
+  auto sl = [c](int s) { return ((c - s) % kP2Stream + kP2Stream) % kP2Stream; };
+  for (int s = 0; s < 7; s++) {
+    a.s_mt[s] = e->p2_s[sl(s)];
+    a.s_tag[s] = e->p2_s_tag[sl(s)];
+  }
+  a.s_idx6 = sl(6);
+  auto dr = [e](int k) { return P2Draw{e->p2_d_tag[k], e->p2_d_k[k], e->p2_d_q[k], e->p2_d_bag[k], e->p2_d_cur[k]}; };
+  a.ab_w = dr(r);
+  a.ab_r = dr(w);
+  a.bc_w = dr(2 + r);
+  a.bc_r = dr(2 + w);
+  a.pl_w = dr(4 + c % 3);
+  a.pl_a = dr(4 + (c + 2) % 3);  // written by call c - 1
+  a.pl_b = dr(4 + (c + 1) % 3);  // written by call c - 2
+  a.m_tag_w = e->p2_m_tag[r];
+  a.m_i_w = e->p2_m_i[r];
+  a.m_st_w = e->p2_m_st[r];
+  a.m_q_w = e->p2_m_q[r];
+  a.m_tag_r = e->p2_m_tag[w];
+  a.m_i_r = e->p2_m_i[w];
+  a.m_st_r = e->p2_m_st[w];
+  a.m_q_r = e->p2_m_q[w];
+  a.h_w = e->p2_h[c % 3];
+  a.h_tag_w = e->p2_h_tag[c % 3];
+  a.h_a = e->p2_h[(c + 2) % 3];
+  a.h_tag_a = e->p2_h_tag[(c + 2) % 3];
+  a.h_b = e->p2_h[(c + 1) % 3];
+  a.h_tag_b = e->p2_h_tag[(c + 1) % 3];
+  const int nblk = grid_for(e->n);
+  hipLaunchKernelGGL(k_play2, dim3(3 * nblk), dim3(kStageThreads), kResetLds, e->stream, a, nblk);
+  if (int err = launch_err()) return err;
+  e->lazy = 1;
+  e->calls2++;
+  e->primed = 0;  // the other pipeline's episode prediction is stale now
+  return 0;
 }
 
 extern "C" {
@@ -1190,7 +1919,8 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
                           (int)kResetLds) != hipSuccess ||
       hipFuncSetAttribute((const void *)k_rollout<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)kResetLds) != hipSuccess ||
-      false) {
+      hipFuncSetAttribute((const void *)k_play2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResetLds) !=
+          hipSuccess) {
     free(e);
     return nullptr;
   }
@@ -1231,6 +1961,10 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   }
   ok = ok && hipDeviceSynchronize() == hipSuccess;
   e->seed_ahead = kAheadDraws;
+  {  // HZ_PIPELINE=2: hz_play's second pipeline by default (hz_env_set_pipeline)
+    const char *pv = getenv("HZ_PIPELINE");
+    e->pipeline = pv && atoi(pv) == 2 ? 2 : 1;
+  }
   if (!ok) {
     hz_env_destroy(e);
     return nullptr;
@@ -1240,6 +1974,7 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
 
 void hz_env_destroy(hz_env *e) {
   if (!e) return;
+  free_p2(e);
   for (int k = 0; k < 2; k++) {
     if (e->ahead_mt[k]) (void)hipFree(e->ahead_mt[k]);
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
@@ -1267,6 +2002,14 @@ void hz_env_destroy(hz_env *e) {
 
 int32_t hz_env_size(const hz_env *e) { return e ? e->n : -1; }
 
+int hz_env_set_pipeline(hz_env *e, int32_t pipeline) {
+  if (!e || (pipeline != 1 && pipeline != 2)) return -1;
+  e->pipeline = pipeline;
+  e->primed = 0;
+  e->primed2 = 0;
+  return 0;
+}
+
 int hz_env_set_stream(hz_env *e, void *stream) {
   if (!e) return -1;
   e->stream = (hipStream_t)stream;
@@ -1286,6 +2029,8 @@ int hz_env_set_seed_ahead(hz_env *e, int32_t draws) {
   if (!e || draws < 0) return -1;
   e->seed_ahead = draws > kAheadDraws ? kAheadDraws : draws;
   e->primed = 0;
+  e->primed2 = 0;
+  if (e->p2_s[0] && p2_clear_tags(e)) return 1;
   // draw1's work depends on the draw count: start the ring afresh
   for (int k = 0; k < kRing; k++)
     if (hipMemsetAsync(e->ring_tag[k], 0xff, e->nrow * sizeof(int32_t), e->stream)) return 1;
@@ -1296,6 +2041,7 @@ int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   if (!e) return -1;
   if (int err = materialize(e)) return err;  // unselected boards keep their streams
   e->primed = 0;  // episode counters move outside hz_play's plan
+  e->primed2 = 0;
   hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
   return launch_err();
@@ -1359,6 +2105,7 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
   if (!e || max_plies < 0) return -1;
+  e->primed2 = 0;  // (pipeline 2's episode prediction is stale after this launch)
   // hz_rollout continues the current games on their streams; hz_play starts
   // every board's next game (its old stream is dead)
   if (!reset_first)
@@ -1420,6 +2167,9 @@ int hz_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, uint64_t *traj_
 
 int hz_play(hz_env *e, int32_t max_plies, int32_t auto_reset, uint64_t *traj_state, uint64_t *traj_mask,
             int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
+  if (e && e->pipeline == 2 && !auto_reset && !traj_state && !traj_mask && !traj_action &&
+      max_plies >= kP2MinPlies)
+    return launch_play2(e, max_plies, games_done, steps_done);
   return launch_rollout(e, max_plies, auto_reset, 1, traj_state, traj_mask, traj_action, games_done, steps_done);
 }
 

@@ -9,8 +9,9 @@
 //
 // One wave (64 lanes) owns one board in every tree kernel: lanes are edges
 // in selection and backup, children in expansion.  Per board, in HBM:
-//   node pool  [max_nodes] : 48 B state, 64-bit key digest, first edge, #edges
-//   edge pool  [max_edges] : action, child node, N (int), W (f64), P (f32), player
+//   node pool  [max_nodes] : 48 B state, 64 B canonical key, first edge, #edges
+//   edge pool  [max_edges] : action, child node, N (int), W (f64), P (f32), player,
+//                            hint (the child's first edge / edge count / terminal flag)
 //   hash table [hcap] u64  : search generation << 32 | node id (linear probing;
 //                            entries of older searches read as empty, so the
 //                            table is never cleared)
@@ -34,7 +35,7 @@ struct hz_mcts {
   int32_t dedup_walk;    // hz_mcts_set_dedup_walk (tests): every sibling dedup takes the serial walk
   hipStream_t stream;
   uint64_t *node_state;  // [n][max_nodes][6]
-  uint64_t *node_hash;   // [n][max_nodes]
+  uint64_t *node_key;    // [n][max_nodes][8] canonical key (a probe compares it whole: no key rebuilt)
   int32_t *node_e0;      // [n][max_nodes]
   int32_t *node_ne;      // [n][max_nodes]
   int16_t *edge_action;  // [n][max_edges]
@@ -43,6 +44,11 @@ struct hz_mcts {
   double *edge_w;        // [n][max_edges]
   float *edge_p;         // [n][max_edges]
   uint8_t *edge_player;  // [n][max_edges]
+  // [n][max_edges] the child node's e0 << 8 | terminal << 7 | ne as far as
+  // known: ne = 0 means "not expanded when last seen" (select then reads the
+  // node itself and repairs the hint), so the walk takes one memory round
+  // trip per level (edges + hints) instead of two (node, then its edges)
+  int32_t *edge_hint;
   uint64_t *ht;          // [n][hcap]
   int32_t *counts;       // [n][4]: nodes, edges, generation, overflow
   int32_t *path;         // [n][max_depth]
@@ -107,7 +113,8 @@ __global__ void __launch_bounds__(kWave) k_begin(hz_mcts m, const uint64_t *__re
   store_node(m.node_state + nb * 6, s);
   CKey key = canon_key(s, !m.exact_keys);
   uint64_t h = key_hash(key);
-  m.node_hash[nb] = h;
+#pragma unroll
+  for (int w = 0; w < 8; w++) m.node_key[nb * 8 + w] = key.w[w];
   m.node_e0[nb] = 0;
   m.node_ne[nb] = 0;
   int gen = cnt[2] + 1;
@@ -124,6 +131,58 @@ __global__ void __launch_bounds__(kWave) k_begin(hz_mcts m, const uint64_t *__re
 // with NumPy promotion: cpuct*P in float32, the rest float64; Q = W/N
 // (0 while N == 0); the first edge (insertion = ascending action order)
 // with the largest Q+U by strict '>' wins.
+// The walk reads each level's edges with their hints (the child's first
+// edge and edge count): one dependent memory round trip per level.  A hint
+// with ne = 0 (the child was unexpanded when the edge was written, or is a
+// transposition target expanded through another parent since) is checked
+// against the node and repaired; a terminal child (never expanded) needs no
+// check.
+constexpr int kHintNe = 127, kHintTerm = 128;
+// Wave reductions of the walk: within each row of 16 lanes by DPP moves (a
+// VALU operand modifier: quad_perm xor 1, xor 2, then row_ror 4, 8), across
+// the four rows by two ds_bpermute rounds (xor 16, 32): 2 LDS-crossbar
+// round trips per reduction instead of 6.  Every lane ends with the result.
+template <int Ctrl>
+__device__ __forceinline__ int dpp_mov(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, Ctrl, 0xf, 0xf, false);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppRor4 = 0x124, kDppRor8 = 0x128;
+__device__ __forceinline__ int wave_sum_i(int v) {
+  v += dpp_mov<kDppXor1>(v);
+  v += dpp_mov<kDppXor2>(v);
+  v += dpp_mov<kDppRor4>(v);
+  v += dpp_mov<kDppRor8>(v);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+// (value, index): the largest value, the smallest index among equal values
+// (MCTS.py:102-121's first strict '>' in insertion order); associative and
+// commutative, so the reduction order does not change the result
+__device__ __forceinline__ void argmax_take(double ob, int oi, double &best, int &bi) {
+  if (ob > best || (ob == best && oi < bi)) {
+    best = ob;
+    bi = oi;
+  }
+}
+template <int Ctrl>
+__device__ __forceinline__ void argmax_dpp(double &best, int &bi) {
+  const long long b = __double_as_longlong(best);
+  const int lo = dpp_mov<Ctrl>((int)b), hi = dpp_mov<Ctrl>((int)(b >> 32)), oi = dpp_mov<Ctrl>(bi);
+  argmax_take(__longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo)), oi, best,
+              bi);
+}
+__device__ __forceinline__ void wave_argmax(double &best, int &bi) {
+  argmax_dpp<kDppXor1>(best, bi);
+  argmax_dpp<kDppXor2>(best, bi);
+  argmax_dpp<kDppRor4>(best, bi);
+  argmax_dpp<kDppRor8>(best, bi);
+#pragma unroll
+  for (int o = 16; o < kWave; o <<= 1) argmax_take(__shfl_xor(best, o), __shfl_xor(bi, o), best, bi);
+}
+__device__ __forceinline__ int32_t edge_hint_of(int e0, int ne, bool term) {
+  return (int32_t)((uint32_t)e0 << 8 | (term ? (uint32_t)kHintTerm : 0u) | (uint32_t)ne);
+}
 __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
                                              float cpuct) {
   int32_t *cnt = m.counts + (size_t)b * 4;
@@ -137,30 +196,38 @@ __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, 
   size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
   int node = 0, d = 0;
   int32_t *path = m.path + (size_t)b * m.max_depth;
+  int ne = m.node_ne[nb], e0 = m.node_e0[nb];  // the root
+  bool term = false;                           // an active board's root is not terminal
+  bool known = true;                           // ne came from the node itself
   for (;;) {
-    int ne = m.node_ne[nb + node];
-    if (ne <= 0) break;
-    int e0 = m.node_e0[nb + node];
-    int n0 = 0, n1 = 0, c0 = 0, c1 = 0;
+    if (ne <= 0) {
+      if (known || term) break;
+      // the hint says unexpanded: the node decides (and the hint is repaired)
+      ne = m.node_ne[nb + node];
+      e0 = m.node_e0[nb + node];
+      if (ne <= 0) break;
+      if (lane == 0) m.edge_hint[eb + path[d - 1]] = edge_hint_of(e0, ne, false);
+    }
+    int n0 = 0, n1 = 0, c0 = 0, c1 = 0, h0 = 0, h1 = 0;
     double w0 = 0, w1 = 0;
     float p0 = 0, p1 = 0;
-    // each edge's child is read with its statistics (one memory round trip
-    // per level instead of a second, dependent one for the winner's child)
+    // each edge's child and hint are read with its statistics (one memory
+    // round trip per level)
     if (lane < ne) {
       n0 = m.edge_n[eb + e0 + lane];
       w0 = m.edge_w[eb + e0 + lane];
       p0 = m.edge_p[eb + e0 + lane];
       c0 = m.edge_child[eb + e0 + lane];
+      h0 = m.edge_hint[eb + e0 + lane];
     }
     if (lane + kWave < ne) {
       n1 = m.edge_n[eb + e0 + lane + kWave];
       w1 = m.edge_w[eb + e0 + lane + kWave];
       p1 = m.edge_p[eb + e0 + lane + kWave];
       c1 = m.edge_child[eb + e0 + lane + kWave];
+      h1 = m.edge_hint[eb + e0 + lane + kWave];
     }
-    int ns = n0 + n1;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+    const int ns = wave_sum_i(n0 + n1);
     double sqrt_ns = __dsqrt_rn(ns > 1 ? (double)ns : 1.0);
     double best = -INFINITY;
     int bi = 0x7fffffff;
@@ -176,12 +243,7 @@ __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, 
       double v = __dadd_rn(q, u);
       if (v > best) { best = v; bi = lane + kWave; }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      double ob = __shfl_xor(best, o);
-      int oi = __shfl_xor(bi, o);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
+    wave_argmax(best, bi);
     int sel = e0 + bi;
     if (d >= m.max_depth) {
       if (lane == 0) cnt[3] = 1;
@@ -189,13 +251,19 @@ __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, 
     }
     if (lane == 0) path[d] = sel;
     d++;
-    node = __shfl(bi < kWave ? c0 : c1, bi & (kWave - 1));  // edge_child[sel], from the winner's lane
+    const int src = bi & (kWave - 1);
+    node = __shfl(bi < kWave ? c0 : c1, src);  // edge_child[sel], from the winner's lane
+    const int hint = __shfl(bi < kWave ? h0 : h1, src);
+    ne = hint & kHintNe;
+    e0 = (int)((uint32_t)hint >> 8);
+    term = (hint & kHintTerm) != 0;
+    known = false;
   }
   if (lane == 0) {
     m.leaf[b] = node;
     m.depth[b] = d;
-    State s = load_node(m.node_state + (nb + node) * 6);
-    m.leaf_gidx[b] = game_done(s.misc) ? -1 : (int)(nb + node);
+    if (d == 0) term = game_done(m.node_state[(nb + node) * 6 + 5]);
+    m.leaf_gidx[b] = term ? -1 : (int)(nb + node);
   }
 }
 
@@ -242,6 +310,76 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
     count[0] = part[t];
     if (m.eval_ctr) m.eval_ctr[0] += part[t];  // one workgroup, stream-ordered: no atomic needed
   }
+}
+
+// ------------------------------------------------- gather + encode, one launch
+// k_gather's result and both encoders in one launch for any batch: every
+// workgroup owns leaf rows [8 g, 8 g + 8) (a pair per wave) and finds their
+// boards itself: it scans all n leaf flags (thread t: boards [t per, (t + 1)
+// per), per = ceil(n / 256); 16 KB of L2 reads per workgroup at 4096 boards),
+// so no workgroup waits for another and there is no separate gather launch
+// (k_gather: 7 us of one 1024-thread workgroup, then two encoder launches).
+// Rows, slots, gidx_c and the count are exactly k_gather's (board order);
+// workgroup 0 writes the count, the eval counter and the slots of the boards
+// that need no network.
+constexpr int kGEWaves = 4, kGERows = 2 * kGEWaves, kGEThreads = kGEWaves * kWave, kGELoads = 16;
+__global__ void __launch_bounds__(kGEThreads) k_gather_encode(hz_mcts m, int32_t *__restrict__ rows,
+                                                               int32_t *__restrict__ count,
+                                                               float *__restrict__ board, float *__restrict__ glob) {
+  __shared__ uint64_t smask[kGEWaves][76];
+  __shared__ float sval[kGEWaves][76];
+  __shared__ int32_t wsum[kGEWaves];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int per = (m.n + kGEThreads - 1) / kGEThreads;
+  const int b0 = t * per < m.n ? t * per : m.n, b1 = b0 + per < m.n ? b0 + per : m.n;
+  const int r0 = (int)blockIdx.x * kGERows;
+  int c = 0;
+  for (int base = b0; base < b1; base += kGELoads) {  // one pass up to 4096 boards: all loads in flight
+    int g[kGELoads];
+#pragma unroll
+    for (int k = 0; k < kGELoads; k++) g[k] = base + k < b1 ? m.leaf_gidx[base + k] : -1;
+#pragma unroll
+    for (int k = 0; k < kGELoads; k++) c += g[k] >= 0;
+  }
+  // exclusive prefix of the per-thread counts: wave scan, then the waves' totals
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == kWave - 1) wsum[w] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < kGEWaves; k++) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  int r = before + incl - c;  // rank of the thread's first needed board
+  const bool first = blockIdx.x == 0;
+  if (first || (r < r0 + kGERows && r + c > r0)) {
+    for (int b = b0; b < b1; b++) {
+      const int g = m.leaf_gidx[b];
+      if (g >= 0) {
+        if (r >= r0 && r < r0 + kGERows) {
+          m.slot[b] = r;
+          m.gidx_c[r] = g;
+          if (rows) rows[r] = b;
+        }
+        r++;
+      } else if (first) {
+        m.slot[b] = -1;
+      }
+    }
+  }
+  if (first && t == 0) {
+    count[0] = total;
+    if (m.eval_ctr) m.eval_ctr[0] += total;  // one thread of one workgroup, stream-ordered
+  }
+  if (r0 >= total) return;
+  __syncthreads();  // the workgroup's gidx_c entries (global, written above) are visible to all its threads
+  encode_pair<true>(m.node_state, 1, 6, m.gidx_c, total, board, glob, lane, r0 + 2 * w, smask[w], sval[w]);
 }
 
 // --------------------------------- select + gather + encode for small batches
@@ -472,6 +610,7 @@ struct ExpandLds {
   uint64_t hash[kChildLds];
   int32_t child[kChildLds];
   int32_t flag[kChildLds];  // 0 new, 1 existing node, 2 self-loop (skipped), 3 sibling duplicate
+  float prior[kChildLds];   // the children's priors (policy row, by action)
 };
 static_assert(kDedupSlots * sizeof(uint32_t) <= kChildLds * sizeof(uint64_t), "the dedup table fits the scripts");
 static_assert(kDedupSlots > kMaxChildren && kChildLds <= 256, "a free slot for every child, 8-bit child index");
@@ -487,21 +626,26 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
                                                          const float *__restrict__ value,
                                                          const double *__restrict__ noise, double eps,
                                                          float one_minus_eps, int testing,
-                                                         const int32_t *__restrict__ row_of) {
+                                                         const int32_t *__restrict__ row_of, int prio) {
   __shared__ ExpandLds L;
   int b = blockIdx.x;
   int lane = threadIdx.x;
   HZ_XSTAMP(0)
   HZ_XFLAG(10, 0)
   int leaf = m.leaf[b];
+  const int d = m.depth[b];
   if (leaf < 0) return;
   int32_t *cnt = m.counts + (size_t)b * 4;
   size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
+  const int32_t *path = m.path + (size_t)b * m.max_depth;
+  // the edge into the leaf: its hint gets the leaf's edges once expanded
+  // (loaded now, used at the end)
+  const int in_edge = d > 0 ? path[d - 1] : -1;
   State ls = load_node(m.node_state + (nb + leaf) * 6);
   int leaf_player = player_of(ls.misc);
   // policy/value row of this board: its own (per-board batch) or its row in
   // the gathered batch (hz_mcts_gather_leaves)
-  const size_t row = row_of ? (size_t)row_of[b] : (size_t)b;
+  const size_t row = (size_t)__builtin_amdgcn_readfirstlane(row_of ? row_of[b] : b);
   double v;
   if (game_done(ls.misc)) {
     // MCTS.py:333-341: outcome from the leaf player's perspective
@@ -516,6 +660,11 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
     HZ_XSTAMP(1)
     if (nl > 0 && nl <= kMaxChildren && m.node_ne[nb + leaf] == 0) {
       bool turn_end = phase_of(ls.misc) == PH_P3;
+      // the launch lasts as long as its slowest waves, the turn-end
+      // expansions (chance replay + ~21 children: ~58 k cycles median against
+      // ~41 k for the others, profiles/r03/expand_phases_spec_draws.json);
+      // they take issue priority over the three other waves of their SIMD
+      if (turn_end && prio) __builtin_amdgcn_s_setprio(2);
       HZ_XFLAG(10, 1 | (turn_end ? 2 : 0) | (nl << 8))
       if (turn_end) {
         // the children's _end_turn_actions draw from the board's stream in
@@ -558,18 +707,16 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
         __syncthreads();  // the stream copy is read before the children's states overwrite it
       }
       HZ_XSTAMP(2)
-      // the board's counters and the children's priors are loaded here, their
-      // latency hidden under the children's rule work (the counters are
-      // written by this wave alone, at the end)
-      const int gen = cnt[2], base_n = cnt[0], base_e = cnt[1];
-      float prior[2] = {0.f, 0.f};
-      // children: lane handles child c = lane and lane + 64
-#pragma unroll
+      // the children's priors are loaded here, their latency hidden under
+      // the children's rule work
+      // children: lane handles child c = lane and lane + 64 (one at a time:
+      // the rule work of two children at once held 38 more registers than fit)
+#pragma unroll 1
       for (int r = 0; r < 2; r++) {
         const int c = lane + r * kWave;
         if (c < nl) {
           int a = kth_action(mk, c);
-          prior[r] = policy[row * kActions + a];
+          L.prior[c] = policy[row * kActions + a];
           State ch = ls;
           ScriptDraw sd{turn_end ? L.script[c] : ~0ull};
           step_state(ch, a, sd);
@@ -587,6 +734,10 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
       }
       __syncthreads();
       HZ_XSTAMP(3)
+      // the board's counters (written by this wave alone, at the end); loaded
+      // after the children's rule work, whose registers they would have held
+      const int gen = __builtin_amdgcn_readfirstlane(cnt[2]), base_n = __builtin_amdgcn_readfirstlane(cnt[0]),
+                base_e = __builtin_amdgcn_readfirstlane(cnt[1]);
       // transpositions (MCTS.py:177-204): a child whose key is already in the
       // tree reuses that node (flag 1), or is skipped if it is the leaf itself
       // (flag 2) ...
@@ -600,24 +751,21 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           uint64_t e = ht[slot];
           if ((int)(e >> 32) != gen) break;
           int nid = (int)(uint32_t)e;
-          if (m.node_hash[nb + nid] != h) continue;
-          // equal state words give equal keys: the common transposition (the
-          // same tiles placed in another order) is accepted without building
-          // the node's canonical key, which costs more than the rest of a probe
-          const uint64_t *ns = m.node_state + (nb + nid) * 6;
-          bool same = true;
+          // the node's stored canonical key against the child's (one memory
+          // round trip after the table's; no key is rebuilt from a state)
+          const uint64_t *nk = m.node_key + (nb + nid) * 8;
+          const int nne = m.node_ne[nb + nid], ne0 = m.node_e0[nb + nid];  // (same round trip)
+          bool eq = true;
 #pragma unroll
-          for (int w = 0; w < 6; w++) same = same && ns[w] == L.state[c][w];
-          bool eq = same;
-          if (!same) {
-            CKey k;
-#pragma unroll
-            for (int w = 0; w < 8; w++) k.w[w] = L.key[c][w];
-            eq = key_eq(canon_key(load_node(ns), !m.exact_keys), k);
-          }
+          for (int w = 0; w < 8; w++) eq = eq && nk[w] == L.key[c][w];
           if (eq) {
             L.flag[c] = nid == leaf ? 2 : 1;
             L.child[c] = nid;
+            // the edge's hint: the node's own edges and terminal mark (its
+            // stored state decides, as the reference's Node does: equal keys
+            // do not imply equal game_over); kept in the child's hash word,
+            // which only new children read from here on
+            L.hash[c] = (uint64_t)(uint32_t)edge_hint_of(nne > 0 ? ne0 : 0, nne > 0 ? nne : 0, nne < 0);
             break;
           }
         }
@@ -735,9 +883,10 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
             uint64_t *ns = m.node_state + (nb + node_id) * 6;
 #pragma unroll
             for (int w = 0; w < 6; w++) ns[w] = L.state[c][w];
-            m.node_hash[nb + node_id] = L.hash[c];
+#pragma unroll
+            for (int w = 0; w < 8; w++) m.node_key[(nb + node_id) * 8 + w] = L.key[c][w];
             m.node_e0[nb + node_id] = 0;
-            m.node_ne[nb + node_id] = 0;
+            m.node_ne[nb + node_id] = game_done(L.state[c][5]) ? -1 : 0;  // -1: terminal (never expanded)
             for (uint64_t slot = L.hash[c] & hmask;; slot = (slot + 1) & hmask) {
               unsigned long long old = ht[slot];
               if ((int)(old >> 32) == gen) continue;
@@ -748,7 +897,7 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
           }
           if (f != 2) {
             int a = kth_action(mk, c);
-            float p = prior[r];
+            float p = L.prior[c];
             if (noisy) p = __double2float_rn(__dadd_rn((double)__fmul_rn(one_minus_eps, p),
                                                        __dmul_rn(eps, noise[(size_t)b * kMaxChildren + c])));
             int e = base_e + (L.flag[c] >> 4);
@@ -758,11 +907,18 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
             m.edge_w[eb + e] = 0.0;
             m.edge_p[eb + e] = p;
             m.edge_player[eb + e] = (uint8_t)leaf_player;
+            // the child node's edges and terminal mark: an existing node's
+            // from the probe; a new node has no edges, and is terminal as the
+            // state it was created from (a sibling duplicate's: its target's)
+            m.edge_hint[eb + e] =
+                f == 1 ? (int32_t)(uint32_t)L.hash[c]
+                       : edge_hint_of(0, 0, game_done(L.state[f == 3 ? L.child[c] : c][5]));
           }
         }
         if (lane == 0) {
           m.node_e0[nb + leaf] = base_e;
           m.node_ne[nb + leaf] = n_edges;
+          if (in_edge >= 0) m.edge_hint[eb + in_edge] = edge_hint_of(base_e, n_edges, false);
           cnt[0] = base_n + n_new;
           cnt[1] = base_e + n_edges;
         }
@@ -774,8 +930,6 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
   HZ_XSTAMP(6)
   // back_fill: every path edge gets N += 1, W += v * (+1 if the edge's mover
   // is the leaf's player else -1)
-  int d = m.depth[b];
-  const int32_t *path = m.path + (size_t)b * m.max_depth;
   // (the path's edges are distinct: the adds are read-modify-writes done by
   // the memory side, one round trip less; the f64 add rounds as __dadd_rn)
   for (int i = lane; i < d; i += kWave) {
@@ -898,9 +1052,10 @@ hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, 
   m->exact_keys = exact_keys;
   m->stream = (hipStream_t)stream;
   size_t n = (size_t)n_boards, N = n * max_nodes, E = n * m->max_edges;
-  bool ok = alloc(&m->node_state, N * 6) && alloc(&m->node_hash, N) && alloc(&m->node_e0, N) &&
+  bool ok = alloc(&m->node_state, N * 6) && alloc(&m->node_key, N * 8) && alloc(&m->node_e0, N) &&
             alloc(&m->node_ne, N) && alloc(&m->edge_action, E) && alloc(&m->edge_child, E) &&
             alloc(&m->edge_n, E) && alloc(&m->edge_w, E) && alloc(&m->edge_p, E) && alloc(&m->edge_player, E) &&
+            alloc(&m->edge_hint, E) &&
             alloc(&m->ht, n * m->hcap) && alloc(&m->counts, n * 4) && alloc(&m->path, n * max_depth) &&
             alloc(&m->depth, n) && alloc(&m->leaf, n) && alloc(&m->leaf_gidx, n) && alloc(&m->slot, n) &&
             alloc(&m->gidx_c, n);
@@ -920,8 +1075,8 @@ hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, 
 
 void hz_mcts_destroy(hz_mcts *m) {
   if (!m) return;
-  void *ptrs[] = {m->node_state, m->node_hash, m->node_e0,   m->node_ne, m->edge_action, m->edge_child,
-                  m->edge_n,     m->edge_w,    m->edge_p,    m->edge_player, m->ht, m->counts,
+  void *ptrs[] = {m->node_state, m->node_key, m->node_e0,   m->node_ne, m->edge_action, m->edge_child,
+                  m->edge_n,     m->edge_w,    m->edge_p,    m->edge_player, m->edge_hint, m->ht, m->counts,
                   m->path,       m->depth,     m->leaf,      m->leaf_gidx, m->slot, m->gidx_c};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -979,6 +1134,17 @@ int hz_mcts_select_gather(hz_mcts *m, const uint8_t *active, float cpuct, float 
 
 int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, int32_t *count) {
   if (!m || !count || (!board && !glob)) return -1;
+  // default: k_gather_encode (one launch); HZ_GATHER_ENCODE=0: k_gather + the
+  // encoder launches (same results)
+  static const bool fused = [] {
+    const char *e = getenv("HZ_GATHER_ENCODE");
+    return !(e && atoi(e) == 0);
+  }();
+  if (fused && board && glob) {
+    hipLaunchKernelGGL(k_gather_encode, dim3((m->n + kGERows - 1) / kGERows), dim3(kGEThreads), 0, m->stream, *m,
+                       rows, count, board, glob);
+    return launch_err();
+  }
   hipLaunchKernelGGL(k_gather, dim3(1), dim3(kGatherThreads), 0, m->stream, *m, rows, count);
   launch_encode(m->node_state, 1, 6, m->gidx_c, m->n, board, glob, m->stream, count);
   return launch_err();
@@ -995,12 +1161,17 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
     const char *e = getenv("HZ_EXPAND_WAVES");
     return e && atoi(e) == 3 ? 3 : 4;
   }();
+  // HZ_EXPAND_PRIO=0: the turn-end waves keep the default issue priority (A/B)
+  static const int prio = [] {
+    const char *e = getenv("HZ_EXPAND_PRIO");
+    return e && atoi(e) == 0 ? 0 : 1;
+  }();
   if (waves == 4)
     hipLaunchKernelGGL(k_expand_backup<4>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
+                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio);
   else
     hipLaunchKernelGGL(k_expand_backup<3>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot);
+                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio);
   return launch_err();
 }
 

@@ -39,6 +39,7 @@ _SIGS = {
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_play": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_env_set_seed_ahead": ([_vp, _c.c_int32], _c.c_int),
+    "hz_env_set_pipeline": ([_vp, _c.c_int32], _c.c_int),
     "hz_greedy_actions": ([_vp, _vp, _vp], _c.c_int),
     "hz_export_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_import_state": ([_vp, _vp, _vp, _vp], _c.c_int),

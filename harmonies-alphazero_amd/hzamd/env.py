@@ -56,6 +56,12 @@ class BatchedEnv:
         `draws` pile draws) on/off; results are identical either way."""
         nat.check(nat.lib().hz_env_set_seed_ahead(self._h, int(draws) if enable else 0), "hz_env_set_seed_ahead")
 
+    def set_pipeline(self, pipeline):
+        """hz_play's pipeline: 1 = chance-ahead (k_rollout), 2 = every game
+        spread over seven consecutive calls (k_play2); results are identical
+        either way (hz_env_set_pipeline)."""
+        nat.check(nat.lib().hz_env_set_pipeline(self._h, int(pipeline)), "hz_env_set_pipeline")
+
     # -- env surface ---------------------------------------------------------
     def reset(self, sel=None, seeds=None):
         """HarmoniesGameState() on every board (or on boards where sel != 0)."""

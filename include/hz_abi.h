@@ -138,6 +138,15 @@ int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_s
 /* chance-ahead for hz_play: draws = piles prepared per board (0 = off,
  * capped at 24 = the default). */
 int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
+/* hz_play's pipeline: 1 (default; HZ_PIPELINE=2 in the environment at
+ * hz_env_create makes 2 the default) = the chance-ahead pipeline above;
+ * 2 = every board's game spread over seven consecutive calls, one stage per
+ * call (seeding pass 1, pass 2, three draw stages, the first 40 plies, the
+ * rest), all seven running in each launch on different episodes.  Same
+ * results as pipeline 1; applies to calls with auto_reset = 0, no trajectory
+ * outputs and max_plies >= 96 (others take pipeline 1).  Returns -1 for a
+ * value other than 1 or 2. */
+int hz_env_set_pipeline(hz_env *env, int32_t pipeline);
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
 /* export: state[6][n] and, optionally, the MT streams in CPython getstate()
@@ -252,7 +261,9 @@ int hz_conv3x3_x6_bias_act(const float *x, const void *wpack6, const float *bias
  * hz_conv3x3_x6_bias_act(x, w1, b1, NULL, tmp) followed by
  * hz_conv3x3_x6_bias_act(tmp, w2, b2, x, out); in its one-launch form
  * (hz_resblock_x6_fused(batch) == 1) the intermediate activation stays on
- * the CU (tmp holds half of it, briefly). */
+ * the CU (tmp holds half of it, briefly: a [2][288][32]-float slice per
+ * 8-state group, which the one-launch form is taken only to fit in the
+ * batch*35*128 floats above, i.e. never below 5 rows). */
 int hz_resblock_x6_bias_act(const float *x, const void *w1, const float *b1, const void *w2, const float *b2,
                             float *out, float *tmp, int32_t batch, const int32_t *live, void *stream);
 int32_t hz_resblock_x6_fused(int32_t batch);

@@ -188,6 +188,58 @@ def test_play_seed_ahead_pipeline(Env, ahead, draws):
         _check_episode(env, base, ep, steps)
 
 
+@pytest.mark.parametrize("draws", [24, 19, 3, 0])
+def test_play_pipeline2(Env, draws):
+    """hz_play's second pipeline (k_play2: seeding pass 1, pass 2, three draw
+    stages, plies 0-39, the rest, one stage per call on seven episodes at
+    once): ten consecutive calls (the first six fill the stages, from the
+    seventh every board replays a fully prepared episode), an hz_reset +
+    hz_rollout (re-primes: the hand-off slots then hold stale episodes), then
+    eight more calls; every game, ply count and stream bit-exact vs the
+    oracle's episode.  draws < 19 runs games past their pile scripts onto the
+    stream slots; 0 prepares no script at all."""
+    n, base = 4096, 4242
+    env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(2)
+    env.set_seed_ahead(draws > 0, draws)
+    for ep in range(10):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+    env.reset()
+    _, steps, _ = env.rollout(200)
+    _check_episode(env, base, 10, steps)
+    for ep in range(11, 19):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+
+
+def test_play_pipeline2_partial_block_and_switch(Env):
+    """Pipeline 2 with a partial block (1000 boards), switched to pipeline 1
+    and back mid-stream (each pipeline's hand-offs go stale while the other
+    runs), and after an auto-reset call that moves counters board by board."""
+    n, base = 1000, 99
+    env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(2)
+    ep = 0
+    for pipe, calls in ((2, 8), (1, 2), (2, 9)):
+        env.set_pipeline(pipe)
+        for _ in range(calls):
+            _, steps, _ = env.rollout(200, reset=True)
+            _check_episode(env, base, ep, steps)
+            ep += 1
+    games, _, _ = env.rollout(64, auto_reset=True, reset=True)  # episode ep, then maybe ep + 1
+    resets = games.cpu().numpy() - env.done().cpu().numpy().astype(np.int64)
+    nxt_ep = ep + 1 + resets
+    _, steps, _ = env.rollout(200, reset=True)
+    st = states_of(env)
+    steps = steps.cpu().numpy()
+    for e in sorted(set(nxt_ep.tolist())):
+        _, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=int(e))
+        sel = nxt_ep == e
+        assert (st[sel] == finals[sel]).all(), e
+        assert (steps[sel] == plies[sel]).all(), e
+
+
 def test_play_pipeline_partial_block(Env):
     """hz_play's pipeline with a board count that leaves a partial block
     (1000 = 15 x 64 + 40): ring slots padded to whole blocks, play slots

@@ -135,6 +135,95 @@ __device__ __forceinline__ uint32_t pass2(uint32_t *w, uint32_t prev) {
   return prev ^ acc;
 }
 
+// random.seed(int) (init_by_array) with every word in global memory,
+// word-major w[i * ns]: the chain wave issues no LDS operation (its stores
+// are fire-and-forget vector stores; pass 2 reads its pass-1 words PF steps
+// ahead), init_genrand's table through the scalar cache (no LDS waits mix
+// with it).  Same words as mt_seed.
+template <int PF>
+__device__ __forceinline__ void mt_seed_global(uint32_t *w, size_t ns, uint64_t seed) {
+  const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  const uint32_t kA = key0, kB = key1 ? key1 + 1u : key0;
+  uint32_t prev = 19650218u, m1 = 0;
+  for (int g = 1; g < kMT - 7; g += 8) {  // i = 1..616
+    uint32_t iv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[g + u];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      w[(size_t)(g + u) * ns] = v;
+      if (u == 0 && g == 1) m1 = v;
+      prev = v;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // i = 617..623
+    const uint32_t v = (kInitGen.v[617 + u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(size_t)(617 + u) * ns] = v;
+    prev = v;
+  }
+  // mt[0] = mt[623]; the 624th step at i = 1 (key j = 623 % keylen -> kB)
+  prev = (m1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+  const uint32_t first1 = prev;
+  // pass 2: i = 2..623 over the pass-1 words, read PF steps ahead
+  uint32_t ring[PF];
+#pragma unroll
+  for (int u = 0; u < PF; u++) ring[u] = w[(size_t)(2 + u) * ns];
+  for (int g = 2; g < 2 + ((kMT - 2) / PF) * PF; g += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      const uint32_t cur = ring[u];
+      const int nx = g + PF + u;
+      ring[u] = nx < kMT ? w[(size_t)nx * ns] : 0u;
+      const uint32_t v = (cur ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
+      w[(size_t)(g + u) * ns] = v;
+      prev = v;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < (kMT - 2) % PF; u++) {
+    const int i = 2 + ((kMT - 2) / PF) * PF + u;
+    const uint32_t v = (ring[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    w[(size_t)i * ns] = v;
+    prev = v;
+  }
+  w[ns] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
+  w[0] = 0x80000000U;
+}
+
+template <int PF>
+__global__ void __launch_bounds__(64) k_seedglob(uint32_t *out, uint64_t *cyc, uint32_t *ws, size_t ns) {
+  const int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
+  const uint64_t sd = 1234 + (uint64_t)b;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  mt_seed_global<PF>(ws + b, ns, sd);
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[b] = ws[7 * ns + b];
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+// the same seeds through mt_seed (LDS), for the comparison of the words
+__global__ void __launch_bounds__(64) k_seedref(uint32_t *ws, size_t ns) {
+  const int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
+  mt_seed(hz_lds + lane, 64, 1234 + (uint64_t)b);
+  __syncthreads();
+  for (int i = 0; i < kMT; i++) ws[(size_t)i * ns + b] = hz_lds[i * 64 + lane];
+}
+
+extern "C" int seed_glob(int pf, void *out, void *cyc, void *ws, long ns, int blocks) {
+  dim3 g(blocks), b(64);
+  if (pf == 8) hipLaunchKernelGGL(k_seedglob<8>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, (uint32_t *)ws, (size_t)ns);
+  else if (pf == 16) hipLaunchKernelGGL(k_seedglob<16>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, (uint32_t *)ws, (size_t)ns);
+  else if (pf == 24) hipLaunchKernelGGL(k_seedglob<24>, g, b, 0, 0, (uint32_t *)out, (uint64_t *)cyc, (uint32_t *)ws, (size_t)ns);
+  else if (pf == 0) {
+    size_t lds = (size_t)kMT * 64 * 4;
+    hipFuncSetAttribute((const void *)k_seedref, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_seedref, g, b, lds, 0, (uint32_t *)ws, (size_t)ns);
+  } else return -1;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) k_seedvar(uint32_t *out, uint64_t *cyc) {
   extern __shared__ uint32_t lds[];
