@@ -6,6 +6,7 @@
 // element-parallel instead (it writes 5,488 B per board and is HBM-bound).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -14,6 +15,21 @@
 #include "hz_encode.hpp"
 
 using namespace hz;
+
+// pipeline-2 hand-offs (k_play2), per board, rows of nrow
+struct P2Draw {   // a draw stage's output: the pile script so far
+  int32_t *tag;   // [nrow] episode * 8 + draw stages done
+  int32_t *k;     // [nrow] draws done
+  uint64_t *q;    // [4][nrow] the script: draw i at bits 9 i ..
+  uint64_t *bag;  // [nrow] bag fields (misc layout) after those draws
+  int32_t *c;     // [nrow] stream cursor after those draws
+};
+struct P2Mid {    // a play stage's end state, for the next play stage
+  int32_t *tag;   // [nrow] episode
+  uint64_t *st;   // [6][nrow] state
+  uint64_t *q;    // [4][nrow] the rest of the script
+  int32_t *i;     // [3][nrow] script entries used, plies played, stream cursor if fell (else -1)
+};
 
 struct hz_env {
   int32_t n;
@@ -50,23 +66,21 @@ struct hz_env {
   int32_t *mt_src;           // [n]
   int lazy;                  // some board may have mt_src >= 0
   // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
-  // spread over seven consecutive hz_play calls, one stage per call
+  // spread over eleven consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
   int calls2, primed2;
-  uint32_t *p2_s[8];         // [624][nrow] streams: seeded (pass 1, then 2), rows [0, 224) pre-twisted
-  int32_t *p2_s_tag[8];      // [nrow] episode * 4 + 1 (pass 1 done) / + 2 (seeded, pre-twisted)
-  int32_t *p2_d_tag[7];      // draw hand-offs AB[2], BC[2], PL[3]: [nrow] episode * 4 + stage
-  int32_t *p2_d_k[7];        // [nrow] draws done
-  uint64_t *p2_d_q[7];       // [4][nrow] the script so far
-  uint64_t *p2_d_bag[7];     // [nrow] bag fields after those draws
-  int32_t *p2_d_cur[7];      // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
-  int32_t *p2_m_tag[2];      // playA -> playB: [nrow] episode
-  uint64_t *p2_m_st[2];      // [6][nrow] state after the first kP2Half plies
-  uint64_t *p2_m_q[2];       // [4][nrow] the rest of the script
-  int32_t *p2_m_i[2];        // [3][nrow] script entries used, plies played, stream cursor if fell (else -1)
-  uint32_t *p2_h[3];         // [kRulePlies][nrow] rule hashes
-  int32_t *p2_h_tag[3];      // [nrow] episode
-  int32_t *p2_ep[2];         // [n] episode counter each board ended the call with
+  int p2_cut1, p2_cut2;      // the play stages' ply boundaries (HZ_P2_CUTS)
+  uint32_t *p2_s[12];        // [624][nrow] stream slots (kP2Stream)
+  int32_t *p2_s_tag[12];     // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 seeded, rows 0-223 twisted
+  int32_t *p2_s_cur[12];     // [kAheadDraws + 1][nrow] the slot's cursor before draw 0 and after each draw
+  uint32_t *p2_p1h[2];       // [nrow] P1a -> P1b
+  uint32_t *p2_p2h[2];       // [2][nrow] P2a -> P2b
+  P2Draw p2_x[3][2];         // D1 -> D2 -> D3 -> D4, by call parity
+  P2Draw p2_pl[4];           // D4 -> playA, playB, playC: a ring of four
+  P2Mid p2_m[2][2];          // playA -> playB, playB -> playC, by call parity
+  uint32_t *p2_h[4];         // [kRulePlies][nrow] rule hashes, a ring of four
+  int32_t *p2_h_tag[4];      // [nrow] their episode
+  int32_t *p2_ep[2];         // [nrow] episode counter each board ended the call with
 };
 
 #ifdef HZ_DIAG
@@ -1080,69 +1094,85 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // hz_play's second pipeline (hz_env_set_pipeline(e, 2)).  Each of
 // k_rollout's roles runs one serial per-board chain of ~60 k cycles (a whole
 // game, a whole seeding, 16 pile draws), and a launch lasts as long as its
-// longest chain.  Here every board's episode is cut into seven stages of
-// about half that, one per consecutive hz_play call, and one launch runs all
-// seven stages at once, each on a different episode of the board:
-//   seed blocks [2 nblk, 3 nblk): wave 0 P1 (init_by_array's pass 1,
-//     episode ep + 6), wave 1 P2 (pass 2 and the next generation's first 224
-//     words twisted, episode ep + 5), straight into the episode's stream slot
-//     in HBM (word-major: no LDS operation in either chain);
-//   draw blocks [nblk, 2 nblk): waves 0-2 the draw stages A (draws 0-7,
-//     episode ep + 4), B (8-15, ep + 3), C (16-23, ep + 2), each on its own
-//     LDS window of its episode's pre-twisted stream (rows [0, 192)); wave 3
-//     the rule hashes of episode ep + 2;
-//   play blocks [0, nblk): wave 1 playA (plies [0, 40) of episode ep + 1
-//     from its pile script), wave 0 playB (the rest of episode ep, final
-//     scoring, the board's state, cursor and counters).
-// ep = the episode counter the previous call left (p2_ep).  A stage uses an
-// input only when its tag names the stage's episode, so a wrong prediction
-// costs time, never results: the stages skip the board and playB plays its
-// whole game from scratch (seeding and drawing in LDS, like k_rollout's
-// unprepared boards).  In steady state a call seeds, draws and plays one
-// episode's worth per board: the work of one call is one game per board,
-// spread over seven episodes.  The results are k_rollout's: the board ends
+// longest chain.  Here every board's episode is cut into eleven stages of
+// 20-35 k cycles, one per consecutive hz_play call, and one launch runs all
+// eleven at once, each on a different episode of the board (ep = the episode
+// counter the previous call left, p2_ep; stage s works on episode ep + 10 - s):
+//   s = 0  P1a   seeding pass 1, steps 1-312          seed blocks, wave 0
+//   s = 1  P1b   pass 1, steps 313-624                draw-X blocks, wave 2
+//   s = 2  P2a   pass 2, steps 2-312 (LDS rows 1-312) seed blocks, wave 1
+//   s = 3  P2b   pass 2, steps 313-624 (rows 313-623) seed blocks, waves 2-3
+//                and rows 0-223 of the next generation twisted
+//   s = 4  D1    pile draws 0-5                       draw-X blocks, wave 0
+//   s = 5  D2    draws 6-11                           draw-X blocks, wave 1
+//   s = 6  D3    draws 12-17                          draw-Y blocks, wave 0
+//   s = 7  D4    draws 18-23                          draw-Y blocks, wave 1
+//          (the episode's rule hashes meanwhile:      play blocks, wave 3)
+//   s = 8  playA plies [0, cut1)                      play blocks, wave 2
+//   s = 9  playB plies [cut1, cut2)                   play blocks, wave 1
+//   s = 10 playC the rest, final scoring, the board's play blocks, wave 0
+//                state, cursor and counters
+// An episode's stream lives in one slot of a ring of kP2Stream from P1a to
+// playC (and afterwards as the board's current stream until materialize or
+// the next call); stage s of call c uses slot (c - s) mod kP2Stream.  A stage
+// uses an input only when its tag names the stage's episode, so a wrong
+// prediction costs time, never results: the stages skip the board and playC
+// plays its whole game from scratch (seeding and drawing in LDS, like
+// k_rollout's unprepared boards).  The results are k_rollout's: the board ends
 // the call with episode ep's final state, cursor and counters, and
-// games_done / steps_done count that game (its first plies ran one call
-// earlier, in playA).
-constexpr int kP2Win = 192;   // draw stages' LDS window rows (a draw reads <= 24 words past its cursor)
-constexpr int kP2Half = 40;   // playA's plies: five turn pairs
-constexpr int kP2Stream = 8;  // stream slots: written at call c (P1), used through c + 6, read by materialize
-constexpr int kP2MinPlies = 96;  // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
-// the windows fit the block's LDS, and a scan from a cursor <= kP2Win (rows
-// up to kP2Win + 23 past the last window's base) stays inside it
-static_assert(kP2Win <= kAheadTwist && (2 * kP2Win + kP2Win + 24) * kLdsStride * 4 <= (int)kResetLds, "windows fit");
-
-struct P2Draw {        // a draw stage's output / the play stages' pile script, per board
-  int32_t *tag;        // [nrow] episode * 4 + stage (1 A, 2 B, 3 C)
-  int32_t *k;          // [nrow] draws done
-  uint64_t *q;         // [4][nrow] the script: draw i at bits 9 i ..
-  uint64_t *bag;       // [nrow] bag fields (misc layout) after the draws
-  int32_t *cur;        // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
-};
+// games_done / steps_done count that game (its first plies ran in the two
+// calls before, in playA and playB).  In steady state a call does every
+// stage once per board: one game's worth of work per board per call.
+constexpr int kP2Win = 96;        // rows a draw stage stages, from its wave's lowest cursor
+constexpr int kP2WinRows = kP2Win + 24;  // LDS rows per window (a scan reads up to 23 rows past its cursor)
+constexpr int kP2Stages = 11;
+constexpr int kP2Stream = 12;     // stream slots (>= kP2Stages + 1: playC's slot stays the board's stream)
+constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
+constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
+constexpr int kP1Split = 313;
+#ifdef HZ_DIAG
+constexpr int kP2Stamps = 32;  // stamp slots per board in k_play2 (tools/p2_roles.py)
+#define P2_PHASE(slot, t0)                                                                                       \
+  do {                                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                                           \
+    if (g_stamps && b < a.n) g_stamps[(size_t)b * kP2Stamps + (slot)] = __builtin_amdgcn_s_memtime() - (t0); \
+    __builtin_amdgcn_sched_barrier(0);                                                                           \
+  } while (0)
+#else
+#define P2_PHASE(slot, t0) \
+  do {                     \
+  } while (0)
+#endif     // pass 1: P1a runs steps [1, 313), P1b [313, 624) and the 624th
+static_assert(4 * kP2DrawsPer == kAheadDraws, "four draw stages cover the script");
+static_assert(2 * kP2WinRows * kLdsStride * 4 <= (int)kResetLds, "two windows per draw block");
+static_assert((kP1Split - 1) % 8 == 0 && (617 - kP1Split) % 8 == 0, "pass-1 halves in groups of eight");
 
 struct P2Args {
   uint64_t *st;
   uint32_t *mt;
   int32_t *pos, *ply, *episode;
   uint64_t *seed;
-  int n, max_plies, draws;
+  int n, max_plies, draws, cut1, cut2;
   uint64_t seed_base;
   long nrow;
   int32_t *games_done, *steps_done, *mt_src;
   const int32_t *ep_in;
   int32_t *ep_out;
-  uint32_t *s_mt[7];   // stream slot of stage s (0 P1, 1 P2, 2-4 draws A-C, 5 playA, 6 playB)
-  int32_t *s_tag[7];
-  int s_idx6;          // playB's slot index (materialize: mt_src = 2 + index)
-  P2Draw ab_w, ab_r, bc_w, bc_r, pl_w, pl_a, pl_b;
-  int32_t *m_tag_w, *m_i_w;
-  const int32_t *m_tag_r, *m_i_r;
-  uint64_t *m_st_w, *m_q_w;
-  const uint64_t *m_st_r, *m_q_r;
-  uint32_t *h_w;
-  const uint32_t *h_a, *h_b;
-  int32_t *h_tag_w;
-  const int32_t *h_tag_a, *h_tag_b;
+  uint32_t *s_mt[kP2Stages];  // the stream slot of each stage this call
+  int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 seeded, rows 0-223 twisted
+  int32_t *s_cur[kP2Stages];  // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
+  int s_idx10;                // playC's slot index (materialize: mt_src = 2 + index)
+  uint32_t *p1h_w;            // [nrow] P1a -> P1b: pass 1's last value
+  const uint32_t *p1h_r;
+  uint32_t *p2h_w;            // [2][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word
+  const uint32_t *p2h_r;
+  P2Draw x_w[3], x_r[3];      // D1 -> D2 -> D3 -> D4 (tag: episode * 8 + stages done)
+  P2Draw pl_w, pl_a, pl_b, pl_c;  // D4's script: written this call; read by playA, playB, playC
+  P2Mid m1_w, m1_r, m2_w, m2_r;   // playA -> playB -> playC
+  uint32_t *h_w;                  // [kRulePlies][nrow] rule hashes
+  const uint32_t *h_a, *h_b, *h_c;
+  int32_t *ht_w;                  // [nrow] their episode
+  const int32_t *ht_a, *ht_b, *ht_c;
 };
 
 // PlayDraw for the prepared stages: the pile script in registers, then (a
@@ -1151,7 +1181,8 @@ struct PlayDraw2 {
   uint64_t q0, q1, q2, q3;
   int d, nd;
   bool fell;
-  MTR gm;
+  MTR gm;                  // valid once fell
+  const int32_t *cur_nd;   // the slot's cursor after the last scripted draw (read when the script runs out)
   __device__ __forceinline__ uint32_t pop() {
     uint32_t p9 = (uint32_t)q0 & 0x1FFu;
     q0 = (q0 >> 9) | (q1 << 55);
@@ -1164,7 +1195,10 @@ struct PlayDraw2 {
   __device__ __forceinline__ bool pair_pops() const { return d + 2 <= nd; }
   __device__ __forceinline__ uint32_t draw_one(uint64_t misc) {
     if (d < nd) return pop();
-    fell = true;
+    if (!fell) {
+      gm = MTR(gm.w, gm.stride, *cur_nd);
+      fell = true;
+    }
     uint32_t p9;
     return draw_pile(misc, gm, p9) ? p9 : 0x1FFu;
   }
@@ -1209,12 +1243,31 @@ __device__ __forceinline__ int p2_plies(State &s, Draw &draw, int g, int g_end, 
                                         size_t nr) {
   const int g0 = g;
   auto hash = [&](int ply) -> uint32_t { return hs && ply < kRulePlies ? hs[(size_t)ply * nr] : rule_h32(rkey, ply); };
+  // the next turn pair's hashes, read one pair ahead (a slot's are in HBM).
+  // Wave-uniform choices: a per-lane select would evaluate both sides, i.e.
+  // compute all eight hashes and issue their loads every pair.
+  const bool all_hs = __all(hs != nullptr);
+  uint32_t hn[8];
+  int hn_g = -1;  // (wave-uniform)
   while (g < g_end) {
     if (phase_of(s.misc) == PH_OVER) break;
     if (__all(g + 8 <= g_end && turn_pair_safe(s))) {
       uint32_t h[8];
+      if (__all(hn_g == g)) {
 #pragma unroll
-      for (int j = 0; j < 8; j++) h[j] = hash(g + j);
+        for (int j = 0; j < 8; j++) h[j] = hn[j];
+      } else if (all_hs && __all(g + 8 <= kRulePlies)) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = hs[(size_t)(g + j) * nr];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = hash(g + j);
+      }
+      if (all_hs && __all(g + 16 <= g_end && g + 16 <= kRulePlies)) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) hn[j] = hs[(size_t)(g + 8 + j) * nr];
+        hn_g = __builtin_amdgcn_readfirstlane(g + 8);
+      }
       int done = 4;
       if (__all(draw.pair_pops())) {
         play_turn_h<0, Draw, true>(s, draw, h[0], h[1], h[2], h[3]);
@@ -1240,19 +1293,6 @@ __device__ __forceinline__ int p2_plies(State &s, Draw &draw, int g, int g_end, 
   return g - g0;
 }
 
-// P2 in LDS: pass 2 is a serial chain whose every step reads the next
-// pass-1 word, too close ahead for an HBM round trip (pass 2 straight from
-// the slot took ~100 k cycles), so the seed block's LDS holds the 64 streams
-// ([624][65]): wave 2 stages the pass-1 words in row order ahead of the
-// chain (s_in: rows [0, s_in) present), wave 1 runs pass 2 and the
-// pre-twist in LDS (s_out: rows [2, s_out) final; kMT + 1 once all are),
-// wave 3 stores the final rows [kAheadTwist, kMT) back as they come, and
-// after the pre-twist waves 2 and 3 store rows [0, kAheadTwist).  A wave's
-// LDS operations execute in order, so a counter stored after its rows is
-// seen after them (SeedProgress's reasoning); readers load with acquire.
-struct P2Flags {
-  int in, out;
-};
 __device__ __forceinline__ int p2_wait(int *flag, int need) {
   int v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
   // every publisher reaches kMT + 1 (or kMT rows); the bound only guards
@@ -1267,216 +1307,445 @@ __device__ __forceinline__ void p2_publish(int *flag, int v) {
   asm volatile("" ::: "memory");
   __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// rows [r0, r1) of the block's 64 boards between LDS [row][65] and the slot
-// (16-B accesses, four boards of a row per lane: a wave covers four rows)
-template <bool ToLds>
-__device__ __forceinline__ void p2_rows(uint32_t *__restrict__ slot, size_t nr, int b0, int lane, int r0, int r1) {
-  constexpr int U = 16;
-  const int c4 = (lane & 15) * 4;
-  for (int q0 = r0; q0 < r1; q0 += 4 * U) {
+// init_by_array's pass 1, steps [i0, i1) (i0 odd, groups of eight: odd
+// steps take key word kA, even ones kB), rows at w[i * ns]; step 1's value
+// goes to row 1 (the 624th step reads it back)
+// (wb = the slot's column of the wave's first board, wave-uniform, so a
+// row's address is a scalar base plus the lane: no 64-bit address
+// arithmetic per step in the chain)
+__device__ __forceinline__ void mt_pass1_span(uint32_t *__restrict__ wb, int lane, size_t ns, uint32_t kA, uint32_t kB,
+                                              int i0, int i1, uint32_t &prev) {
+  // init_genrand's table words a group ahead (scalar loads: their wait
+  // would otherwise sit in the chain once per group)
+  uint32_t iv[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[i0 + u];
+#pragma unroll 1
+  for (int g = i0; g < i1; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      wb[(size_t)(g + u) * ns + lane] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = nx[u];
+  }
+}
+__device__ __forceinline__ void p2_keys(uint64_t seed, uint32_t &kA, uint32_t &kB) {
+  const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  kA = key0;
+  kB = key1 ? key1 + 1u : key0;
+}
+
+// P1a (seed blocks, wave 0) and P1b (draw-X blocks, wave 2): no LDS
+__device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
+  const int b = b0 + lane;
+  const size_t nr = (size_t)a.nrow;
+  const int e = a.ep_in[b] + 10;
+  uint32_t kA, kB;
+  p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
+  uint32_t prev = 19650218u;
+  mt_pass1_span(a.s_mt[0] + b0, lane, nr, kA, kB, 1, kP1Split, prev);
+  a.p1h_w[b] = prev;
+  a.s_tag[0][b] = e * 8 + 1;
+}
+__device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
+  const int b = b0 + lane;
+  const size_t nr = (size_t)a.nrow;
+  const int e = a.ep_in[b] + 9;
+  if (a.s_tag[1][b] != e * 8 + 1) return;
+  uint32_t kA, kB;
+  p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
+  uint32_t prev = a.p1h_r[b];
+  uint32_t *w = a.s_mt[1] + b;
+  mt_pass1_span(a.s_mt[1] + b0, lane, nr, kA, kB, kP1Split, 617, prev);
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // steps 617..623
+    const uint32_t v = (kInitGen.v[617 + u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(size_t)(617 + u) * nr] = v;
+    prev = v;
+  }
+  // mt[0] = mt[623]; the 624th step at i = 1 (key j = 623 % keylen -> kB)
+  w[nr] = (w[nr] ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+  a.s_tag[1][b] = e * 8 + 2;
+}
+
+// Pass 2 in two halves, P2a (steps 2-312) and P2b (steps 313-623 and the
+// last step at i = 1), in one seed block.  Every step reads the next pass-1
+// word, too close ahead for an HBM round trip (a chain reading the slot
+// through a register ring stalled on the memory counter: ~220 k cycles),
+// and a chain that spends a memory instruction per step is bound by their
+// issue (one LDS read and one LDS write per step: ~79 cycles a step; an LDS
+// read and an HBM store: ~72), so the block's LDS holds each board's words
+// transposed: lane l's column of R words at l * kP2RS (P2a: rows [0, 316),
+// P2b: rows [312, 628) - 312 in the second region), four rows per 16-B
+// access (kP2RS / 4 odd: the 64 lanes' 16-B accesses spread over all banks).
+// A chain reads four pass-1 words and writes four final words per LDS
+// operation (in place, the read-ahead past the rows written).  Pass-1 rows
+// arrive in three pieces (dword loads, one row of the wave's 64 boards per
+// load, the next piece in flight while the chain works through the
+// current one); final rows leave through coalesced dword stores (P2a's at
+// its end, P2b's by wave 0 as they are published).
+constexpr int kP2aEnd = 313;
+constexpr int kP2RS = 316;                   // words per lane column
+constexpr int kP2Reg = 64 * kP2RS;           // words per region
+constexpr int kP2bBase = 312;                // P2b region row 0 = absolute row 312
+static_assert(2 * kP2Reg * 4 <= (int)kResetLds && (kP2RS / 4) % 2 == 1, "two transposed regions");
+// LDS word of (region base, lane, absolute row - region row 0)
+__device__ __forceinline__ uint32_t *p2_col(int reg, int lane) { return hz_lds + reg + lane * kP2RS; }
+// rows [R0, R1) (R0 % 4 == 0) of the wave's 64 boards, pass 1 -> the lanes'
+// columns (rel = region row 0): dword loads, 16-B LDS writes
+template <int R0, int R1, int REL>
+struct P2Piece {
+  static constexpr int N = R1 - R0;
+  static_assert(R0 % 4 == 0 && (R0 - REL) % 4 == 0, "aligned groups of four rows");
+  uint32_t v[(N + 3) / 4 * 4];
+  __device__ __forceinline__ void load(const uint32_t *__restrict__ slot, size_t nr, int b0, int lane) {
+#pragma unroll
+    for (int k = 0; k < N; k++) v[k] = slot[(size_t)(R0 + k) * nr + b0 + lane];
+  }
+  __device__ __forceinline__ void put(uint32_t *col) const {
+#pragma unroll
+    for (int k = 0; k < N; k += 4)
+      *reinterpret_cast<uint4 *>(col + R0 - REL + k) =
+          make_uint4(v[k], k + 1 < N ? v[k + 1] : 0u, k + 2 < N ? v[k + 2] : 0u, k + 3 < N ? v[k + 3] : 0u);
+  }
+};
+// final rows [r0, r1) of the lane's column (rows from REL) -> the slot,
+// coalesced dword stores (one row of 64 boards each); r0 % 4 == 0; eight
+// groups of four rows per batch, the batch's LDS reads issued first
+template <int REL>
+__device__ __forceinline__ void p2_out(const uint32_t *col, uint32_t *__restrict__ slot, size_t nr, int b0, int lane,
+                                       int r0, int r1) {
+  constexpr int B = 8;
+#pragma unroll 1
+  for (int rb = r0; rb < r1; rb += 4 * B) {  // (wave-uniform)
+    uint4 q[B];
+#pragma unroll
+    for (int k = 0; k < B; k++)
+      if (rb + 4 * k < r1) q[k] = *reinterpret_cast<const uint4 *>(col + rb + 4 * k - REL);
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const int r = rb + 4 * k;
+      if (r < r1) {
+        uint32_t *o = slot + (size_t)r * nr + b0 + lane;
+        o[0] = q[k].x;
+        if (r + 1 < r1) o[nr] = q[k].y;
+        if (r + 2 < r1) o[2 * nr] = q[k].z;
+        if (r + 3 < r1) o[3 * nr] = q[k].w;
+      }
+    }
+  }
+}
+// steps [G0, G1) of pass 2 (the first and last groups of four rows may be
+// partial) on the lane's column `col` (rows from REL): four words per LDS
+// read, kP2Ahead groups (24 rows, ~400 cycles of chain) ahead, four final
+// words per LDS write; reads stay below RL (the rows staged); with prog,
+// progress published every 8 steps
+constexpr int kP2Ahead = 6;
+template <int G0, int G1, int RL, int REL>
+__device__ __forceinline__ void p2_chain(uint32_t *col, uint32_t &prev, int *prog) {
+  constexpr int D = kP2Ahead, Q0 = G0 & ~3;
+  uint4 c[D];
+#pragma unroll
+  for (int d = 0; d < D; d++)
+    c[d] = Q0 + 4 * d < RL ? *reinterpret_cast<const uint4 *>(col + Q0 + 4 * d - REL) : make_uint4(0, 0, 0, 0);
+#pragma unroll 1
+  for (int q0 = Q0; q0 < G1; q0 += 4 * D) {
+    const uint32_t kq = __builtin_amdgcn_readfirstlane(0u - (uint32_t)q0);
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      const int q = q0 + 4 * d;
+      if (q < G1) {  // (wave-uniform)
+        uint32_t w[4] = {c[d].x, c[d].y, c[d].z, c[d].w};
+        c[d] = q + 4 * D < RL ? *reinterpret_cast<const uint4 *>(col + q + 4 * D - REL) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = q + u;
+          if (i >= G0 && i < G1) {  // (wave-uniform: only the first and last groups are partial)
+            const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
+            uint32_t v;
+            // (cur ^ p) - i as one v_xad_u32 with the offset in an SGPR
+            asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(w[u]), "s"(kq - (uint32_t)(4 * d + u)));
+            w[u] = v;
+            prev = v;
+          }
+        }
+        *reinterpret_cast<uint4 *>(col + q - REL) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (prog && (q & 4)) p2_publish(prog, q + 4 < G1 ? q + 4 : G1);  // rows [., q + 4) final
+      }
+    }
+  }
+}
+
+// P2a (seed blocks, wave 1): episode ep + 8, whose pass 1 completed in the
+// previous call; hands pass 2's state (prev, and pass 1's row-1 word) to P2b
+__device__ __forceinline__ void p2_p2a(const P2Args &a, int b0, int lane) {
+  const int b = b0 + lane;
+  const bool act = b < a.n;
+  const size_t nr = (size_t)a.nrow;
+  const int e = act ? a.ep_in[b] + 8 : 0;
+  const bool ok = act && a.s_tag[2][b] == e * 8 + 2;
+  if (!__any(ok)) return;
+  uint32_t *slot = a.s_mt[2];
+  uint32_t *col = p2_col(0, lane);
+#ifdef HZ_DIAG
+  const uint64_t tq = __builtin_amdgcn_s_memtime();
+#endif
+  {
+    P2Piece<0, 104, 0> p0;  // (row 0: pass 1 leaves it unused here; loaded for the alignment)
+    p0.load(slot, nr, b0, lane);
+    p0.put(col);
+  }
+  P2Piece<104, 208, 0> p1;
+  p1.load(slot, nr, b0, lane);
+#ifdef HZ_DIAG
+  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 7] = __builtin_amdgcn_s_memtime() - tq;  // P2a staged
+#endif
+  const uint32_t first1 = col[1];
+  uint32_t prev = first1;
+  p2_chain<2, 96, 104, 0>(col, prev, nullptr);  // steps 2..95 (reads below row 104)
+  p1.put(col);
+  P2Piece<208, kP2aEnd, 0> p2;
+  p2.load(slot, nr, b0, lane);
+  p2_chain<96, 200, 208, 0>(col, prev, nullptr);  // 96..199
+  p2.put(col);
+  p2_chain<200, kP2aEnd, kP2aEnd, 0>(col, prev, nullptr);  // 200..312
+#ifdef HZ_DIAG
+  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 10] = __builtin_amdgcn_s_memtime() - tq;  // P2a chain
+#endif
+  if (ok) {
+    a.p2h_w[b] = prev;
+    a.p2h_w[nr + b] = first1;
+    a.s_tag[2][b] = e * 8 + 3;
+  }
+  // rows 2..312 back (rows 0 and 1 keep their pass-1 words for P2b, which
+  // makes them final)
+  slot[(size_t)2 * nr + b0 + lane] = col[2];
+  slot[(size_t)3 * nr + b0 + lane] = col[3];
+  p2_out<0>(col, slot, nr, b0, lane, 4, kP2aEnd);
+}
+
+// P2b's final rows [313, 624) back to the slot as the chain publishes them
+// (seed blocks, wave 0, after P1a; p2b: whether P2b runs in this block)
+__device__ __forceinline__ void p2_p2b_out(const P2Args &a, int b0, int lane, bool p2b, int *s_prog, int *s_done) {
+  if (!p2b) return;
+  uint32_t *slot = a.s_mt[3];
+  const size_t nr = (size_t)a.nrow;
+  const uint32_t *col = p2_col(kP2Reg, lane);
+  // row 313 (alone: the region's groups start at 312), then groups of four
+  p2_wait(s_prog, 316);
+  slot[(size_t)313 * nr + b0 + lane] = col[313 - kP2bBase];
+  slot[(size_t)314 * nr + b0 + lane] = col[314 - kP2bBase];
+  slot[(size_t)315 * nr + b0 + lane] = col[315 - kP2bBase];
+  int stored = 316;
+#pragma unroll 1
+  while (stored + 32 <= kMT) {
+    const int have = p2_wait(s_prog, stored + 32);
+    const int r1 = stored + ((min(have, kMT) - stored) & ~3);
+    p2_out<kP2bBase>(col, slot, nr, b0, lane, stored, r1);
+    stored = r1;
+  }
+  p2_wait(s_done, 1);
+  p2_out<kP2bBase>(col, slot, nr, b0, lane, stored, kMT);
+}
+
+// P2b (seed blocks, wave 2, with wave 3): episode ep + 7.  The rest of pass
+// 2 (staged in three pieces like P2a's), then rows [0, kAheadTwist) of the
+// next generation twisted into the slot (the stream at cursor kMTAhead): row
+// r from rows r, r + 1 (P2a's, written to HBM by the previous call; rows 0
+// and 1 from here) and r + 397 (this stage's, in LDS).  Wave 3 loads the HBM
+// rows at once (lane: four boards, rows grp + 4 i, grp = lane / 16, so
+// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on),
+// then follows the chain's progress (s_prog): it twists rows 4-223 as rows
+// 401+ become final, and rows 0-3 once the chain's last step has made row 1
+// (s_done).  All of wave 3's loads precede its stores, so no row is
+// overwritten before it was read.  Wave 0, once its P1a chain is done,
+// stores P2b's final rows back as they are published (p2_p2b_out).
+constexpr int kTwIters = kAheadTwist / 4;
+__device__ __forceinline__ uint4 shfl4(const uint4 &v, int src) {
+  return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+// (e, ok: the board's episode and whether its pass 1 + P2a were this
+// episode's, read by every wave of the block before its barrier, so before
+// wave 2 rewrites the tag)
+__device__ __forceinline__ void p2_p2b(const P2Args &a, int b0, int lane, int w, int e, bool ok, uint32_t *s_row1,
+                                       int *s_done, int *s_prog) {
+  const int b = b0 + lane;
+  const bool act = b < a.n;
+  const size_t nr = (size_t)a.nrow;
+  uint32_t *slot = a.s_mt[3];
+  if (!__any(ok)) return;
+  if (w == 2) {
+    uint32_t *col = p2_col(kP2Reg, lane);
+#ifdef HZ_DIAG
+    const uint64_t tq = __builtin_amdgcn_s_memtime();
+#endif
+    {
+      P2Piece<312, 416, kP2bBase> p0;  // (row 312 is P2a's: loaded for the alignment, never written here)
+      p0.load(slot, nr, b0, lane);
+      p0.put(col);
+    }
+    P2Piece<416, 520, kP2bBase> p1;
+    p1.load(slot, nr, b0, lane);
+#ifdef HZ_DIAG
+    if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 11] = __builtin_amdgcn_s_memtime() - tq;  // P2b staged
+#endif
+    uint32_t prev = act ? a.p2h_r[b] : 0u;
+    const uint32_t first1 = act ? a.p2h_r[nr + b] : 0u;
+    p2_chain<kP2aEnd, 408, 416, kP2bBase>(col, prev, s_prog);  // 313..407
+    p1.put(col);
+    P2Piece<520, kMT, kP2bBase> p2;
+    p2.load(slot, nr, b0, lane);
+    p2_chain<408, 512, 520, kP2bBase>(col, prev, s_prog);  // 408..511
+    p2.put(col);
+    p2_chain<512, kMT, kMT, kP2bBase>(col, prev, s_prog);  // 512..623
+    p2_publish(s_prog, kMT);
+    s_row1[lane] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
+    p2_publish(s_done, 1);
+    if (ok) a.s_tag[3][b] = e * 8 + 4;
+    return;
+  }
+  const int grp = lane >> 4, c4 = (lane & 15) * 4, up = (lane + 16) & 63;
+  const uint32_t *colh = slot + b0 + c4;
+  // (the loads wait until the chain is a piece in: they stay out of the
+  // launch's opening burst, and land before the first twist needs them)
+  int have = p2_wait(s_prog, 360);
+  uint4 o[kTwIters + 1];
+#pragma unroll
+  for (int i = 0; i <= kTwIters; i++) {
+    const int r = grp + 4 * i;
+    if (r >= 2) o[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
+  }
+  auto twist_row = [&](int i, const uint4 &n1) {
+    const int r = grp + 4 * i;
+    const uint32_t *f = hz_lds + kP2Reg + c4 * kP2RS + (r + 397 - kP2bBase);  // boards c4..c4+3: four columns
+    uint4 v;
+    v.x = twist_word(o[i].x, n1.x, f[0]);
+    v.y = twist_word(o[i].y, n1.y, f[kP2RS]);
+    v.z = twist_word(o[i].z, n1.z, f[2 * kP2RS]);
+    v.w = twist_word(o[i].w, n1.w, f[3 * kP2RS]);
+    *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v;
+  };
+#pragma unroll
+  for (int i = 1; i < kTwIters; i++) {
+    const int need = 4 * i + 3 + 397 + 1;  // rows up to 4 i + 3 + 397 final
+    if (have < need) have = p2_wait(s_prog, need);
+    const uint4 t0 = shfl4(o[i], up), t1 = shfl4(o[i + 1], up);
+    twist_row(i, grp < 3 ? t0 : t1);
+  }
+  p2_wait(s_done, 1);
+  if (grp == 0) o[0] = make_uint4(0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u);
+  if (grp == 1) o[0] = make_uint4(s_row1[c4], s_row1[c4 + 1], s_row1[c4 + 2], s_row1[c4 + 3]);
+  const uint4 t0 = shfl4(o[0], up), t1 = shfl4(o[1], up);
+  twist_row(0, grp < 3 ? t0 : t1);
+  // (rows 224..312 keep P2a's words and rows 313..623 this stage's: the
+  // current generation's tail)
+}
+
+// seed blocks: wave 0 P1a; wave 1 P2a; waves 2-3 P2b
+__device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
+  __shared__ uint32_t s_row1[kBlock];
+  __shared__ int s_done, s_prog;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock, b = b0 + lane;
+  if (tid == 0) {
+    s_done = 0;
+    s_prog = 0;
+  }
+  // P2b's episode and decision, in every wave before the barrier
+  const int e7 = b < a.n ? a.ep_in[b] + 7 : 0;
+  const bool ok7 = b < a.n && a.s_tag[3][b] == e7 * 8 + 3;
+  __syncthreads();
+  if (w == 0) {
+    const bool p2b = __any(ok7);
+    if (b < a.n) p2_p1a(a, b0, lane);
+    p2_p2b_out(a, b0, lane, p2b, &s_prog, &s_done);
+  } else if (w == 1) {
+    p2_p2a(a, b0, lane);
+  } else {
+    p2_p2b(a, b0, lane, w, e7, ok7, s_row1, &s_done, &s_prog);
+  }
+}
+
+// a draw stage: draws [d0, d1) of episode e on its stream slot, from an LDS
+// window (at `base`) of kP2Win rows starting at the wave's lowest start
+// cursor (the wave's 64 boards, staged here); `in` (stage > 0) holds the
+// draws so far, `out` gets them plus these; the cursors go to the slot's
+// cursor table
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane, int stage, int base) {
+  const int b = b0 + lane;
+#ifdef HZ_DIAG
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  const bool act = b < a.n;
+  const size_t nr = (size_t)a.nrow;
+  const int d0 = kP2DrawsPer * stage, d1 = stage == 3 ? a.draws : min(a.draws, d0 + kP2DrawsPer);
+  const int e = act ? a.ep_in[b] + 6 - stage : 0;
+  const uint32_t *slot = a.s_mt[4 + stage];
+  int32_t *cur = a.s_cur[4 + stage] + b;
+  const P2Draw &in = a.x_r[stage > 0 ? stage - 1 : 0];
+  const P2Draw &out = stage == 3 ? a.pl_w : a.x_w[stage];
+  bool ok = act && a.s_tag[4 + stage][b] == e * 8 + 4;
+  int k0 = 0, c0 = kMTAhead;
+  uint64_t bag = initial_bag(), q[kAheadWords] = {0, 0, 0, 0};
+  if (stage > 0 && act) {  // (one round trip: used only if the tag matches)
+    const int itag = in.tag[b];
+    k0 = in.k[b];
+    c0 = in.c[b];
+    bag = in.bag[b];
+#pragma unroll
+    for (int i = 0; i < kAheadWords; i++) q[i] = in.q[(size_t)i * nr + b];
+    ok = ok && itag == e * 8 + stage;
+  }
+  const bool draws = ok && k0 >= d0 && d0 < d1;
+  const int r0 = wave_min_i(draws ? (c0 & 0xFFFF) : kAheadTwist) & ~3;
+  if (r0 < kAheadTwist) {  // the window: rows [r0, r0 + kP2Win), 16-B loads (four boards of a row per lane), all in flight
+    constexpr int U = kP2Win / 4;
+    const int c4 = (lane & 15) * 4;
     uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int r = q0 + 4 * u + (lane >> 4);
-      if (r < r1) {
-        if (ToLds) {
-          v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
-        } else {
-          const uint32_t *d = hz_lds + r * kLdsStride + c4;
-          v[u] = make_uint4(d[0], d[1], d[2], d[3]);
-        }
-      }
+      const int r = r0 + 4 * u + (lane >> 4);
+      v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int r = q0 + 4 * u + (lane >> 4);
-      if (r < r1) {
-        if (ToLds) {
-          uint32_t *d = hz_lds + r * kLdsStride + c4;
-          d[0] = v[u].x;
-          d[1] = v[u].y;
-          d[2] = v[u].z;
-          d[3] = v[u].w;
-        } else {
-          *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v[u];
-        }
-      }
+      uint32_t *dd = hz_lds + base + (4 * u + (lane >> 4)) * kLdsStride + c4;
+      dd[0] = v[u].x;
+      dd[1] = v[u].y;
+      dd[2] = v[u].z;
+      dd[3] = v[u].w;
     }
   }
-}
-
-// pass 2 of init_by_array on the lane's LDS column, waiting for staged rows
-// (f.in) and publishing final ones (f.out every 32 rows); then the pre-twist
-__device__ __forceinline__ void p2_pass2_lds(int lane, P2Flags &f) {
-  uint32_t *w = hz_lds + lane;
-  constexpr int S = kLdsStride;
-  int have = p2_wait(&f.in, 18);
-  const uint32_t first1 = w[1 * S];
-  uint32_t prev = first1;
-  uint32_t cur[8];
-#pragma unroll
-  for (int u = 0; u < 8; u++) cur[u] = w[(2 + u) * S];
-  for (int g = 2; g < kMT - 6; g += 8) {  // i = 2..617
-    if (g + 16 > have) have = p2_wait(&f.in, g + 16 < kMT ? g + 16 : kMT);
-    uint32_t nx[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) nx[u] = w[(g + 8 + u < kMT ? g + 8 + u : kMT - 1) * S];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(g + u);
-      w[(g + u) * S] = v;
-      prev = v;
-    }
-    if (((g + 8) & 31) == 2) p2_publish(&f.out, g + 8);
-#pragma unroll
-    for (int u = 0; u < 8; u++) cur[u] = nx[u];
-  }
-#pragma unroll
-  for (int u = 0; u < 6; u++) {  // i = 618..623
-    const uint32_t v = (cur[u] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)(618 + u);
-    w[(618 + u) * S] = v;
-    prev = v;
-  }
-  w[1 * S] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
-  w[0] = 0x80000000U;
-  p2_publish(&f.out, kMT);  // rows [kAheadTwist, kMT) final (the pre-twist rewrites only rows below)
-  mt_pretwist_g(w, (size_t)S, kAheadTwist);
-  p2_publish(&f.out, kMT + 1);
-}
-
-__device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
-  __shared__ P2Flags f;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b0 = blk * kBlock, b = b0 + lane;
-  const bool act = b < a.n;
-  const size_t nr = (size_t)a.nrow;
-  if (tid == 0) {
-    f.in = 0;
-    f.out = 0;
-  }
-  __syncthreads();
-  if (w == 0) {  // P1: pass 1 of episode ep + 6 into its fresh slot
-    if (act) {
-      const int e = a.ep_in[b] + 6;
-      mt_seed_pass1_g(a.s_mt[0] + b, nr, episode_seed(a.seed_base, b, e));
-      a.s_tag[0][b] = e * 4 + 1;
-    }
-    return;
-  }
-  // P2: episode ep + 5, whose pass 1 ran in the previous call.  Every lane
-  // runs the chain (lockstep); only boards whose pass 1 was this episode's
-  // get the tag.
-  uint32_t *slot = a.s_mt[1];
-  if (w == 1) {
-    const int e = act ? a.ep_in[b] + 5 : 0;
-    const bool ok = act && a.s_tag[1][b] == e * 4 + 1;
-    p2_pass2_lds(lane, f);
-    if (ok) a.s_tag[1][b] = e * 4 + 2;
-  } else if (w == 2) {  // stage rows [0, kMT) in chunks, publishing as they land
-    constexpr int kChunk = 64;
-    for (int r0 = 0; r0 < kMT; r0 += kChunk) {
-      const int r1 = r0 + kChunk < kMT ? r0 + kChunk : kMT;
-      p2_rows<true>(slot, nr, b0, lane, r0, r1);
-      p2_publish(&f.in, r1);
-    }
-    p2_wait(&f.out, kMT + 1);
-    p2_rows<false>(slot, nr, b0, lane, 0, kAheadTwist / 2);
-  } else {  // w == 3: final rows back as pass 2 publishes them
-    int done = kAheadTwist;
-    while (done < kMT) {
-      const int upto = p2_wait(&f.out, done + 32 < kMT ? done + 32 : kMT);
-      const int r1 = upto < kMT ? upto : kMT;
-      if (r1 > done) p2_rows<false>(slot, nr, b0, lane, done, r1);
-      done = r1 > done ? r1 : done;
-    }
-    p2_wait(&f.out, kMT + 1);
-    p2_rows<false>(slot, nr, b0, lane, kAheadTwist / 2, kAheadTwist);
-  }
-}
-
-__device__ __forceinline__ void p2_draw(const P2Args &a, int blk) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b0 = blk * kBlock, b = b0 + lane;
-  const bool act = b < a.n;
-  const size_t nr = (size_t)a.nrow;
-  if (w == 3) {  // the rule hashes of episode ep + 2
-    if (!act) return;
-    const int e = a.ep_in[b] + 2;
-    const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
-#pragma unroll 1
-    for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
-    a.h_tag_w[b] = e;
-    return;
-  }
-  // stage w: draws [lo, hi) of episode ep + 4 - w, on stream slot s_mt[2 + w]
-  const int lo = 8 * w, hi = w == 2 ? a.draws : min(a.draws, lo + 8);
-  const int e = act ? a.ep_in[b] + 4 - w : 0;
-  const uint32_t *slot = a.s_mt[2 + w];
-  const P2Draw &in = w == 1 ? a.ab_r : a.bc_r;
-  const P2Draw &out = w == 0 ? a.ab_w : w == 1 ? a.bc_w : a.pl_w;
-  bool ok = act && a.s_tag[2 + w][b] == e * 4 + 2;
-  if (w > 0) ok = ok && in.tag[b] == e * 4 + w;
-  // the window: rows [0, kP2Win) of the wave's 64 boards into LDS rows of
-  // stride 65 (16-B loads, four boards of a row per lane, half the window's
-  // loads in flight at once)
-  const int base = w * kP2Win * kLdsStride;
-  if (__any(ok)) {
-    constexpr int U = 24;
-    static_assert(kP2Win % (4 * U) == 0, "window rows per pass");
-    const int c4 = (lane & 15) * 4;
-#pragma unroll 1
-    for (int r0 = 0; r0 < kP2Win; r0 += 4 * U) {
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int r = r0 + 4 * u + (lane >> 4);
-        v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        uint32_t *dd = hz_lds + base + (r0 + 4 * u + (lane >> 4)) * kLdsStride + c4;
-        dd[0] = v[u].x;
-        dd[1] = v[u].y;
-        dd[2] = v[u].z;
-        dd[3] = v[u].w;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  P2_PHASE(25 + stage, t0);  // window staged
   if (!act) return;
   if (!ok) {
     out.tag[b] = -1;
     return;
   }
-  int k0 = 0, c0 = kMTAhead;
-  uint64_t bag = initial_bag(), q[kAheadWords] = {0, 0, 0, 0};
-  if (w > 0) {
-    k0 = in.k[b];
-    bag = in.bag[b];
-#pragma unroll
-    for (int i = 0; i < kAheadWords; i++) q[i] = in.q[(size_t)i * nr + b];
-    int32_t cv[kAheadDraws + 1];  // the cursors so far, forwarded (all loads first)
-#pragma unroll
-    for (int i = 0; i <= kAheadDraws; i++) cv[i] = i <= 8 * w ? in.cur[(size_t)i * nr + b] : 0;
-#pragma unroll
-    for (int i = 0; i <= kAheadDraws; i++)
-      if (i <= 8 * w && i <= k0) out.cur[(size_t)i * nr + b] = cv[i];
-    c0 = in.cur[(size_t)k0 * nr + b];
-  } else {
-    out.cur[b] = kMTAhead;
-  }
-  int k = k0;
-  if (k0 >= lo) {  // every earlier draw is done: continue in the window
-    StreamDraw<WinMT> d{WinMT(base + lane, c0, kP2Win)};
+  if (stage == 0) cur[0] = kMTAhead;
+  int k = k0, cc = c0;
+  if (draws) {  // every earlier draw is done: continue in the window
+    const int lim = min(r0 + kP2Win, kAheadTwist);
+    StreamDraw<WinMT> d{WinMT(base - r0 * kLdsStride + lane, c0, lim)};
 #pragma unroll 1
-    for (int i = lo; i < hi; i++) {
-      if (d.m.pos >= kP2Win) break;
+    for (int i = d0; i < d1; i++) {
+      if (d.m.pos >= lim) break;
       const uint32_t p9 = d(bag);
-      // a draw that consumed words past the window is discarded: the play
-      // stages redo it from the stream slot (from the last cursor kept)
-      if (d.m.pos > kP2Win) break;
+      // a draw that consumed words past the window is discarded: the next
+      // stage (or a play stage, from the stream slot) redoes it from the
+      // last cursor kept
+      if (d.m.pos > lim) break;
       apply_pile_fast(bag, p9);
       const int bit = 9 * i, wd = bit >> 6, off = bit & 63;
       const uint64_t lo9 = (uint64_t)p9 << off, hi9 = off > 55 ? (uint64_t)p9 >> (64 - off) : 0ull;
@@ -1484,17 +1753,67 @@ __device__ __forceinline__ void p2_draw(const P2Args &a, int blk) {
       q[1] |= wd == 1 ? lo9 : wd == 0 ? hi9 : 0ull;
       q[2] |= wd == 2 ? lo9 : wd == 1 ? hi9 : 0ull;
       q[3] |= wd == 3 ? lo9 : wd == 2 ? hi9 : 0ull;
-      out.cur[(size_t)(i + 1) * nr + b] = d.m.cursor();
+      cc = d.m.cursor();
+      cur[(size_t)(i + 1) * nr] = cc;
       k = i + 1;
     }
   }
   out.k[b] = k;
+  out.c[b] = cc;
   out.bag[b] = bag;
 #pragma unroll
   for (int i = 0; i < kAheadWords; i++) out.q[(size_t)i * nr + b] = q[i];
-  out.tag[b] = e * 4 + w + 1;
+  out.tag[b] = e * 8 + stage + 1;
 }
 
+// draw-X blocks: D1 (wave 0), D2 (wave 1), P1b (wave 2); draw-Y blocks: D3,
+// D4 (waves 0, 1).  Each draw wave stages its own window and reads only it.
+__device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock;
+  if (w < 2) {
+    p2_draw_stage(a, b0, lane, 2 * y + w, w * kP2WinRows * kLdsStride);
+  } else if (w == 2 && !y && b0 + lane < a.n) {
+    p2_p1b(a, b0, lane);
+  }
+}
+
+// a play stage's state after its plies, for the next play stage
+__device__ __forceinline__ void p2_mid_put(const P2Mid &m, size_t nr, int b, const State &s, const PlayDraw2 &d, int g,
+                                           int e) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) m.st[(size_t)k * nr + b] = s.pl[k];
+  m.st[4 * nr + b] = s.piles;
+  m.st[5 * nr + b] = s.misc;
+  m.q[b] = d.q0;
+  m.q[nr + b] = d.q1;
+  m.q[2 * nr + b] = d.q2;
+  m.q[3 * nr + b] = d.q3;
+  m.i[b] = d.d;
+  m.i[nr + b] = g;
+  m.i[2 * nr + b] = d.fell ? d.gm.cursor() : -1;
+  m.tag[b] = e;
+}
+// the previous play stage's state; the draw source continues its script
+// (nd entries, cursors in `cur`) or the slot stream it fell onto
+__device__ __forceinline__ PlayDraw2 p2_mid_get(const P2Mid &m, size_t nr, int b, State &s, int &g, int nd,
+                                               uint32_t *slot, const int32_t *cur) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) s.pl[k] = m.st[(size_t)k * nr + b];
+  s.piles = m.st[4 * nr + b];
+  s.misc = m.st[5 * nr + b];
+  const int d = m.i[b], fc = m.i[2 * nr + b];
+  g = m.i[nr + b];
+  return PlayDraw2{m.q[b], m.q[nr + b], m.q[2 * nr + b], m.q[3 * nr + b], d, nd, fc >= 0,
+                   MTR(slot, (int)nr, fc >= 0 ? fc : 0), cur + (size_t)nd * nr};
+}
+
+// play blocks: wave 2 playA (episode ep + 2), wave 1 playB (ep + 1), wave 0
+// playC (the rest of episode ep, or all of it), wave 3 the rule hashes of
+// episode ep + 3.  The three play stages run one code path (st = 2 - wave),
+// so the block's three playing waves share one copy of the ply loop in the
+// instruction cache (three inlined copies of it, ~50 KB each, thrashed the
+// cache the two CUs of a pair share).
 __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
   __shared__ uint64_t s_lds_mask;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1506,111 +1825,114 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
 #ifdef HZ_DIAG
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  if (w == 1) {  // playA: plies [0, kP2Half) of episode ep + 1
+  if (w == 3) {
     if (act) {
-      const int e = a.ep_in[b] + 1;
-      const P2Draw &pl = a.pl_a;
-      if (pl.tag[b] == e * 4 + 3) {
-        const int nd = pl.k[b];
-        PlayDraw2 draw{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
-                       MTR(a.s_mt[5] + b, (int)nr, pl.cur[(size_t)nd * nr + b])};
-        State s;
-        if (__all(nd >= 5)) draw.scripted_reset(s);
-        else reset_state(s, draw);
-        const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
-        const uint32_t *hs = a.h_tag_a[b] == e ? a.h_a + b : nullptr;
-        const int lim = kP2Half < a.max_plies ? kP2Half : a.max_plies;
-        const int steps = p2_plies(s, draw, 0, lim, rk, hs, nr);
-#pragma unroll
-        for (int k = 0; k < 4; k++) a.m_st_w[(size_t)k * nr + b] = s.pl[k];
-        a.m_st_w[4 * nr + b] = s.piles;
-        a.m_st_w[5 * nr + b] = s.misc;
-        a.m_q_w[b] = draw.q0;
-        a.m_q_w[nr + b] = draw.q1;
-        a.m_q_w[2 * nr + b] = draw.q2;
-        a.m_q_w[3 * nr + b] = draw.q3;
-        a.m_i_w[b] = draw.d;
-        a.m_i_w[nr + b] = steps;
-        a.m_i_w[2 * nr + b] = draw.fell ? draw.gm.cursor() : -1;
-        a.m_tag_w[b] = e;
-      } else {
-        a.m_tag_w[b] = -1;
-      }
+      const int e = a.ep_in[b] + 3;
+      const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
+#pragma unroll 1
+      for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
+      a.ht_w[b] = e;
 #ifdef HZ_DIAG
-      if (g_stamps) g_stamps[(size_t)b * 16 + 9] = __builtin_amdgcn_s_memtime() - t0;  // playA alone
+      if (g_stamps) g_stamps[(size_t)b * kP2Stamps + 3] = __builtin_amdgcn_s_memtime() - t0;  // hashes
 #endif
     }
-  }
-  if (w == 0) {  // playB: the rest of episode ep (or all of it)
+  } else {
+    const int st = __builtin_amdgcn_readfirstlane(2 - w);  // 0 playA, 1 playB, 2 playC
     bool lds_used = false;
     if (act) {
-      const int e = a.episode[b];
+      const int e = st == 2 ? a.episode[b] : a.ep_in[b] + 2 - st;
+      const P2Draw &pl = st == 0 ? a.pl_a : st == 1 ? a.pl_b : a.pl_c;
+      const P2Mid &mi = st == 1 ? a.m1_r : a.m2_r;
+      const uint32_t *hsrc = st == 0 ? a.h_a : st == 1 ? a.h_b : a.h_c;
+      const int32_t *htag = st == 0 ? a.ht_a : st == 1 ? a.ht_b : a.ht_c;
+      uint32_t *slot = a.s_mt[8 + st] + b;
+      const int32_t *cur = a.s_cur[8 + st] + b;
+      const int g_end = st == 0 ? min(a.cut1, a.max_plies) : st == 1 ? min(a.cut2, a.max_plies) : a.max_plies;
       const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
-      a.episode[b] = e + 1;
+      // every input's loads issued together (used only if the tags match)
+      const int ptag = pl.tag[b], nd = pl.k[b];
+      const int mtag = st > 0 ? mi.tag[b] : e;
+      const uint32_t *hs = htag[b] == e ? hsrc + b : nullptr;
       State s;
-      int g = 0, cursor = 0, src = -1;
-      const P2Draw &pl = a.pl_b;
-      if (a.m_tag_r[b] == e && pl.tag[b] == e * 4 + 3) {  // continue after playA
-#pragma unroll
-        for (int k = 0; k < 4; k++) s.pl[k] = a.m_st_r[(size_t)k * nr + b];
-        s.piles = a.m_st_r[4 * nr + b];
-        s.misc = a.m_st_r[5 * nr + b];
-        const int d = a.m_i_r[b], fc = a.m_i_r[2 * nr + b], nd = pl.k[b];
-        g = a.m_i_r[nr + b];
-        PlayDraw2 draw{a.m_q_r[b], a.m_q_r[nr + b], a.m_q_r[2 * nr + b], a.m_q_r[3 * nr + b], d, nd, fc >= 0,
-                       MTR(a.s_mt[6] + b, (int)nr, fc >= 0 ? fc : pl.cur[(size_t)nd * nr + b])};
-        const uint32_t *hs = a.h_tag_b[b] == e ? a.h_b + b : nullptr;
-        g += p2_plies(s, draw, g, a.max_plies, rk, hs, nr);
-        cursor = draw.fell ? draw.gm.cursor() : pl.cur[(size_t)draw.d * nr + b];
-        src = 2 + a.s_idx6;
-      } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
-        mt_seed(hz_lds + lane, kLdsStride, sd);
-        PlayDraw draw{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
-        reset_state(s, draw);
-        g = p2_plies(s, draw, 0, a.max_plies, rk, nullptr, nr);
-        cursor = draw.m.cursor();
-        lds_used = true;
+      int g = 0;
+      PlayDraw2 draw = st == 0 ? PlayDraw2{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
+                                           MTR(slot, (int)nr, 0), cur + (size_t)nd * nr}
+                               : p2_mid_get(mi, nr, b, s, g, nd, slot, cur);
+      const bool prep = ptag == e * 8 + 4 && mtag == e;
+      if (prep) {
+        if (st == 0) {
+          if (__all(nd >= 5)) draw.scripted_reset(s);
+          else reset_state(s, draw);
+        }
+        P2_PHASE(16 + 3 * st, t0);
+        g += p2_plies(s, draw, g, g_end, rk, hs, nr);
+        P2_PHASE(17 + 3 * st, t0);
       }
-      if (score_pending(s.misc)) finish_game(s);
-      store_state(a.st, a.n, b, s);
-      a.pos[b] = cursor;
-      a.mt_src[b] = src;
-      a.ply[b] = g;
-      a.seed[b] = sd;
-      a.ep_out[b] = e + 1;
-      // the game this call completes, as hz_play's other pipeline counts it
-      // (its first plies ran one call earlier, in playA)
-      if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
-      if (a.steps_done) a.steps_done[b] = g;
+      if (st < 2) {
+        const P2Mid &mo = st == 0 ? a.m1_w : a.m2_w;
+        if (prep) p2_mid_put(mo, nr, b, s, draw, g, e);
+        else mo.tag[b] = -1;
+      } else {
+        int cursor, src;
+        if (prep) {
+          cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
+          src = 2 + a.s_idx10;
+        } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
+          mt_seed(hz_lds + lane, kLdsStride, sd);
+          PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
+          reset_state(s, fb);
+          g = p2_plies(s, fb, 0, a.max_plies, rk, nullptr, nr);
+          cursor = fb.m.cursor();
+          src = -1;
+          lds_used = true;
+        }
+        a.episode[b] = e + 1;
+        if (score_pending(s.misc)) finish_game(s);
+        P2_PHASE(24, t0);
+        store_state(a.st, a.n, b, s);
+        a.pos[b] = cursor;
+        a.mt_src[b] = src;
+        a.ply[b] = g;
+        a.seed[b] = sd;
+        a.ep_out[b] = e + 1;
+        // the game this call completes, as hz_play's other pipeline counts it
+        if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
+        if (a.steps_done) a.steps_done[b] = g;
+      }
 #ifdef HZ_DIAG
-      if (g_stamps) g_stamps[(size_t)b * 16 + 8] = __builtin_amdgcn_s_memtime() - t0;  // playB alone
+      if (g_stamps) g_stamps[(size_t)b * kP2Stamps + w] = __builtin_amdgcn_s_memtime() - t0;  // playC, B, A
 #endif
     }
-    const uint64_t lm = __ballot(lds_used);
-    if (lane == 0) s_lds_mask = lm;
+    if (w == 0) {
+      const uint64_t lm = __ballot(lds_used);
+      if (lane == 0) s_lds_mask = lm;
+    }
   }
-  if (w == 0 && actmask == 0 && lane == 0) s_lds_mask = 0;
   __syncthreads();
   const uint64_t lds_mask = s_lds_mask & actmask;
   if (lds_mask) stage_mt(a.mt + (size_t)b0 * kMT, nb, tid, lds_mask, false);
 }
 
-__global__ void __launch_bounds__(kStageThreads) k_play2(P2Args a, int nblk) {
+// one 162 KB-LDS block per CU, so one wave per SIMD: every wave may use the
+// whole register file (the P2b twist wave keeps 57 rows in registers)
+__global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_play2(P2Args a, int nblk) {
   const int blk = (int)blockIdx.x;
-  const int role = blk < nblk ? 0 : blk < 2 * nblk ? 1 : 2;  // play, draw, seed blocks
+  const int role = blk / nblk;  // 0 play, 1 draw X, 2 draw Y, 3 seed blocks
+  const int rb = blk - role * nblk;
 #ifdef HZ_DIAG
   if (g_role_only >= 0 && g_role_only != role) return;
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  if (role == 0) p2_play(a, blk);
-  else if (role == 1) p2_draw(a, blk - nblk);
-  else p2_seed(a, blk - 2 * nblk);
+  if (role == 0) p2_play(a, rb);
+  else if (role == 3) p2_seed(a, rb);
+  else p2_draw(a, rb, role - 1);
 #ifdef HZ_DIAG
-  {  // stage durations, per board: 0 playB, 1 playA, 2-4 draws A-C, 5 hashes, 6 P1, 7 P2
-    const int w = threadIdx.x >> 6, bb = (blk - role * nblk) * kBlock + (threadIdx.x & 63);
-    const int slot = role == 0 ? w : role == 1 ? 2 + w : 6 + w;
-    if (g_stamps && bb < a.n && slot < 8 && (role != 0 || w < 2))
-      g_stamps[(size_t)bb * 16 + slot] = __builtin_amdgcn_s_memtime() - t0;
+  {  // wave durations per board, slot 4 role + wave: 0-3 play (C, B, A,
+     // hashes: stamped in p2_play, before its barrier), 4-6 draw X (D1, D2,
+     // P1b), 8-9 draw Y (D3, D4), 12-15 seed (P1a, P2 chain, stagers)
+    const int w = threadIdx.x >> 6, bb = rb * kBlock + (threadIdx.x & 63);
+    const bool idle = (role == 1 && w == 3) || (role == 2 && w >= 2);
+    if (g_stamps && role > 0 && !idle && bb < a.n) g_stamps[(size_t)bb * kP2Stamps + 4 * role + w] = __builtin_amdgcn_s_memtime() - t0;
   }
 #endif
 }
@@ -1621,7 +1943,7 @@ struct P2Slots {
   uint32_t *s[kP2Stream];
 };
 __global__ void __launch_bounds__(64) k_mt_materialize2(uint32_t *__restrict__ mt, P2Slots slots,
-                                                       int32_t *__restrict__ mt_src, int n, long nrow) {
+                                                       int32_t *__restrict__ mt_src, long nrow) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int src = mt_src[b];
   if (src < 2 || src >= 2 + kP2Stream) return;
@@ -1745,7 +2067,7 @@ static int materialize(hz_env *e) {
   if (e->p2_s[0]) {
     P2Slots sl;
     for (int k = 0; k < kP2Stream; k++) sl.s[k] = e->p2_s[k];
-    hipLaunchKernelGGL(k_mt_materialize2, dim3(e->n), dim3(64), 0, e->stream, e->mt, sl, e->mt_src, e->n,
+    hipLaunchKernelGGL(k_mt_materialize2, dim3(e->n), dim3(64), 0, e->stream, e->mt, sl, e->mt_src,
                        (long)e->nrow);
   }
   e->lazy = 0;
@@ -1753,74 +2075,85 @@ static int materialize(hz_env *e) {
 }
 
 // ---------------------------------------------------------- pipeline 2 host
+static_assert(sizeof(((hz_env *)0)->p2_s) / sizeof(uint32_t *) == kP2Stream, "slot ring");
 static void free_p2(hz_env *e) {
-  auto f = [](void *p) {
-    if (p) (void)hipFree(p);
+  auto f = [](auto *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
   };
   for (int k = 0; k < kP2Stream; k++) {
     f(e->p2_s[k]);
     f(e->p2_s_tag[k]);
-    e->p2_s[k] = nullptr;
-    e->p2_s_tag[k] = nullptr;
+    f(e->p2_s_cur[k]);
   }
-  for (int k = 0; k < 7; k++) {
-    f(e->p2_d_tag[k]);
-    f(e->p2_d_k[k]);
-    f(e->p2_d_q[k]);
-    f(e->p2_d_bag[k]);
-    f(e->p2_d_cur[k]);
-    e->p2_d_tag[k] = e->p2_d_k[k] = e->p2_d_cur[k] = nullptr;
-    e->p2_d_q[k] = e->p2_d_bag[k] = nullptr;
-  }
-  for (int k = 0; k < 2; k++) {
-    f(e->p2_m_tag[k]);
-    f(e->p2_m_st[k]);
-    f(e->p2_m_q[k]);
-    f(e->p2_m_i[k]);
-    f(e->p2_ep[k]);
-    e->p2_m_tag[k] = e->p2_m_i[k] = e->p2_ep[k] = nullptr;
-    e->p2_m_st[k] = e->p2_m_q[k] = nullptr;
-  }
-  for (int k = 0; k < 3; k++) {
+  auto fd = [&](P2Draw &d) {
+    f(d.tag);
+    f(d.k);
+    f(d.q);
+    f(d.bag);
+    f(d.c);
+  };
+  for (int k = 0; k < 3; k++) fd(e->p2_x[k][0]), fd(e->p2_x[k][1]);
+  for (int k = 0; k < 4; k++) fd(e->p2_pl[k]);
+  for (int k = 0; k < 2; k++)
+    for (int j = 0; j < 2; j++) {
+      P2Mid &m = e->p2_m[k][j];
+      f(m.tag);
+      f(m.st);
+      f(m.q);
+      f(m.i);
+    }
+  for (int k = 0; k < 4; k++) {
     f(e->p2_h[k]);
     f(e->p2_h_tag[k]);
-    e->p2_h[k] = nullptr;
-    e->p2_h_tag[k] = nullptr;
+  }
+  for (int k = 0; k < 2; k++) {
+    f(e->p2_p1h[k]);
+    f(e->p2_p2h[k]);
+    f(e->p2_ep[k]);
   }
 }
 
 // every hand-off tag to "none" (a tag names the episode its slot holds, and a
 // slot's contents depend only on (board, episode), so this is never needed
-// for correctness; it keeps a fresh pipeline from trusting freshly allocated
-// memory)
+// for correctness; it keeps a fresh pipeline from trusting fresh memory)
 static int p2_clear_tags(hz_env *e) {
   const size_t bytes = e->nrow * sizeof(int32_t);
+  auto c = [&](int32_t *t) { return hipMemsetAsync(t, 0xff, bytes, e->stream) != hipSuccess; };
   for (int k = 0; k < kP2Stream; k++)
-    if (hipMemsetAsync(e->p2_s_tag[k], 0xff, bytes, e->stream)) return 1;
-  for (int k = 0; k < 7; k++)
-    if (hipMemsetAsync(e->p2_d_tag[k], 0xff, bytes, e->stream)) return 1;
-  for (int k = 0; k < 2; k++)
-    if (hipMemsetAsync(e->p2_m_tag[k], 0xff, bytes, e->stream)) return 1;
+    if (c(e->p2_s_tag[k])) return 1;
   for (int k = 0; k < 3; k++)
-    if (hipMemsetAsync(e->p2_h_tag[k], 0xff, bytes, e->stream)) return 1;
+    if (c(e->p2_x[k][0].tag) || c(e->p2_x[k][1].tag)) return 1;
+  for (int k = 0; k < 4; k++)
+    if (c(e->p2_pl[k].tag) || c(e->p2_h_tag[k])) return 1;
+  for (int k = 0; k < 2; k++)
+    if (c(e->p2_m[k][0].tag) || c(e->p2_m[k][1].tag)) return 1;
   return 0;
 }
 
-// allocated on first use: 8 stream slots of 2.5 KB per board plus ~1.5 KB of
-// hand-offs per board
+// allocated on first use: 12 stream slots of 2.5 KB per board plus ~1.6 KB
+// of hand-offs per board
 static int alloc_p2(hz_env *e) {
   if (e->p2_s[0]) return 0;
   const size_t nr = e->nrow;
   auto m = [](auto **p, size_t bytes) { return hipMalloc((void **)p, bytes) == hipSuccess; };
   bool ok = true;
-  for (int k = 0; ok && k < kP2Stream; k++) ok = m(&e->p2_s[k], nr * kMT * 4) && m(&e->p2_s_tag[k], nr * 4);
-  for (int k = 0; ok && k < 7; k++)
-    ok = m(&e->p2_d_tag[k], nr * 4) && m(&e->p2_d_k[k], nr * 4) && m(&e->p2_d_q[k], kAheadWords * nr * 8) &&
-         m(&e->p2_d_bag[k], nr * 8) && m(&e->p2_d_cur[k], (kAheadDraws + 1) * nr * 4);
+  for (int k = 0; ok && k < kP2Stream; k++)
+    ok = m(&e->p2_s[k], nr * kMT * 4) && m(&e->p2_s_tag[k], nr * 4) &&
+         m(&e->p2_s_cur[k], (kAheadDraws + 1) * nr * 4);
+  auto md = [&](P2Draw &d) {
+    return m(&d.tag, nr * 4) && m(&d.k, nr * 4) && m(&d.q, kAheadWords * nr * 8) && m(&d.bag, nr * 8) &&
+           m(&d.c, nr * 4);
+  };
+  for (int k = 0; ok && k < 3; k++) ok = md(e->p2_x[k][0]) && md(e->p2_x[k][1]);
+  for (int k = 0; ok && k < 4; k++) ok = md(e->p2_pl[k]) && m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
   for (int k = 0; ok && k < 2; k++)
-    ok = m(&e->p2_m_tag[k], nr * 4) && m(&e->p2_m_st[k], 6 * nr * 8) && m(&e->p2_m_q[k], 4 * nr * 8) &&
-         m(&e->p2_m_i[k], 3 * nr * 4) && m(&e->p2_ep[k], nr * 4);
-  for (int k = 0; ok && k < 3; k++) ok = m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
+    for (int j = 0; ok && j < 2; j++) {
+      P2Mid &mm = e->p2_m[k][j];
+      ok = m(&mm.tag, nr * 4) && m(&mm.st, 6 * nr * 8) && m(&mm.q, 4 * nr * 8) && m(&mm.i, 3 * nr * 4);
+    }
+  for (int k = 0; ok && k < 2; k++)
+    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 2 * nr * 4) && m(&e->p2_ep[k], nr * 4);
   if (!ok || p2_clear_tags(e)) {
     free_p2(e);
     return 1;
@@ -1830,10 +2163,11 @@ static int alloc_p2(hz_env *e) {
 }
 
 // one hz_play call of pipeline 2 (k_play2).  Call c uses stream slot
-// (c - s) % 8 for stage s (0 P1 .. 6 playB), draw hand-offs AB / BC by call
-// parity, the pile scripts and rule hashes in rings of three, playA -> playB
-// by parity; every slot written by call c is read by call c + 1 or later, so
-// launch order on the stream is the only synchronisation.
+// (c - s) % kP2Stream for stage s; the D1 -> D2 -> D3 -> D4 hand-offs, P1a ->
+// P1b and playA -> playB -> playC by call parity; D4's script and the rule
+// hashes in rings of four (read by playA, playB, playC one, two and three
+// calls later).  Every slot written by call c is read by call c + 1 or later,
+// so launch order on the stream is the only synchronisation.
 static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32_t *steps_done) {
   if (alloc_p2(e)) return 1;
   const int c = e->calls2, r = c & 1, w = r ^ 1;
@@ -1853,6 +2187,8 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
   a.n = e->n;
   a.max_plies = max_plies;
   a.draws = e->seed_ahead;
+  a.cut1 = e->p2_cut1;
+  a.cut2 = e->p2_cut2;
   a.seed_base = e->seed_base;
   a.nrow = (long)e->nrow;
   a.games_done = games_done;
@@ -1861,38 +2197,41 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
   a.ep_in = e->p2_ep[w];
   a.ep_out = e->p2_ep[r];
   auto sl = [c](int s) { return ((c - s) % kP2Stream + kP2Stream) % kP2Stream; };
-  for (int s = 0; s < 7; s++) {
+  for (int s = 0; s < kP2Stages; s++) {
     a.s_mt[s] = e->p2_s[sl(s)];
     a.s_tag[s] = e->p2_s_tag[sl(s)];
+    a.s_cur[s] = e->p2_s_cur[sl(s)];
   }
-  a.s_idx6 = sl(6);
-  auto dr = [e](int k) { return P2Draw{e->p2_d_tag[k], e->p2_d_k[k], e->p2_d_q[k], e->p2_d_bag[k], e->p2_d_cur[k]}; };
-  a.ab_w = dr(r);
-  a.ab_r = dr(w);
-  a.bc_w = dr(2 + r);
-  a.bc_r = dr(2 + w);
-  a.pl_w = dr(4 + c % 3);
-  a.pl_a = dr(4 + (c + 2) % 3);  // written by call c - 1
-  a.pl_b = dr(4 + (c + 1) % 3);  // written by call c - 2
-  a.m_tag_w = e->p2_m_tag[r];
-  a.m_i_w = e->p2_m_i[r];
-  a.m_st_w = e->p2_m_st[r];
-  a.m_q_w = e->p2_m_q[r];
-  a.m_tag_r = e->p2_m_tag[w];
-  a.m_i_r = e->p2_m_i[w];
-  a.m_st_r = e->p2_m_st[w];
-  a.m_q_r = e->p2_m_q[w];
-  a.h_w = e->p2_h[c % 3];
-  a.h_tag_w = e->p2_h_tag[c % 3];
-  a.h_a = e->p2_h[(c + 2) % 3];
-  a.h_tag_a = e->p2_h_tag[(c + 2) % 3];
-  a.h_b = e->p2_h[(c + 1) % 3];
-  a.h_tag_b = e->p2_h_tag[(c + 1) % 3];
+  a.s_idx10 = sl(10);
+  a.p1h_w = e->p2_p1h[r];
+  a.p1h_r = e->p2_p1h[w];
+  a.p2h_w = e->p2_p2h[r];
+  a.p2h_r = e->p2_p2h[w];
+  for (int k = 0; k < 3; k++) {
+    a.x_w[k] = e->p2_x[k][r];
+    a.x_r[k] = e->p2_x[k][w];
+  }
+  a.pl_w = e->p2_pl[c % 4];
+  a.pl_a = e->p2_pl[(c + 3) % 4];  // written by call c - 1
+  a.pl_b = e->p2_pl[(c + 2) % 4];  // c - 2
+  a.pl_c = e->p2_pl[(c + 1) % 4];  // c - 3
+  a.m1_w = e->p2_m[0][r];
+  a.m1_r = e->p2_m[0][w];
+  a.m2_w = e->p2_m[1][r];
+  a.m2_r = e->p2_m[1][w];
+  a.h_w = e->p2_h[c % 4];
+  a.ht_w = e->p2_h_tag[c % 4];
+  a.h_a = e->p2_h[(c + 3) % 4];
+  a.ht_a = e->p2_h_tag[(c + 3) % 4];
+  a.h_b = e->p2_h[(c + 2) % 4];
+  a.ht_b = e->p2_h_tag[(c + 2) % 4];
+  a.h_c = e->p2_h[(c + 1) % 4];
+  a.ht_c = e->p2_h_tag[(c + 1) % 4];
   const int nblk = grid_for(e->n);
-  hipLaunchKernelGGL(k_play2, dim3(3 * nblk), dim3(kStageThreads), kResetLds, e->stream, a, nblk);
+  hipLaunchKernelGGL(k_play2, dim3(4 * nblk), dim3(kStageThreads), kResetLds, e->stream, a, nblk);
   if (int err = launch_err()) return err;
   e->lazy = 1;
-  e->calls2++;
+  e->calls2 = (c + 1) % (kP2Stream * 4);  // (a multiple of every ring length)
   e->primed = 0;  // the other pipeline's episode prediction is stale now
   return 0;
 }
@@ -1964,6 +2303,15 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   {  // HZ_PIPELINE=2: hz_play's second pipeline by default (hz_env_set_pipeline)
     const char *pv = getenv("HZ_PIPELINE");
     e->pipeline = pv && atoi(pv) == 2 ? 2 : 1;
+    // HZ_P2_CUTS="a,b": pipeline 2's play stage boundaries (plies; multiples of 8)
+    e->p2_cut1 = 24;
+    e->p2_cut2 = 48;
+    const char *cv = getenv("HZ_P2_CUTS");
+    int c1, c2;
+    if (cv && sscanf(cv, "%d,%d", &c1, &c2) == 2 && c1 > 0 && c2 > c1 && c1 % 8 == 0 && c2 % 8 == 0) {
+      e->p2_cut1 = c1;
+      e->p2_cut2 = c2;
+    }
   }
   if (!ok) {
     hz_env_destroy(e);

@@ -60,7 +60,10 @@ class BatchedEnv:
         """hz_play's pipeline: 1 = chance-ahead (k_rollout), 2 = every game
         spread over seven consecutive calls (k_play2); results are identical
         either way (hz_env_set_pipeline)."""
-        nat.check(nat.lib().hz_env_set_pipeline(self._h, int(pipeline)), "hz_env_set_pipeline")
+        L = nat.lib()
+        if not hasattr(L, "hz_env_set_pipeline") and int(pipeline) == 1:
+            return  # (an older A/B build: pipeline 1 is all it has)
+        nat.check(L.hz_env_set_pipeline(self._h, int(pipeline)), "hz_env_set_pipeline")
 
     # -- env surface ---------------------------------------------------------
     def reset(self, sel=None, seeds=None):

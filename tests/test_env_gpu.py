@@ -176,6 +176,7 @@ def test_play_seed_ahead_pipeline(Env, ahead, draws):
     boundary; 16 leaves draw2 nothing to draw."""
     n, base = 4096, 2024
     env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(1)
     env.set_seed_ahead(ahead, draws)
     for ep in range(5):
         _, steps, _ = env.rollout(200, reset=True)
@@ -190,25 +191,25 @@ def test_play_seed_ahead_pipeline(Env, ahead, draws):
 
 @pytest.mark.parametrize("draws", [24, 19, 3, 0])
 def test_play_pipeline2(Env, draws):
-    """hz_play's second pipeline (k_play2: seeding pass 1, pass 2, three draw
-    stages, plies 0-39, the rest, one stage per call on seven episodes at
-    once): ten consecutive calls (the first six fill the stages, from the
-    seventh every board replays a fully prepared episode), an hz_reset +
-    hz_rollout (re-primes: the hand-off slots then hold stale episodes), then
-    eight more calls; every game, ply count and stream bit-exact vs the
-    oracle's episode.  draws < 19 runs games past their pile scripts onto the
-    stream slots; 0 prepares no script at all."""
+    """hz_play's second pipeline (k_play2: seeding pass 1 in two halves, pass
+    2 in two halves, four draw stages, three play stages, one stage per call
+    on eleven episodes at once): fourteen consecutive calls (the first ten
+    fill the stages, from the eleventh every board replays a fully prepared
+    episode), an hz_reset + hz_rollout (re-primes: the hand-off slots then
+    hold stale episodes), then fourteen more calls; every game, ply count and
+    stream bit-exact vs the oracle's episode.  draws < 19 runs games past
+    their pile scripts onto the stream slots; 0 prepares no script at all."""
     n, base = 4096, 4242
     env = Env(n, seed_base=base, device=DEV)
     env.set_pipeline(2)
     env.set_seed_ahead(draws > 0, draws)
-    for ep in range(10):
+    for ep in range(14):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
     env.reset()
     _, steps, _ = env.rollout(200)
-    _check_episode(env, base, 10, steps)
-    for ep in range(11, 19):
+    _check_episode(env, base, 14, steps)
+    for ep in range(15, 29):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
 
@@ -221,7 +222,7 @@ def test_play_pipeline2_partial_block_and_switch(Env):
     env = Env(n, seed_base=base, device=DEV)
     env.set_pipeline(2)
     ep = 0
-    for pipe, calls in ((2, 8), (1, 2), (2, 9)):
+    for pipe, calls in ((2, 13), (1, 2), (2, 13)):
         env.set_pipeline(pipe)
         for _ in range(calls):
             _, steps, _ = env.rollout(200, reset=True)
@@ -247,17 +248,20 @@ def test_play_pipeline_partial_block(Env):
     game bit-exact."""
     n, base = 1000, 777
     env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(1)
     for ep in range(6):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
 
 
-def test_play_after_auto_reset_mispredicts_safely(Env):
+@pytest.mark.parametrize("pipeline", [1, 2])
+def test_play_after_auto_reset_mispredicts_safely(Env, pipeline):
     """hz_play with auto_reset moves episode counters by a board-dependent
     amount, so the concurrent seed-ahead guesses wrong for some boards: the
     next hz_play must still play every board's true next episode."""
     n, base = 1024, 55
     env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(pipeline)
     env.rollout(200, reset=True)                                  # episode 0 everywhere
     games, _, _ = env.rollout(64, auto_reset=True, reset=True)    # episode 1, then maybe 2
     resets = games.cpu().numpy() - env.done().cpu().numpy().astype(np.int64)
@@ -359,12 +363,15 @@ def test_encoder_odd_counts_and_empty_slots(Env):
                 assert (b[k] == f["boards"][j]).all() and (g[k] == f["globs"][j]).all(), (m, k)
 
 
-def test_play_partial_blocks(Env):
+@pytest.mark.parametrize("pipeline,calls", [(1, 3), (2, 13)])
+def test_play_partial_blocks(Env, pipeline, calls):
     """100 boards (a partial 64-board block in every role of the launch):
-    three consecutive hz_play calls, each bit-exact vs the oracle's episode."""
+    consecutive hz_play calls (pipeline 2: until episodes are fully
+    prepared), each bit-exact vs the oracle's episode."""
     n, base = 100, 9
     env = Env(n, seed_base=base, device=DEV)
-    for ep in range(3):
+    env.set_pipeline(pipeline)
+    for ep in range(calls):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
 

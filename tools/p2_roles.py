@@ -12,18 +12,21 @@ from hzamd.env import BatchedEnv
 n = 4096
 L = nat.lib()
 L.hz_diag_set_stamps.argtypes = [ctypes.c_void_p]
-stamps = torch.zeros(n, 16, dtype=torch.int64, device="cuda")
+stamps = torch.zeros(n, 32, dtype=torch.int64, device="cuda")  # (k_play2 uses 32 slots per board)
 L.hz_diag_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
 out = {}
 for pipe in (1, 2):
     env = BatchedEnv(n, device="cuda")
     env.set_pipeline(pipe)
-    names = (["play_block", "play_block_", "drawA", "drawB", "drawC", "hashes", "P1", "P2", "playB",
-              "playA"] if pipe == 2 else
+    names = ({0: "playC", 1: "playB", 2: "playA", 3: "hashes", 4: "D1", 5: "D2", 6: "P1b", 8: "D3", 9: "D4",
+              12: "P1a", 13: "P2a", 14: "P2b", 15: "P2b_twist", 7: "P2a_staged", 10: "P2a_chain_to_305",
+              11: "P2b_staged", 16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
+              22: "playC_loaded", 23: "playC_plies", 24: "playC_scored", 25: "D1_staged", 26: "D2_staged",
+              27: "D3_staged", 28: "D4_staged"} if pipe == 2 else
              {5: "play", 6: "draw2", 15: "draw1", 7: "seed"})
-    for only in (-1, 0, 1, 2) if pipe == 2 else (-1,):
+    for only in (-1, 0, 1, 2, 3) if pipe == 2 else (-1,):
         L.hz_diag_set_role_only(-1)
-        for _ in range(8):
+        for _ in range(12):
             env.rollout(200, reset=True)
         L.hz_diag_set_role_only(only)
         stamps.zero_()
@@ -31,10 +34,14 @@ for pipe in (1, 2):
         e0.record(); env.rollout(200, reset=True); e1.record()
         torch.cuda.synchronize()
         s = stamps.cpu().double()
-        items = enumerate(names) if pipe == 2 else names.items()
-        key = f"p{pipe}_" + ("all" if only < 0 else ("play", "draw", "seed")[only] + "_alone")
+        if pipe == 1:  # (k_rollout's stamps: 16 slots per board)
+            s = s.reshape(-1, 16)[:n]
+        items = names.items()
+        key = f"p{pipe}_" + ("all" if only < 0 else ("play", "drawX", "drawY", "seed")[only] + "_alone")
         out[key] = {"us": e0.elapsed_time(e1) * 1e3,
                     **{nm: [s[:, k].max().item(), s[:, k].median().item()] for k, nm in items}}
+        if pipe == 2 and only < 0:  # every stage's worst board vs the kernel (the longest chain sets the time)
+            out[key]["longest"] = max((v[0], k) for k, v in out[key].items() if k != "us" and isinstance(v, list))
     env.close()
 L.hz_diag_set_role_only(-1)
 print(json.dumps(out))
