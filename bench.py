@@ -49,7 +49,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 # hz_play launches until every board replays a fully prepared episode, by
 # pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's seven stages)
-PIPELINE_DEPTH = {1: 4, 2: 7}
+PIPELINE_DEPTH = {1: 4, 2: 12}
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 X6_PRODUCTS = 6                # bf16 MFMAs per fp32 product block in the x6 kernels
@@ -1115,7 +1115,7 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("k_rollout_bytes_per_launch")
+            traffic = json.load(open(args.traffic_json)).get(f"{kname}_bytes_per_launch")
         except Exception:
             traffic = None
     cycles = kern_ms * 1e-3 * CLOCK_GHZ * 1e9

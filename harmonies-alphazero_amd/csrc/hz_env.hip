@@ -66,15 +66,16 @@ struct hz_env {
   int32_t *mt_src;           // [n]
   int lazy;                  // some board may have mt_src >= 0
   // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
-  // spread over eleven consecutive hz_play calls, one stage per call
+  // spread over twelve consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
   int calls2, primed2;
   int p2_cut1, p2_cut2;      // the play stages' ply boundaries (HZ_P2_CUTS)
-  uint32_t *p2_s[12];        // [624][nrow] stream slots (kP2Stream)
-  int32_t *p2_s_tag[12];     // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 seeded, rows 0-223 twisted
-  int32_t *p2_s_cur[12];     // [kAheadDraws + 1][nrow] the slot's cursor before draw 0 and after each draw
+  uint32_t *p2_s[14];        // [624][nrow] stream slots (kP2Stream)
+  int32_t *p2_s_tag[14];     // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
+  int32_t *p2_s_cur[14];     // [kAheadDraws + 1][nrow] the slot's cursor before draw 0 and after each draw
   uint32_t *p2_p1h[2];       // [nrow] P1a -> P1b
   uint32_t *p2_p2h[2];       // [2][nrow] P2a -> P2b
+  uint32_t *p2_p3h[2];       // [2][nrow] P2b -> P2c
   P2Draw p2_x[3][2];         // D1 -> D2 -> D3 -> D4, by call parity
   P2Draw p2_pl[4];           // D4 -> playA, playB, playC: a ring of four
   P2Mid p2_m[2][2];          // playA -> playB, playB -> playC, by call parity
@@ -1094,23 +1095,24 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // hz_play's second pipeline (hz_env_set_pipeline(e, 2)).  Each of
 // k_rollout's roles runs one serial per-board chain of ~60 k cycles (a whole
 // game, a whole seeding, 16 pile draws), and a launch lasts as long as its
-// longest chain.  Here every board's episode is cut into eleven stages of
+// longest chain.  Here every board's episode is cut into twelve stages of
 // 20-35 k cycles, one per consecutive hz_play call, and one launch runs all
-// eleven at once, each on a different episode of the board (ep = the episode
-// counter the previous call left, p2_ep; stage s works on episode ep + 10 - s):
-//   s = 0  P1a   seeding pass 1, steps 1-312          seed blocks, wave 0
+// twelve at once, each on a different episode of the board (ep = the episode
+// counter the previous call left, p2_ep; stage s works on episode ep + 11 - s):
+//   s = 0  P1a   seeding pass 1, steps 1-312          draw-Y blocks, wave 2
 //   s = 1  P1b   pass 1, steps 313-624                draw-X blocks, wave 2
-//   s = 2  P2a   pass 2, steps 2-312 (LDS rows 1-312) seed blocks, wave 1
-//   s = 3  P2b   pass 2, steps 313-624 (rows 313-623) seed blocks, waves 2-3
-//                and rows 0-223 of the next generation twisted
-//   s = 4  D1    pile draws 0-5                       draw-X blocks, wave 0
-//   s = 5  D2    draws 6-11                           draw-X blocks, wave 1
-//   s = 6  D3    draws 12-17                          draw-Y blocks, wave 0
-//   s = 7  D4    draws 18-23                          draw-Y blocks, wave 1
+//   s = 2  P2a   pass 2, steps 2-208                  seed blocks, wave 0
+//   s = 3  P2b   pass 2, steps 209-416                seed blocks, wave 1
+//   s = 4  P2c   pass 2, steps 417-624; rows 0-223    seed blocks, wave 2
+//                of the next generation twisted       (twist: wave 3)
+//   s = 5  D1    pile draws 0-5                       draw-X blocks, wave 0
+//   s = 6  D2    draws 6-11                           draw-X blocks, wave 1
+//   s = 7  D3    draws 12-17                          draw-Y blocks, wave 0
+//   s = 8  D4    draws 18-23                          draw-Y blocks, wave 1
 //          (the episode's rule hashes meanwhile:      play blocks, wave 3)
-//   s = 8  playA plies [0, cut1)                      play blocks, wave 2
-//   s = 9  playB plies [cut1, cut2)                   play blocks, wave 1
-//   s = 10 playC the rest, final scoring, the board's play blocks, wave 0
+//   s = 9  playA plies [0, cut1)                      play blocks, wave 2
+//   s = 10 playB plies [cut1, cut2)                   play blocks, wave 1
+//   s = 11 playC the rest, final scoring, the board's play blocks, wave 0
 //                state, cursor and counters
 // An episode's stream lives in one slot of a ring of kP2Stream from P1a to
 // playC (and afterwards as the board's current stream until materialize or
@@ -1125,8 +1127,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // stage once per board: one game's worth of work per board per call.
 constexpr int kP2Win = 96;        // rows a draw stage stages, from its wave's lowest cursor
 constexpr int kP2WinRows = kP2Win + 24;  // LDS rows per window (a scan reads up to 23 rows past its cursor)
-constexpr int kP2Stages = 11;
-constexpr int kP2Stream = 12;     // stream slots (>= kP2Stages + 1: playC's slot stays the board's stream)
+constexpr int kP2Stages = 12;
+constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: playC's slot stays the board's stream)
 constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
 constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
 constexpr int kP1Split = 313;
@@ -1159,13 +1161,15 @@ struct P2Args {
   const int32_t *ep_in;
   int32_t *ep_out;
   uint32_t *s_mt[kP2Stages];  // the stream slot of each stage this call
-  int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 seeded, rows 0-223 twisted
+  int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
   int32_t *s_cur[kP2Stages];  // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
-  int s_idx10;                // playC's slot index (materialize: mt_src = 2 + index)
+  int s_idx11;                // playC's slot index (materialize: mt_src = 2 + index)
   uint32_t *p1h_w;            // [nrow] P1a -> P1b: pass 1's last value
   const uint32_t *p1h_r;
   uint32_t *p2h_w;            // [2][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word
   const uint32_t *p2h_r;
+  uint32_t *p3h_w;            // [2][nrow] P2b -> P2c: the same
+  const uint32_t *p3h_r;
   P2Draw x_w[3], x_r[3];      // D1 -> D2 -> D3 -> D4 (tag: episode * 8 + stages done)
   P2Draw pl_w, pl_a, pl_b, pl_c;  // D4's script: written this call; read by playA, playB, playC
   P2Mid m1_w, m1_r, m2_w, m2_r;   // playA -> playB -> playC
@@ -1345,7 +1349,7 @@ __device__ __forceinline__ void p2_keys(uint64_t seed, uint32_t &kA, uint32_t &k
 __device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
   const int b = b0 + lane;
   const size_t nr = (size_t)a.nrow;
-  const int e = a.ep_in[b] + 10;
+  const int e = a.ep_in[b] + 11;
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
   uint32_t prev = 19650218u;
@@ -1356,7 +1360,7 @@ __device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
 __device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
   const int b = b0 + lane;
   const size_t nr = (size_t)a.nrow;
-  const int e = a.ep_in[b] + 9;
+  const int e = a.ep_in[b] + 10;
   if (a.s_tag[1][b] != e * 8 + 1) return;
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
@@ -1374,267 +1378,208 @@ __device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
   a.s_tag[1][b] = e * 8 + 2;
 }
 
-// Pass 2 in two halves, P2a (steps 2-312) and P2b (steps 313-623 and the
-// last step at i = 1), in one seed block.  Every step reads the next pass-1
-// word, too close ahead for an HBM round trip (a chain reading the slot
-// through a register ring stalled on the memory counter: ~220 k cycles),
-// and a chain that spends a memory instruction per step is bound by their
-// issue (one LDS read and one LDS write per step: ~79 cycles a step; an LDS
-// read and an HBM store: ~72), so the block's LDS holds each board's words
-// transposed: lane l's column of R words at l * kP2RS (P2a: rows [0, 316),
-// P2b: rows [312, 628) - 312 in the second region), four rows per 16-B
-// access (kP2RS / 4 odd: the 64 lanes' 16-B accesses spread over all banks).
-// A chain reads four pass-1 words and writes four final words per LDS
-// operation (in place, the read-ahead past the rows written).  Pass-1 rows
-// arrive in three pieces (dword loads, one row of the wave's 64 boards per
-// load, the next piece in flight while the chain works through the
-// current one); final rows leave through coalesced dword stores (P2a's at
-// its end, P2b's by wave 0 as they are published).
-constexpr int kP2aEnd = 313;
-constexpr int kP2RS = 316;                   // words per lane column
-constexpr int kP2Reg = 64 * kP2RS;           // words per region
-constexpr int kP2bBase = 312;                // P2b region row 0 = absolute row 312
-static_assert(2 * kP2Reg * 4 <= (int)kResetLds && (kP2RS / 4) % 2 == 1, "two transposed regions");
-// LDS word of (region base, lane, absolute row - region row 0)
-__device__ __forceinline__ uint32_t *p2_col(int reg, int lane) { return hz_lds + reg + lane * kP2RS; }
-// rows [R0, R1) (R0 % 4 == 0) of the wave's 64 boards, pass 1 -> the lanes'
-// columns (rel = region row 0): dword loads, 16-B LDS writes
-template <int R0, int R1, int REL>
-struct P2Piece {
-  static constexpr int N = R1 - R0;
-  static_assert(R0 % 4 == 0 && (R0 - REL) % 4 == 0, "aligned groups of four rows");
-  uint32_t v[(N + 3) / 4 * 4];
-  __device__ __forceinline__ void load(const uint32_t *__restrict__ slot, size_t nr, int b0, int lane) {
+// Pass 2 in three stages, P2a (steps 2-208), P2b (209-416) and P2c
+// (417-623 and the last step at i = 1), in one seed block on disjoint rows
+// of its [624][65] LDS array (the rows of three different episodes).  Every
+// step reads the next pass-1 word, too close ahead for an HBM round trip (a
+// chain reading the slot through a register ring stalled on the memory
+// counter: ~220 k cycles per half), so each chain first stages its third of
+// the pass-1 words into its own rows (all loads in flight at once), then
+// runs on LDS reads, storing each final word to the slot with a buffer store
+// (the row offset a scalar: no address arithmetic in the chain).  A chain
+// step costs ~70 cycles with one wave per SIMD (the four dependent VALU
+// operations of the recurrence plus the step's memory instructions; staging
+// transposed, four words per LDS access, changed nothing), so the chain is
+// cut into thirds rather than made cheaper per step.
+constexpr int kP2aEnd = 209, kP2bEnd = 417;
+constexpr int kTwKeep = 397;  // P2c's final rows from here on stay in LDS (the twist reads rows 397-620)
+template <int R0, int R1>
+__device__ __forceinline__ void p2_stage(const uint32_t *__restrict__ slot, size_t nr, int b0, int lane) {
+  constexpr int U = (R1 - R0 + 3) / 4;  // 16-B loads: four boards of a row per lane, four rows per instruction
+  const int c4 = (lane & 15) * 4;
+  uint4 v[U];
 #pragma unroll
-    for (int k = 0; k < N; k++) v[k] = slot[(size_t)(R0 + k) * nr + b0 + lane];
+  for (int u = 0; u < U; u++) {
+    const int r = R0 + 4 * u + (lane >> 4);
+    if (r < R1) v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
   }
-  __device__ __forceinline__ void put(uint32_t *col) const {
 #pragma unroll
-    for (int k = 0; k < N; k += 4)
-      *reinterpret_cast<uint4 *>(col + R0 - REL + k) =
-          make_uint4(v[k], k + 1 < N ? v[k + 1] : 0u, k + 2 < N ? v[k + 2] : 0u, k + 3 < N ? v[k + 3] : 0u);
-  }
-};
-// final rows [r0, r1) of the lane's column (rows from REL) -> the slot,
-// coalesced dword stores (one row of 64 boards each); r0 % 4 == 0; eight
-// groups of four rows per batch, the batch's LDS reads issued first
-template <int REL>
-__device__ __forceinline__ void p2_out(const uint32_t *col, uint32_t *__restrict__ slot, size_t nr, int b0, int lane,
-                                       int r0, int r1) {
-  constexpr int B = 8;
-#pragma unroll 1
-  for (int rb = r0; rb < r1; rb += 4 * B) {  // (wave-uniform)
-    uint4 q[B];
-#pragma unroll
-    for (int k = 0; k < B; k++)
-      if (rb + 4 * k < r1) q[k] = *reinterpret_cast<const uint4 *>(col + rb + 4 * k - REL);
-#pragma unroll
-    for (int k = 0; k < B; k++) {
-      const int r = rb + 4 * k;
-      if (r < r1) {
-        uint32_t *o = slot + (size_t)r * nr + b0 + lane;
-        o[0] = q[k].x;
-        if (r + 1 < r1) o[nr] = q[k].y;
-        if (r + 2 < r1) o[2 * nr] = q[k].z;
-        if (r + 3 < r1) o[3 * nr] = q[k].w;
-      }
+  for (int u = 0; u < U; u++) {
+    const int r = R0 + 4 * u + (lane >> 4);
+    if (r < R1) {
+      uint32_t *d = hz_lds + r * kLdsStride + c4;
+      d[0] = v[u].x;
+      d[1] = v[u].y;
+      d[2] = v[u].z;
+      d[3] = v[u].w;
     }
+  }
+  // (a wave's LDS operations execute in order: its later reads see these)
+}
+// the slot's columns of boards [b0, b0 + 64) as a buffer (rows of nr words)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, int b0, size_t nr) {
+  const uint64_t base = (uint64_t)(slot + b0);
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+// steps [G0, G1) of pass 2 (G1 - G0 a multiple of 8) on the lane's LDS
+// column, pass-1 words read 8 steps ahead (rows below G1), final words to
+// the slot (buffer stores: voffset the lane, soffset the row) and, with
+// KeepLds, over the pass-1 words in LDS as well (in place: the read-ahead is
+// always past the rows written), publishing progress every 8 steps
+template <int G0, int G1, bool KeepLds>
+__device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev,
+                                        int *prog) {
+  static_assert((G1 - G0) % 8 == 0, "groups of eight");
+  uint32_t *l = hz_lds + lane;
+  constexpr int S = kLdsStride;
+  uint32_t cur[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) cur[u] = l[(G0 + u) * S];
+#pragma unroll 2
+  for (int g = G0; g < G1; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = l[(g + 8 + u < G1 ? g + 8 + u : G1 - 1) * S];
+    const uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
+    const int soff = __builtin_amdgcn_readfirstlane(g * row_bytes);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      // (cur ^ p) - (g + u) as one v_xad_u32 with the offset in an SGPR
+      const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
+      uint32_t v;
+      asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
+      __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, soff + u * row_bytes, 0);
+      if (KeepLds) l[(g + u) * S] = v;
+      prev = v;
+    }
+    if (KeepLds) p2_publish(prog, g + 8);  // rows [G0, g + 8) final in LDS
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
   }
 }
-// steps [G0, G1) of pass 2 (the first and last groups of four rows may be
-// partial) on the lane's column `col` (rows from REL): four words per LDS
-// read, kP2Ahead groups (24 rows, ~400 cycles of chain) ahead, four final
-// words per LDS write; reads stay below RL (the rows staged); with prog,
-// progress published every 8 steps
-constexpr int kP2Ahead = 6;
-template <int G0, int G1, int RL, int REL>
-__device__ __forceinline__ void p2_chain(uint32_t *col, uint32_t &prev, int *prog) {
-  constexpr int D = kP2Ahead, Q0 = G0 & ~3;
-  uint4 c[D];
+// the last steps [G, G1) one by one
+template <int G, int G1, bool KeepLds>
+__device__ __forceinline__ void p2_tail(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev) {
 #pragma unroll
-  for (int d = 0; d < D; d++)
-    c[d] = Q0 + 4 * d < RL ? *reinterpret_cast<const uint4 *>(col + Q0 + 4 * d - REL) : make_uint4(0, 0, 0, 0);
-#pragma unroll 1
-  for (int q0 = Q0; q0 < G1; q0 += 4 * D) {
-    const uint32_t kq = __builtin_amdgcn_readfirstlane(0u - (uint32_t)q0);
-#pragma unroll
-    for (int d = 0; d < D; d++) {
-      const int q = q0 + 4 * d;
-      if (q < G1) {  // (wave-uniform)
-        uint32_t w[4] = {c[d].x, c[d].y, c[d].z, c[d].w};
-        c[d] = q + 4 * D < RL ? *reinterpret_cast<const uint4 *>(col + q + 4 * D - REL) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int i = q + u;
-          if (i >= G0 && i < G1) {  // (wave-uniform: only the first and last groups are partial)
-            const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
-            uint32_t v;
-            // (cur ^ p) - i as one v_xad_u32 with the offset in an SGPR
-            asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(w[u]), "s"(kq - (uint32_t)(4 * d + u)));
-            w[u] = v;
-            prev = v;
-          }
-        }
-        *reinterpret_cast<uint4 *>(col + q - REL) = make_uint4(w[0], w[1], w[2], w[3]);
-        if (prog && (q & 4)) p2_publish(prog, q + 4 < G1 ? q + 4 : G1);  // rows [., q + 4) final
-      }
-    }
+  for (int i = G; i < G1; i++) {
+    const uint32_t v = (hz_lds[i * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, 0);
+    if (KeepLds) hz_lds[i * kLdsStride + lane] = v;
+    prev = v;
   }
 }
 
-// P2a (seed blocks, wave 1): episode ep + 8, whose pass 1 completed in the
-// previous call; hands pass 2's state (prev, and pass 1's row-1 word) to P2b
-__device__ __forceinline__ void p2_p2a(const P2Args &a, int b0, int lane) {
+// P2a (seed blocks, wave 0): episode ep + 9, whose pass 1 completed in the
+// previous call; P2b (wave 1): ep + 8; P2c (wave 2, with wave 3's twist):
+// ep + 7.  Each hands (prev, pass 1's row-1 word) to the next.  (e, ok: the
+// board's episode and whether the stage's input is this episode's, read by
+// every wave of the block before its barrier, so before P2c rewrites its
+// tag.)
+template <int K>  // 0 P2a, 1 P2b, 2 P2c
+__device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int e, bool ok, uint32_t *s_row1,
+                                         int *s_done, int *s_prog) {
   const int b = b0 + lane;
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
-  const int e = act ? a.ep_in[b] + 8 : 0;
-  const bool ok = act && a.s_tag[2][b] == e * 8 + 2;
-  if (!__any(ok)) return;
-  uint32_t *slot = a.s_mt[2];
-  uint32_t *col = p2_col(0, lane);
+  if (!__any(ok)) {
+    if (K == 2) p2_publish(s_done, 2);  // (the twist wave's wait ends: nothing to twist)
+    return;
+  }
+  uint32_t *slot = a.s_mt[2 + K];
 #ifdef HZ_DIAG
   const uint64_t tq = __builtin_amdgcn_s_memtime();
 #endif
-  {
-    P2Piece<0, 104, 0> p0;  // (row 0: pass 1 leaves it unused here; loaded for the alignment)
-    p0.load(slot, nr, b0, lane);
-    p0.put(col);
-  }
-  P2Piece<104, 208, 0> p1;
-  p1.load(slot, nr, b0, lane);
+  constexpr int R0 = K == 0 ? 1 : K == 1 ? kP2aEnd : kP2bEnd, R1 = K == 0 ? kP2aEnd : K == 1 ? kP2bEnd : kMT;
+  p2_stage<R0, R1>(slot, nr, b0, lane);
 #ifdef HZ_DIAG
-  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 7] = __builtin_amdgcn_s_memtime() - tq;  // P2a staged
+  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 29 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
 #endif
-  const uint32_t first1 = col[1];
-  uint32_t prev = first1;
-  p2_chain<2, 96, 104, 0>(col, prev, nullptr);  // steps 2..95 (reads below row 104)
-  p1.put(col);
-  P2Piece<208, kP2aEnd, 0> p2;
-  p2.load(slot, nr, b0, lane);
-  p2_chain<96, 200, 208, 0>(col, prev, nullptr);  // 96..199
-  p2.put(col);
-  p2_chain<200, kP2aEnd, kP2aEnd, 0>(col, prev, nullptr);  // 200..312
-#ifdef HZ_DIAG
-  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 10] = __builtin_amdgcn_s_memtime() - tq;  // P2a chain
-#endif
-  if (ok) {
-    a.p2h_w[b] = prev;
-    a.p2h_w[nr + b] = first1;
-    a.s_tag[2][b] = e * 8 + 3;
+  uint32_t prev, first1;
+  if (K == 0) {
+    first1 = hz_lds[1 * kLdsStride + lane];
+    prev = first1;
+  } else {
+    const uint32_t *h = K == 1 ? a.p2h_r : a.p3h_r;
+    prev = act ? h[b] : 0u;
+    first1 = act ? h[nr + b] : 0u;
   }
-  // rows 2..312 back (rows 0 and 1 keep their pass-1 words for P2b, which
-  // makes them final)
-  slot[(size_t)2 * nr + b0 + lane] = col[2];
-  slot[(size_t)3 * nr + b0 + lane] = col[3];
-  p2_out<0>(col, slot, nr, b0, lane, 4, kP2aEnd);
-}
-
-// P2b's final rows [313, 624) back to the slot as the chain publishes them
-// (seed blocks, wave 0, after P1a; p2b: whether P2b runs in this block)
-__device__ __forceinline__ void p2_p2b_out(const P2Args &a, int b0, int lane, bool p2b, int *s_prog, int *s_done) {
-  if (!p2b) return;
-  uint32_t *slot = a.s_mt[3];
-  const size_t nr = (size_t)a.nrow;
-  const uint32_t *col = p2_col(kP2Reg, lane);
-  // row 313 (alone: the region's groups start at 312), then groups of four
-  p2_wait(s_prog, 316);
-  slot[(size_t)313 * nr + b0 + lane] = col[313 - kP2bBase];
-  slot[(size_t)314 * nr + b0 + lane] = col[314 - kP2bBase];
-  slot[(size_t)315 * nr + b0 + lane] = col[315 - kP2bBase];
-  int stored = 316;
-#pragma unroll 1
-  while (stored + 32 <= kMT) {
-    const int have = p2_wait(s_prog, stored + 32);
-    const int r1 = stored + ((min(have, kMT) - stored) & ~3);
-    p2_out<kP2bBase>(col, slot, nr, b0, lane, stored, r1);
-    stored = r1;
-  }
-  p2_wait(s_done, 1);
-  p2_out<kP2bBase>(col, slot, nr, b0, lane, stored, kMT);
-}
-
-// P2b (seed blocks, wave 2, with wave 3): episode ep + 7.  The rest of pass
-// 2 (staged in three pieces like P2a's), then rows [0, kAheadTwist) of the
-// next generation twisted into the slot (the stream at cursor kMTAhead): row
-// r from rows r, r + 1 (P2a's, written to HBM by the previous call; rows 0
-// and 1 from here) and r + 397 (this stage's, in LDS).  Wave 3 loads the HBM
-// rows at once (lane: four boards, rows grp + 4 i, grp = lane / 16, so
-// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on),
-// then follows the chain's progress (s_prog): it twists rows 4-223 as rows
-// 401+ become final, and rows 0-3 once the chain's last step has made row 1
-// (s_done).  All of wave 3's loads precede its stores, so no row is
-// overwritten before it was read.  Wave 0, once its P1a chain is done,
-// stores P2b's final rows back as they are published (p2_p2b_out).
-constexpr int kTwIters = kAheadTwist / 4;
-__device__ __forceinline__ uint4 shfl4(const uint4 &v, int src) {
-  return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
-}
-// (e, ok: the board's episode and whether its pass 1 + P2a were this
-// episode's, read by every wave of the block before its barrier, so before
-// wave 2 rewrites the tag)
-__device__ __forceinline__ void p2_p2b(const P2Args &a, int b0, int lane, int w, int e, bool ok, uint32_t *s_row1,
-                                       int *s_done, int *s_prog) {
-  const int b = b0 + lane;
-  const bool act = b < a.n;
-  const size_t nr = (size_t)a.nrow;
-  uint32_t *slot = a.s_mt[3];
-  if (!__any(ok)) return;
-  if (w == 2) {
-    uint32_t *col = p2_col(kP2Reg, lane);
-#ifdef HZ_DIAG
-    const uint64_t tq = __builtin_amdgcn_s_memtime();
-#endif
-    {
-      P2Piece<312, 416, kP2bBase> p0;  // (row 312 is P2a's: loaded for the alignment, never written here)
-      p0.load(slot, nr, b0, lane);
-      p0.put(col);
+  const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
+  const int row_bytes = (int)(nr * 4);
+  constexpr int G0 = K == 0 ? 2 : R0;
+  constexpr int G = G0 + 8 * ((R1 - G0) / 8);
+  p2_span<G0, G, K == 2>(lane, rs, row_bytes, prev, s_prog);
+  p2_tail<G, R1, K == 2>(lane, rs, row_bytes, prev);
+  if (K < 2) {
+    if (ok) {
+      uint32_t *h = K == 0 ? a.p2h_w : a.p3h_w;
+      h[b] = prev;
+      h[nr + b] = first1;
+      a.s_tag[2 + K][b] = e * 8 + 3 + K;
     }
-    P2Piece<416, 520, kP2bBase> p1;
-    p1.load(slot, nr, b0, lane);
-#ifdef HZ_DIAG
-    if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 11] = __builtin_amdgcn_s_memtime() - tq;  // P2b staged
-#endif
-    uint32_t prev = act ? a.p2h_r[b] : 0u;
-    const uint32_t first1 = act ? a.p2h_r[nr + b] : 0u;
-    p2_chain<kP2aEnd, 408, 416, kP2bBase>(col, prev, s_prog);  // 313..407
-    p1.put(col);
-    P2Piece<520, kMT, kP2bBase> p2;
-    p2.load(slot, nr, b0, lane);
-    p2_chain<408, 512, 520, kP2bBase>(col, prev, s_prog);  // 408..511
-    p2.put(col);
-    p2_chain<512, kMT, kMT, kP2bBase>(col, prev, s_prog);  // 512..623
+  } else {
     p2_publish(s_prog, kMT);
     s_row1[lane] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
     p2_publish(s_done, 1);
-    if (ok) a.s_tag[3][b] = e * 8 + 4;
-    return;
+    if (ok) a.s_tag[4][b] = e * 8 + 5;
   }
+}
+
+// The twist (seed blocks, wave 3): rows [0, kAheadTwist) of the next
+// generation into P2c's slot (the stream at cursor kMTAhead): row r from
+// rows r, r + 1 (P2a's and P2b's, written to HBM by the two previous calls;
+// rows 0 and 1 from P2c) and r + 397 (P2b's below row 417, from HBM; P2c's
+// from LDS).  Lane: four boards, rows grp + 4 i, grp = lane / 16, so
+// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on.  It
+// loads its HBM rows once P2c is a few rows in (out of the launch's opening
+// burst), twists rows 4-223 as P2c publishes rows 417+ (s_prog), and rows
+// 0-3 once P2c's last step has made row 1 (s_done).  All its loads precede
+// its stores, so no row is overwritten before it was read.
+constexpr int kTwIters = kAheadTwist / 4;
+constexpr int kTwHbm = (kP2bEnd - 397 + 3) / 4;  // iterations whose rows r + 397 are P2b's (HBM)
+__device__ __forceinline__ uint4 shfl4(const uint4 &v, int src) {
+  return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+__device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool any, uint32_t *s_row1, int *s_done,
+                                         int *s_prog) {
+  if (!any) return;
+  const size_t nr = (size_t)a.nrow;
+  uint32_t *slot = a.s_mt[4];
   const int grp = lane >> 4, c4 = (lane & 15) * 4, up = (lane + 16) & 63;
   const uint32_t *colh = slot + b0 + c4;
-  // (the loads wait until the chain is a piece in: they stay out of the
-  // launch's opening burst, and land before the first twist needs them)
-  int have = p2_wait(s_prog, 360);
-  uint4 o[kTwIters + 1];
+  int have = p2_wait(s_prog, kP2bEnd + 8);
+  uint4 o[kTwIters + 1], fh[kTwHbm];
 #pragma unroll
   for (int i = 0; i <= kTwIters; i++) {
     const int r = grp + 4 * i;
     if (r >= 2) o[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
   }
+#pragma unroll
+  for (int i = 0; i < kTwHbm; i++) {
+    const int r = grp + 4 * i + 397;
+    if (r < kP2bEnd) fh[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
+  }
   auto twist_row = [&](int i, const uint4 &n1) {
     const int r = grp + 4 * i;
-    const uint32_t *f = hz_lds + kP2Reg + c4 * kP2RS + (r + 397 - kP2bBase);  // boards c4..c4+3: four columns
+    uint4 f;
+    if (i < kTwHbm && r + 397 < kP2bEnd) {
+      f = fh[i < kTwHbm ? i : 0];
+    } else {
+      const uint32_t *d = hz_lds + (r + 397) * kLdsStride + c4;
+      f = make_uint4(d[0], d[1], d[2], d[3]);
+    }
     uint4 v;
-    v.x = twist_word(o[i].x, n1.x, f[0]);
-    v.y = twist_word(o[i].y, n1.y, f[kP2RS]);
-    v.z = twist_word(o[i].z, n1.z, f[2 * kP2RS]);
-    v.w = twist_word(o[i].w, n1.w, f[3 * kP2RS]);
+    v.x = twist_word(o[i].x, n1.x, f.x);
+    v.y = twist_word(o[i].y, n1.y, f.y);
+    v.z = twist_word(o[i].z, n1.z, f.z);
+    v.w = twist_word(o[i].w, n1.w, f.w);
     *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v;
   };
 #pragma unroll
   for (int i = 1; i < kTwIters; i++) {
     const int need = 4 * i + 3 + 397 + 1;  // rows up to 4 i + 3 + 397 final
-    if (have < need) have = p2_wait(s_prog, need);
+    if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need);
     const uint4 t0 = shfl4(o[i], up), t1 = shfl4(o[i + 1], up);
     twist_row(i, grp < 3 ? t0 : t1);
   }
@@ -1643,33 +1588,30 @@ __device__ __forceinline__ void p2_p2b(const P2Args &a, int b0, int lane, int w,
   if (grp == 1) o[0] = make_uint4(s_row1[c4], s_row1[c4 + 1], s_row1[c4 + 2], s_row1[c4 + 3]);
   const uint4 t0 = shfl4(o[0], up), t1 = shfl4(o[1], up);
   twist_row(0, grp < 3 ? t0 : t1);
-  // (rows 224..312 keep P2a's words and rows 313..623 this stage's: the
-  // current generation's tail)
+  // (rows 224..623 keep pass 2's words: the current generation's tail)
 }
 
-// seed blocks: wave 0 P1a; wave 1 P2a; waves 2-3 P2b
+// seed blocks: waves 0-2 P2a, P2b, P2c; wave 3 the twist of P2c's episode
 __device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
   __shared__ uint32_t s_row1[kBlock];
   __shared__ int s_done, s_prog;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b0 = blk * kBlock, b = b0 + lane;
+  const bool act = b < a.n;
   if (tid == 0) {
     s_done = 0;
     s_prog = 0;
   }
-  // P2b's episode and decision, in every wave before the barrier
-  const int e7 = b < a.n ? a.ep_in[b] + 7 : 0;
-  const bool ok7 = b < a.n && a.s_tag[3][b] == e7 * 8 + 3;
+  // each stage's episode and decision (and P2c's for the twist wave), read
+  // before the barrier, so before any wave rewrites a tag
+  const int k = w < 3 ? w : 2;
+  const int e = act ? a.ep_in[b] + 9 - k : 0;
+  const bool ok = act && a.s_tag[2 + k][b] == e * 8 + 2 + k;
   __syncthreads();
-  if (w == 0) {
-    const bool p2b = __any(ok7);
-    if (b < a.n) p2_p1a(a, b0, lane);
-    p2_p2b_out(a, b0, lane, p2b, &s_prog, &s_done);
-  } else if (w == 1) {
-    p2_p2a(a, b0, lane);
-  } else {
-    p2_p2b(a, b0, lane, w, e7, ok7, s_row1, &s_done, &s_prog);
-  }
+  if (w == 0) p2_third<0>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
+  else if (w == 1) p2_third<1>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
+  else if (w == 2) p2_third<2>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
+  else p2_twist(a, b0, lane, __any(ok), s_row1, &s_done, &s_prog);
 }
 
 // a draw stage: draws [d0, d1) of episode e on its stream slot, from an LDS
@@ -1691,11 +1633,11 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
   const size_t nr = (size_t)a.nrow;
   const int d0 = kP2DrawsPer * stage, d1 = stage == 3 ? a.draws : min(a.draws, d0 + kP2DrawsPer);
   const int e = act ? a.ep_in[b] + 6 - stage : 0;
-  const uint32_t *slot = a.s_mt[4 + stage];
-  int32_t *cur = a.s_cur[4 + stage] + b;
+  const uint32_t *slot = a.s_mt[5 + stage];
+  int32_t *cur = a.s_cur[5 + stage] + b;
   const P2Draw &in = a.x_r[stage > 0 ? stage - 1 : 0];
   const P2Draw &out = stage == 3 ? a.pl_w : a.x_w[stage];
-  bool ok = act && a.s_tag[4 + stage][b] == e * 8 + 4;
+  bool ok = act && a.s_tag[5 + stage][b] == e * 8 + 5;
   int k0 = 0, c0 = kMTAhead;
   uint64_t bag = initial_bag(), q[kAheadWords] = {0, 0, 0, 0};
   if (stage > 0 && act) {  // (one round trip: used only if the tag matches)
@@ -1773,8 +1715,9 @@ __device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
   const int b0 = blk * kBlock;
   if (w < 2) {
     p2_draw_stage(a, b0, lane, 2 * y + w, w * kP2WinRows * kLdsStride);
-  } else if (w == 2 && !y && b0 + lane < a.n) {
-    p2_p1b(a, b0, lane);
+  } else if (w == 2 && b0 + lane < a.n) {
+    if (y) p2_p1a(a, b0, lane);
+    else p2_p1b(a, b0, lane);
   }
 }
 
@@ -1845,8 +1788,8 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
       const P2Mid &mi = st == 1 ? a.m1_r : a.m2_r;
       const uint32_t *hsrc = st == 0 ? a.h_a : st == 1 ? a.h_b : a.h_c;
       const int32_t *htag = st == 0 ? a.ht_a : st == 1 ? a.ht_b : a.ht_c;
-      uint32_t *slot = a.s_mt[8 + st] + b;
-      const int32_t *cur = a.s_cur[8 + st] + b;
+      uint32_t *slot = a.s_mt[9 + st] + b;
+      const int32_t *cur = a.s_cur[9 + st] + b;
       const int g_end = st == 0 ? min(a.cut1, a.max_plies) : st == 1 ? min(a.cut2, a.max_plies) : a.max_plies;
       const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
       // every input's loads issued together (used only if the tags match)
@@ -1876,7 +1819,7 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
         int cursor, src;
         if (prep) {
           cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
-          src = 2 + a.s_idx10;
+          src = 2 + a.s_idx11;
         } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
           mt_seed(hz_lds + lane, kLdsStride, sd);
           PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
@@ -1929,9 +1872,9 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
 #ifdef HZ_DIAG
   {  // wave durations per board, slot 4 role + wave: 0-3 play (C, B, A,
      // hashes: stamped in p2_play, before its barrier), 4-6 draw X (D1, D2,
-     // P1b), 8-9 draw Y (D3, D4), 12-15 seed (P1a, P2 chain, stagers)
+     // P1b), 8-10 draw Y (D3, D4, P1a), 12-15 seed (P2a, P2b, P2c, twist)
     const int w = threadIdx.x >> 6, bb = rb * kBlock + (threadIdx.x & 63);
-    const bool idle = (role == 1 && w == 3) || (role == 2 && w >= 2);
+    const bool idle = (role == 1 && w == 3) || (role == 2 && w == 3);
     if (g_stamps && role > 0 && !idle && bb < a.n) g_stamps[(size_t)bb * kP2Stamps + 4 * role + w] = __builtin_amdgcn_s_memtime() - t0;
   }
 #endif
@@ -2110,6 +2053,7 @@ static void free_p2(hz_env *e) {
   for (int k = 0; k < 2; k++) {
     f(e->p2_p1h[k]);
     f(e->p2_p2h[k]);
+    f(e->p2_p3h[k]);
     f(e->p2_ep[k]);
   }
 }
@@ -2153,7 +2097,8 @@ static int alloc_p2(hz_env *e) {
       ok = m(&mm.tag, nr * 4) && m(&mm.st, 6 * nr * 8) && m(&mm.q, 4 * nr * 8) && m(&mm.i, 3 * nr * 4);
     }
   for (int k = 0; ok && k < 2; k++)
-    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 2 * nr * 4) && m(&e->p2_ep[k], nr * 4);
+    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 2 * nr * 4) && m(&e->p2_p3h[k], 2 * nr * 4) &&
+         m(&e->p2_ep[k], nr * 4);
   if (!ok || p2_clear_tags(e)) {
     free_p2(e);
     return 1;
@@ -2202,11 +2147,13 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
     a.s_tag[s] = e->p2_s_tag[sl(s)];
     a.s_cur[s] = e->p2_s_cur[sl(s)];
   }
-  a.s_idx10 = sl(10);
+  a.s_idx11 = sl(11);
   a.p1h_w = e->p2_p1h[r];
   a.p1h_r = e->p2_p1h[w];
   a.p2h_w = e->p2_p2h[r];
   a.p2h_r = e->p2_p2h[w];
+  a.p3h_w = e->p2_p3h[r];
+  a.p3h_r = e->p2_p3h[w];
   for (int k = 0; k < 3; k++) {
     a.x_w[k] = e->p2_x[k][r];
     a.x_r[k] = e->p2_x[k][w];

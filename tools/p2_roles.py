@@ -19,14 +19,14 @@ for pipe in (1, 2):
     env = BatchedEnv(n, device="cuda")
     env.set_pipeline(pipe)
     names = ({0: "playC", 1: "playB", 2: "playA", 3: "hashes", 4: "D1", 5: "D2", 6: "P1b", 8: "D3", 9: "D4",
-              12: "P1a", 13: "P2a", 14: "P2b", 15: "P2b_twist", 7: "P2a_staged", 10: "P2a_chain_to_305",
-              11: "P2b_staged", 16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
+              10: "P1a", 12: "P2a", 13: "P2b", 14: "P2c", 15: "twist", 29: "P2a_staged", 30: "P2b_staged",
+              31: "P2c_staged", 16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
               22: "playC_loaded", 23: "playC_plies", 24: "playC_scored", 25: "D1_staged", 26: "D2_staged",
               27: "D3_staged", 28: "D4_staged"} if pipe == 2 else
              {5: "play", 6: "draw2", 15: "draw1", 7: "seed"})
     for only in (-1, 0, 1, 2, 3) if pipe == 2 else (-1,):
         L.hz_diag_set_role_only(-1)
-        for _ in range(12):
+        for _ in range(14):
             env.rollout(200, reset=True)
         L.hz_diag_set_role_only(only)
         stamps.zero_()
