@@ -48,7 +48,7 @@ BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 # hz_play launches until every board replays a fully prepared episode, by
-# pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's seven stages)
+# pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's twelve stages)
 PIPELINE_DEPTH = {1: 4, 2: 12}
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
@@ -69,8 +69,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--boards", type=int, default=4096)
-    ap.add_argument("--pipeline", type=int, choices=(1, 2), default=1,
-                    help="config 2: hz_play's pipeline (1 = chance-ahead k_rollout, 2 = k_play2's seven stages; "
+    ap.add_argument("--pipeline", type=int, choices=(1, 2), default=2,
+                    help="config 2: hz_play's pipeline (1 = chance-ahead k_rollout, 2 = k_play2's twelve stages; "
                          "identical results)")
     ap.add_argument("--launches-per-step", type=int, default=256,
                     help="config 2: hz_play launches (4096-board batches) per bench step")
@@ -1199,10 +1199,11 @@ def main():
                                       "on the other CUs (stream seeding, pile draws and rule hashes, none of which "
                                       "depends on moves); steady state: one preparation per game in the timed region"
                                       if args.pipeline == 1 else
-                                      "k_play2: each hz_play runs seven stages on seven consecutive episodes of every "
-                                      "board (seeding pass 1, pass 2, draws 0-7, 8-15, 16-23 + rule hashes, plies "
-                                      "0-39, the rest + scoring); steady state: one episode's worth of every stage per "
-                                      "call, i.e. one game per board per call"),
+                                      "k_play2: each hz_play runs twelve stages on twelve consecutive episodes of "
+                                      "every board (seeding pass 1 in two stages, pass 2 in three, pile draws 0-5, "
+                                      "6-11, 12-17, 18-23 + rule hashes, plies 0-23, 24-47, the rest + scoring); steady "
+                                      "state: one episode's worth of every stage per call, i.e. one game per board per "
+                                      "call"),
                              "pipeline_prime": prime,
                              "value_off": (off_steps / off_elapsed) if off_steps else None,
                              "ms_per_step_off": (off_elapsed * 1000.0 / args.steps) if off_steps else None},

@@ -2247,9 +2247,9 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   }
   ok = ok && hipDeviceSynchronize() == hipSuccess;
   e->seed_ahead = kAheadDraws;
-  {  // HZ_PIPELINE=2: hz_play's second pipeline by default (hz_env_set_pipeline)
+  {  // hz_play's pipeline: 2 by default, HZ_PIPELINE=1 for the first (hz_env_set_pipeline)
     const char *pv = getenv("HZ_PIPELINE");
-    e->pipeline = pv && atoi(pv) == 2 ? 2 : 1;
+    e->pipeline = pv && atoi(pv) == 1 ? 1 : 2;
     // HZ_P2_CUTS="a,b": pipeline 2's play stage boundaries (plies; multiples of 8)
     e->p2_cut1 = 24;
     e->p2_cut2 = 48;

@@ -57,9 +57,9 @@ class BatchedEnv:
         nat.check(nat.lib().hz_env_set_seed_ahead(self._h, int(draws) if enable else 0), "hz_env_set_seed_ahead")
 
     def set_pipeline(self, pipeline):
-        """hz_play's pipeline: 1 = chance-ahead (k_rollout), 2 = every game
-        spread over seven consecutive calls (k_play2); results are identical
-        either way (hz_env_set_pipeline)."""
+        """hz_play's pipeline: 2 (the default) = every game spread over twelve
+        consecutive calls (k_play2), 1 = chance-ahead (k_rollout); results
+        are identical either way (hz_env_set_pipeline)."""
         L = nat.lib()
         if not hasattr(L, "hz_env_set_pipeline") and int(pipeline) == 1:
             return  # (an older A/B build: pipeline 1 is all it has)

@@ -138,14 +138,14 @@ int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_s
 /* chance-ahead for hz_play: draws = piles prepared per board (0 = off,
  * capped at 24 = the default). */
 int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
-/* hz_play's pipeline: 1 (default; HZ_PIPELINE=2 in the environment at
- * hz_env_create makes 2 the default) = the chance-ahead pipeline above;
- * 2 = every board's game spread over seven consecutive calls, one stage per
- * call (seeding pass 1, pass 2, three draw stages, the first 40 plies, the
- * rest), all seven running in each launch on different episodes.  Same
- * results as pipeline 1; applies to calls with auto_reset = 0, no trajectory
- * outputs and max_plies >= 96 (others take pipeline 1).  Returns -1 for a
- * value other than 1 or 2. */
+/* hz_play's pipeline: 2 (the default; HZ_PIPELINE=1 in the environment at
+ * hz_env_create makes 1 the default) = every board's game spread over
+ * twelve consecutive calls, one stage per call (seeding pass 1 in two
+ * stages, pass 2 in three, four draw stages, three play stages), all twelve
+ * running in each launch on different episodes; 1 = the chance-ahead
+ * pipeline above.  Same results either way; pipeline 2 applies to calls with
+ * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
+ * pipeline 1).  Returns -1 for a value other than 1 or 2. */
 int hz_env_set_pipeline(hz_env *env, int32_t pipeline);
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
