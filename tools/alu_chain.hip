@@ -281,3 +281,115 @@ extern "C" int seed_var(int v, void *out, void *cyc, int blocks) {
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+// ---- pass-2 chain forms, one wave per CU (tools/alu_chain.py "p2chain"):
+// cycles per step of pass 2's recurrence over 616 steps with the step's
+// memory operations of each candidate layout (V):
+//  0 LDS column (stride 65) read 8 ahead + a b32 buffer store per step (P2a)
+//  1 LDS column read 8 ahead, no store
+//  2 no LDS (operand from registers) + a b32 buffer store per step
+//  3 no LDS, no store: the recurrence alone
+//  4 LDS board-major (lane's words contiguous, stride S words): b128 reads, no store
+//  5 as 4 + a b128 buffer store per 4 steps (board-major global)
+//  6 as 4 + a b32 buffer store per step (word-major global)
+//  7 no LDS + a b128 buffer store per 4 steps (board-major global)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+template <int V, int S>
+__global__ void __launch_bounds__(64) k_p2chain(uint32_t *gout, uint32_t *out, uint64_t *cyc) {
+  const int lane = threadIdx.x, b = blockIdx.x * 64 + lane;
+  constexpr bool BM = V >= 4 && V <= 6;  // board-major LDS
+  for (int i = 0; i < kMT; i++) {
+    if (BM) hz_lds[lane * S + i] = i * 2654435761u + b;
+    else hz_lds[i * 65 + lane] = i * 2654435761u + b;
+  }
+  __syncthreads();
+  const uint64_t base = (uint64_t)(gout + (size_t)blockIdx.x * 64 * kMT);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, 64 * kMT * 4, 0x00020000);
+  uint32_t prev = b * 7u + 1u, acc = 0;
+  const uint32_t *l = hz_lds + (BM ? lane * S : lane);
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  if constexpr (V <= 3 || V == 7) {
+    uint32_t cur[8], nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = V <= 1 ? l[(2 + u) * 65] : prev + u;
+#pragma unroll 2
+    for (int g = 2; g < 618; g += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) nx[u] = V <= 1 ? l[(g + 8 + u) * 65] : cur[u] ^ 0x9e3779b9u;
+      const uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
+      const int soff = __builtin_amdgcn_readfirstlane(g * 64 * 4);
+      uint32_t q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
+        uint32_t v;
+        asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
+        if (V == 0 || V == 2) __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, soff + u * 256, 0);
+        else if (V == 7) q[u] = v;
+        else acc ^= v;
+        prev = v;
+      }
+      if (V == 7) {
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{q[0], q[1], q[2], q[3]}, rs, lane * kMT * 4, g * 4, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{q[4], q[5], q[6], q[7]}, rs, lane * kMT * 4, g * 4 + 16, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) cur[u] = nx[u];
+    }
+  } else {
+    uint4 c0 = *reinterpret_cast<const uint4 *>(l + 4), c1 = *reinterpret_cast<const uint4 *>(l + 8);
+#pragma unroll 2
+    for (int g = 4; g < 620; g += 8) {
+      const uint4 n0 = *reinterpret_cast<const uint4 *>(l + g + 8), n1 = *reinterpret_cast<const uint4 *>(l + g + 12);
+      const uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
+      const int soff = __builtin_amdgcn_readfirstlane(g * 64 * 4);
+      const uint32_t cur[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
+        uint32_t v;
+        asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
+        if (V == 6) __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, soff + u * 256, 0);
+        else if (V == 5) q[u] = v;
+        else acc ^= v;
+        prev = v;
+      }
+      if (V == 5) {
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{q[0], q[1], q[2], q[3]}, rs, lane * kMT * 4, g * 4, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{q[4], q[5], q[6], q[7]}, rs, lane * kMT * 4, g * 4 + 16, 0);
+      }
+      c0 = n0;
+      c1 = n1;
+    }
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  out[b] = prev ^ acc;
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+extern "C" int p2chain(int v, int s, void *gout, void *out, void *cyc, int blocks) {
+  dim3 g(blocks), bl(64);
+  const int lds = 160 * 1024;
+#define P2C(V, S)                                                                                               \
+  do {                                                                                                          \
+    hipFuncSetAttribute((const void *)k_p2chain<V, S>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);       \
+    hipLaunchKernelGGL((k_p2chain<V, S>), g, bl, lds, 0, (uint32_t *)gout, (uint32_t *)out, (uint64_t *)cyc); \
+  } while (0)
+  switch (v * 1000 + s) {
+    case 0 * 1000 + 0: P2C(0, 628); break;
+    case 1 * 1000 + 0: P2C(1, 628); break;
+    case 2 * 1000 + 0: P2C(2, 628); break;
+    case 3 * 1000 + 0: P2C(3, 628); break;
+    case 4 * 1000 + 628: P2C(4, 628); break;
+    case 4 * 1000 + 632: P2C(4, 632); break;
+    case 5 * 1000 + 628: P2C(5, 628); break;
+    case 5 * 1000 + 632: P2C(5, 632); break;
+    case 6 * 1000 + 628: P2C(6, 628); break;
+    case 7 * 1000 + 0: P2C(7, 628); break;
+    default: return -1;
+  }
+#undef P2C
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

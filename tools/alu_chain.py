@@ -33,3 +33,20 @@ for v, nm in [(0, "mt_seed_lds"), (1, "pass1_lds"), (2, "pass1_nostore"), (3, "p
     outs[nm] = out[:64 * 64].cpu().numpy()
 sv["tab_equal"] = bool((outs["mt_seed_lds"] == outs["mt_seed_tab64"]).all())
 print(json.dumps(sv))
+# pass-2 chain forms (alu_chain.hip k_p2chain): cycles per step over 616 steps
+L = lib
+L.p2chain.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+gout = torch.zeros(64 * 64 * 624, dtype=torch.int32, device="cuda")
+pc = {}
+for v, s, nm in [(0, 0, "lds_col_read+b32_store (P2a)"), (1, 0, "lds_col_read"), (2, 0, "b32_store"), (3, 0, "bare"),
+                 (4, 628, "lds_bm_b128_read s628"), (4, 632, "lds_bm_b128_read s632"),
+                 (5, 628, "lds_bm_b128_read+b128_store/4 s628"), (5, 632, "lds_bm_b128_read+b128_store/4 s632"),
+                 (6, 628, "lds_bm_b128_read+b32_store"), (7, 0, "b128_store/4")]:
+    out = torch.zeros(64 * 64, dtype=torch.int32, device="cuda")
+    cyc = torch.zeros(64, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        assert L.p2chain(v, s, ctypes.c_void_p(gout.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                         ctypes.c_void_p(cyc.data_ptr()), 64) == 0
+    torch.cuda.synchronize()
+    pc[nm] = float(cyc.double().median().item()) / 616
+print(json.dumps({"p2chain_cycles_per_step": pc}))

@@ -12,21 +12,23 @@ from hzamd.env import BatchedEnv
 n = 4096
 L = nat.lib()
 L.hz_diag_set_stamps.argtypes = [ctypes.c_void_p]
-stamps = torch.zeros(n, 32, dtype=torch.int64, device="cuda")  # (k_play2 uses 32 slots per board)
+stamps = torch.zeros(n, 48, dtype=torch.int64, device="cuda")  # (k_play2 uses 48 slots per board)
 L.hz_diag_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
 out = {}
 for pipe in (1, 2):
     env = BatchedEnv(n, device="cuda")
     env.set_pipeline(pipe)
-    names = ({0: "playC", 1: "playB", 2: "playA", 3: "hashes", 4: "D1", 5: "D2", 6: "P1b", 8: "D3", 9: "D4",
-              10: "P1a", 12: "P2a", 13: "P2b", 14: "P2c", 15: "twist", 29: "P2a_staged", 30: "P2b_staged",
-              31: "P2c_staged", 16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
-              22: "playC_loaded", 23: "playC_plies", 24: "playC_scored", 25: "D1_staged", 26: "D2_staged",
-              27: "D3_staged", 28: "D4_staged"} if pipe == 2 else
+    names = ({0: "playD", 1: "playC", 2: "playB", 3: "playA", 4: "D1", 5: "D2", 6: "P1b", 7: "hashes", 8: "D3",
+              9: "D4", 10: "P1a", 12: "P2a", 13: "P2b", 14: "P2c", 15: "twist",
+              16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
+              22: "playC_loaded", 23: "playC_plies", 25: "playD_loaded", 26: "playD_plies", 27: "playD_scored",
+              28: "D1_staged", 29: "D2_staged", 30: "D3_staged", 31: "D4_staged",
+              32: "P2a_staged", 33: "P2b_staged", 34: "P2c_staged",
+              35: "twist_go", 36: "twist_it1", 37: "twist_looped", 38: "twist_done_seen"} if pipe == 2 else
              {5: "play", 6: "draw2", 15: "draw1", 7: "seed"})
     for only in (-1, 0, 1, 2, 3) if pipe == 2 else (-1,):
         L.hz_diag_set_role_only(-1)
-        for _ in range(14):
+        for _ in range(16):
             env.rollout(200, reset=True)
         L.hz_diag_set_role_only(only)
         stamps.zero_()
