@@ -48,8 +48,8 @@ BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 # hz_play launches until every board replays a fully prepared episode, by
-# pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's twelve stages)
-PIPELINE_DEPTH = {1: 4, 2: 12}
+# pipeline (1: seed -> draw1 -> draw2 -> play; 2: k_play2's thirteen stages)
+PIPELINE_DEPTH = {1: 4, 2: 13}
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 X6_PRODUCTS = 6                # bf16 MFMAs per fp32 product block in the x6 kernels
@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--boards", type=int, default=4096)
     ap.add_argument("--pipeline", type=int, choices=(1, 2), default=2,
-                    help="config 2: hz_play's pipeline (1 = chance-ahead k_rollout, 2 = k_play2's twelve stages; "
+                    help="config 2: hz_play's pipeline (1 = chance-ahead k_rollout, 2 = k_play2's thirteen stages; "
                          "identical results)")
     ap.add_argument("--launches-per-step", type=int, default=256,
                     help="config 2: hz_play launches (4096-board batches) per bench step")
@@ -81,7 +81,7 @@ def parse():
                     help="skip the chance-ahead-off comparison run (profiling)")
     ap.add_argument("--api-mode", action="store_true",
                     help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"))
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="1: one game at a time through the drop-in modules (profile_self_play.py); "
                          "2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
@@ -117,7 +117,10 @@ def parse():
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"], help="config 3 leaf-eval dtype")
     ap.add_argument("--full-game", action="store_true",
                     help="config 3: time one complete game on every board (games/s measured, not estimated)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.stub and args.config != 4:
+        ap.error("--stub applies to --config 4 only (the other configs time the network)")
+    return args
 
 
 _RED_DEV = None  # device of reduction tensors: the GPU under RCCL, the CPU under gloo
@@ -338,6 +341,11 @@ class TimedEvaluator:
         self.calls = 0
         self.snap_at = None  # call index whose leaf batch + outputs are kept (device copies) for nn_guard
         self.snap = None
+        # HZ_BENCH_CALL_DUMP=path: each call's live-row count is kept too (a
+        # device copy after the event pair) and call_stats() writes the
+        # per-call (rows, ms) lists there (tools/tail_trace.py)
+        self.dump = os.environ.get("HZ_BENCH_CALL_DUMP")
+        self.rowlog = []
 
     def attach(self, mcts):
         self.mcts = mcts
@@ -349,6 +357,10 @@ class TimedEvaluator:
         out = self.pred(board, glob, rows, count)
         b.record()
         self.events.append((a, b))
+        if self.dump:
+            self.rowlog.append(count.clone() if torch.is_tensor(count) else
+                               torch.full((1,), board.shape[0] if count is None else int(count),
+                                          dtype=torch.int32, device=board.device))
         if self.calls == self.snap_at:  # after the event pair: not part of the forward's time
             self.snap = (board.clone(), glob.clone(), None if count is None else count.clone(),
                          out[0].clone(), out[1].clone())
@@ -367,6 +379,7 @@ class TimedEvaluator:
     def reset(self):
         torch.cuda.synchronize()
         self.events.clear()
+        self.rowlog.clear()
         self._base = self.mcts.eval_rows_total.clone()
         self._ebase = self.mcts.edges_total.clone()
 
@@ -381,6 +394,10 @@ class TimedEvaluator:
         if not t.size:
             return None
         q = np.percentile(t, [50, 90, 99, 99.9])
+        if self.dump and self.rowlog:
+            rows = torch.cat([r.view(-1)[:1].to(torch.int64) for r in self.rowlog]).cpu().numpy()
+            with open(self.dump, "w") as f:
+                json.dump({"rows": rows.tolist(), "ms": t.tolist()}, f)
         return {"calls": int(t.size), "mean_ms": float(t.mean()), "std_ms": float(t.std()), "p50_ms": float(q[0]),
                 "p90_ms": float(q[1]), "p99_ms": float(q[2]), "p999_ms": float(q[3]), "max_ms": float(t.max()),
                 "calls_over_2x_p50": int((t > 2 * q[0]).sum())}
@@ -542,6 +559,7 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
             "env_steps_per_s": world * env_steps / elapsed,
             "nn_rows_evaluated": rows, "nn_rows_skipped": moves * sims - rows, "nn_s": nn_ms * 1e-3,
             "nn_tflops": flops_per_eval() * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
+            "nn_call_ms": ev.call_stats(),
         }))
 
 
@@ -1122,9 +1140,16 @@ def main():
     issue = {"kernel_cycles": cycles, "longest_game_plies": longest,
              "cycles_per_ply_longest_game": cycles / max(1, longest),
              "cycles_per_mt_seed_step": cycles / MT_SEED_STEPS, "mt_step_floor_cycles": MT_STEP_FLOOR_CYCLES,
-             "note": f"a launch is the longest serial per-lane chain of its roles (one board's whole game, or a "
-                     f"stream's {MT_SEED_STEPS}-step seeding) at {CLOCK_GHZ} GHz; the bare MT recurrence costs "
-                     f"{MT_STEP_FLOOR_CYCLES} cycles/step (tools/alu_chain.py), DESIGN.md §3"}
+             "note": (f"a launch is the longest serial per-lane chain of its roles (one board's whole game, or a "
+                      f"stream's {MT_SEED_STEPS}-step seeding) at {CLOCK_GHZ} GHz; the bare MT recurrence costs "
+                      f"{MT_STEP_FLOOR_CYCLES} cycles/step (tools/alu_chain.py), DESIGN.md §3"
+                      if kname == "k_rollout" else
+                      f"k_play2 runs thirteen stages side by side, one per episode in flight: the game cut into four "
+                      f"play stages, the {MT_SEED_STEPS}-step seeding chain into five stages of 207-312 steps, the "
+                      f"draws into four; a launch lasts as long as its longest stage (tools/p2_roles.py), so "
+                      f"cycles_per_mt_seed_step and cycles_per_ply_longest_game are the launch divided by the whole "
+                      f"chain, a per-launch proxy; the bare recurrence costs {MT_STEP_FLOOR_CYCLES} cycles/step and "
+                      f"a step with its b32 LDS read and HBM store ~56 (tools/alu_chain.py), DESIGN.md §3")}
 
     # the same workload with chance-ahead off (every launch seeds and draws
     # in-kernel), for comparison; not the headline number
@@ -1199,9 +1224,10 @@ def main():
                                       "on the other CUs (stream seeding, pile draws and rule hashes, none of which "
                                       "depends on moves); steady state: one preparation per game in the timed region"
                                       if args.pipeline == 1 else
-                                      "k_play2: each hz_play runs twelve stages on twelve consecutive episodes of "
-                                      "every board (seeding pass 1 in two stages, pass 2 in three, pile draws 0-5, "
-                                      "6-11, 12-17, 18-23 + rule hashes, plies 0-23, 24-47, the rest + scoring); steady "
+                                      "k_play2: each hz_play runs thirteen stages on thirteen consecutive episodes "
+                                      "of every board (seeding pass 1 in two stages, pass 2 in three, pile draws 0-5, "
+                                      "6-11, 12-17, 18-23 + rule hashes, plies 0-23, 24-39, 40-55, the rest + scoring); "
+                                      "steady "
                                       "state: one episode's worth of every stage per call, i.e. one game per board per "
                                       "call"),
                              "pipeline_prime": prime,

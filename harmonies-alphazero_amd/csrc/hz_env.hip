@@ -66,10 +66,10 @@ struct hz_env {
   int32_t *mt_src;           // [n]
   int lazy;                  // some board may have mt_src >= 0
   // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
-  // spread over twelve consecutive hz_play calls, one stage per call
+  // spread over thirteen consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
   int calls2, primed2;
-  int p2_cut1, p2_cut2;      // the play stages' ply boundaries (HZ_P2_CUTS)
+  int p2_cut[3];             // the play stages' ply boundaries (HZ_P2_CUTS)
   uint32_t *p2_s[14];        // [624][nrow] stream slots (kP2Stream)
   int32_t *p2_s_tag[14];     // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
   int32_t *p2_s_cur[14];     // [kAheadDraws + 1][nrow] the slot's cursor before draw 0 and after each draw
@@ -77,10 +77,10 @@ struct hz_env {
   uint32_t *p2_p2h[2];       // [2][nrow] P2a -> P2b
   uint32_t *p2_p3h[2];       // [2][nrow] P2b -> P2c
   P2Draw p2_x[3][2];         // D1 -> D2 -> D3 -> D4, by call parity
-  P2Draw p2_pl[4];           // D4 -> playA, playB, playC: a ring of four
-  P2Mid p2_m[2][2];          // playA -> playB, playB -> playC, by call parity
-  uint32_t *p2_h[4];         // [kRulePlies][nrow] rule hashes, a ring of four
-  int32_t *p2_h_tag[4];      // [nrow] their episode
+  P2Draw p2_pl[5];           // D4 -> playA, playB, playC, playD: a ring of five
+  P2Mid p2_m[3][2];          // playA -> playB -> playC -> playD, by call parity
+  uint32_t *p2_h[5];         // [kRulePlies][nrow] rule hashes, a ring of five
+  int32_t *p2_h_tag[5];      // [nrow] their episode
   int32_t *p2_ep[2];         // [nrow] episode counter each board ended the call with
 };
 
@@ -1095,10 +1095,11 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // hz_play's second pipeline (hz_env_set_pipeline(e, 2)).  Each of
 // k_rollout's roles runs one serial per-board chain of ~60 k cycles (a whole
 // game, a whole seeding, 16 pile draws), and a launch lasts as long as its
-// longest chain.  Here every board's episode is cut into twelve stages of
-// 20-35 k cycles, one per consecutive hz_play call, and one launch runs all
-// twelve at once, each on a different episode of the board (ep = the episode
-// counter the previous call left, p2_ep; stage s works on episode ep + 11 - s):
+// longest chain.  Here every board's episode is cut into thirteen stages of
+// 20-30 k cycles, one per consecutive hz_play call, and one launch runs all
+// thirteen at once, each on a different episode of the board (ep = the
+// episode counter the previous call left, p2_ep; stage s works on episode
+// ep + 12 - s):
 //   s = 0  P1a   seeding pass 1, steps 1-312          draw-Y blocks, wave 2
 //   s = 1  P1b   pass 1, steps 313-624                draw-X blocks, wave 2
 //   s = 2  P2a   pass 2, steps 2-208                  seed blocks, wave 0
@@ -1109,31 +1110,35 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 //   s = 6  D2    draws 6-11                           draw-X blocks, wave 1
 //   s = 7  D3    draws 12-17                          draw-Y blocks, wave 0
 //   s = 8  D4    draws 18-23                          draw-Y blocks, wave 1
-//          (the episode's rule hashes meanwhile:      play blocks, wave 3)
-//   s = 9  playA plies [0, cut1)                      play blocks, wave 2
-//   s = 10 playB plies [cut1, cut2)                   play blocks, wave 1
-//   s = 11 playC the rest, final scoring, the board's play blocks, wave 0
+//          (the episode's rule hashes meanwhile:      draw-X blocks, wave 3)
+//   s = 9  playA plies [0, cut0)                      play blocks, wave 3
+//   s = 10 playB plies [cut0, cut1)                   play blocks, wave 2
+//   s = 11 playC plies [cut1, cut2)                   play blocks, wave 1
+//   s = 12 playD the rest, final scoring, the board's play blocks, wave 0
 //                state, cursor and counters
 // An episode's stream lives in one slot of a ring of kP2Stream from P1a to
-// playC (and afterwards as the board's current stream until materialize or
+// playD (and afterwards as the board's current stream until materialize or
 // the next call); stage s of call c uses slot (c - s) mod kP2Stream.  A stage
 // uses an input only when its tag names the stage's episode, so a wrong
-// prediction costs time, never results: the stages skip the board and playC
+// prediction costs time, never results: the stages skip the board and playD
 // plays its whole game from scratch (seeding and drawing in LDS, like
 // k_rollout's unprepared boards).  The results are k_rollout's: the board ends
 // the call with episode ep's final state, cursor and counters, and
-// games_done / steps_done count that game (its first plies ran in the two
-// calls before, in playA and playB).  In steady state a call does every
-// stage once per board: one game's worth of work per board per call.
+// games_done / steps_done count that game (its first plies ran in the three
+// calls before, in playA, playB and playC).  In steady state a call does
+// every stage once per board: one game's worth of work per board per call.
 constexpr int kP2Win = 96;        // rows a draw stage stages, from its wave's lowest cursor
 constexpr int kP2WinRows = kP2Win + 24;  // LDS rows per window (a scan reads up to 23 rows past its cursor)
-constexpr int kP2Stages = 12;
-constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: playC's slot stays the board's stream)
+constexpr int kP2Play = 4;        // play stages
+constexpr int kP2Stages = 9 + kP2Play;
+constexpr int kP2Last = kP2Stages - 1;  // stage s works on episode ep + kP2Last - s
+constexpr int kP2Ring = kP2Play + 1;    // D4's scripts and the rule hashes: read by the play stages 1..kP2Play calls later
+constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: the last play stage's slot stays the board's stream)
 constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
 constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
 constexpr int kP1Split = 313;
 #ifdef HZ_DIAG
-constexpr int kP2Stamps = 32;  // stamp slots per board in k_play2 (tools/p2_roles.py)
+constexpr int kP2Stamps = 48;  // stamp slots per board in k_play2 (tools/p2_roles.py)
 #define P2_PHASE(slot, t0)                                                                                       \
   do {                                                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                                                           \
@@ -1154,7 +1159,8 @@ struct P2Args {
   uint32_t *mt;
   int32_t *pos, *ply, *episode;
   uint64_t *seed;
-  int n, max_plies, draws, cut1, cut2;
+  int n, max_plies, draws;
+  int cut[kP2Play - 1];
   uint64_t seed_base;
   long nrow;
   int32_t *games_done, *steps_done, *mt_src;
@@ -1163,7 +1169,7 @@ struct P2Args {
   uint32_t *s_mt[kP2Stages];  // the stream slot of each stage this call
   int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
   int32_t *s_cur[kP2Stages];  // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
-  int s_idx11;                // playC's slot index (materialize: mt_src = 2 + index)
+  int s_idx_last;             // the last play stage's slot index (materialize: mt_src = 2 + index)
   uint32_t *p1h_w;            // [nrow] P1a -> P1b: pass 1's last value
   const uint32_t *p1h_r;
   uint32_t *p2h_w;            // [2][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word
@@ -1171,12 +1177,12 @@ struct P2Args {
   uint32_t *p3h_w;            // [2][nrow] P2b -> P2c: the same
   const uint32_t *p3h_r;
   P2Draw x_w[3], x_r[3];      // D1 -> D2 -> D3 -> D4 (tag: episode * 8 + stages done)
-  P2Draw pl_w, pl_a, pl_b, pl_c;  // D4's script: written this call; read by playA, playB, playC
-  P2Mid m1_w, m1_r, m2_w, m2_r;   // playA -> playB -> playC
+  P2Draw pl_w, pl_r[kP2Play];     // D4's script: written this call; read by play stage st (st + 1 calls later)
+  P2Mid m_w[kP2Play - 1], m_r[kP2Play - 1];  // play stage st -> st + 1 (written / read this call)
   uint32_t *h_w;                  // [kRulePlies][nrow] rule hashes
-  const uint32_t *h_a, *h_b, *h_c;
+  const uint32_t *h_r[kP2Play];
   int32_t *ht_w;                  // [nrow] their episode
-  const int32_t *ht_a, *ht_b, *ht_c;
+  const int32_t *ht_r[kP2Play];
 };
 
 // PlayDraw for the prepared stages: the pile script in registers, then (a
@@ -1349,7 +1355,7 @@ __device__ __forceinline__ void p2_keys(uint64_t seed, uint32_t &kA, uint32_t &k
 __device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
   const int b = b0 + lane;
   const size_t nr = (size_t)a.nrow;
-  const int e = a.ep_in[b] + 11;
+  const int e = a.ep_in[b] + kP2Last;
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
   uint32_t prev = 19650218u;
@@ -1360,7 +1366,7 @@ __device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
 __device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
   const int b = b0 + lane;
   const size_t nr = (size_t)a.nrow;
-  const int e = a.ep_in[b] + 10;
+  const int e = a.ep_in[b] + kP2Last - 1;
   if (a.s_tag[1][b] != e * 8 + 1) return;
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
@@ -1494,7 +1500,7 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
   constexpr int R0 = K == 0 ? 1 : K == 1 ? kP2aEnd : kP2bEnd, R1 = K == 0 ? kP2aEnd : K == 1 ? kP2bEnd : kMT;
   p2_stage<R0, R1>(slot, nr, b0, lane);
 #ifdef HZ_DIAG
-  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 29 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
+  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 32 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
 #endif
   uint32_t prev, first1;
   if (K == 0) {
@@ -1531,11 +1537,17 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
 // rows r, r + 1 (P2a's and P2b's, written to HBM by the two previous calls;
 // rows 0 and 1 from P2c) and r + 397 (P2b's below row 417, from HBM; P2c's
 // from LDS).  Lane: four boards, rows grp + 4 i, grp = lane / 16, so
-// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on.  It
-// loads its HBM rows once P2c is a few rows in (out of the launch's opening
-// burst), twists rows 4-223 as P2c publishes rows 417+ (s_prog), and rows
+// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on
+// (one shuffle per row: each lane exposes the word its reader needs, grp 0
+// the next iteration's).  The wave loads its HBM rows at once, twists rows
+// 4-223 two iterations (one publish of P2c's) per wait as P2c publishes rows
+// 417+ (s_prog), with the pair's LDS operations issued together, and rows
 // 0-3 once P2c's last step has made row 1 (s_done).  All its loads precede
-// its stores, so no row is overwritten before it was read.
+// its stores, so no row is overwritten before it was read.  (Measured: the
+// loop runs at about P2c's pace, ~365 cycles per four rows, so the wave
+// ends as long after P2c as its loads take to land; replacing the old words
+// by their far-row-independent parts first, in any layout, cost more than
+// it saved: profiles/r04/p2/.)
 constexpr int kTwIters = kAheadTwist / 4;
 constexpr int kTwHbm = (kP2bEnd - 397 + 3) / 4;  // iterations whose rows r + 397 are P2b's (HBM)
 __device__ __forceinline__ uint4 shfl4(const uint4 &v, int src) {
@@ -1548,7 +1560,10 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
   uint32_t *slot = a.s_mt[4];
   const int grp = lane >> 4, c4 = (lane & 15) * 4, up = (lane + 16) & 63;
   const uint32_t *colh = slot + b0 + c4;
-  int have = p2_wait(s_prog, kP2bEnd + 8);
+#ifdef HZ_DIAG
+  const int b = b0 + lane;
+  const uint64_t tz = __builtin_amdgcn_s_memtime();
+#endif
   uint4 o[kTwIters + 1], fh[kTwHbm];
 #pragma unroll
   for (int i = 0; i <= kTwIters; i++) {
@@ -1560,6 +1575,8 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
     const int r = grp + 4 * i + 397;
     if (r < kP2bEnd) fh[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
   }
+  int have = p2_wait(s_prog, kP2bEnd + 8);
+  P2_PHASE(35, tz);
   auto twist_row = [&](int i, const uint4 &n1) {
     const int r = grp + 4 * i;
     uint4 f;
@@ -1576,18 +1593,29 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
     v.w = twist_word(o[i].w, n1.w, f.w);
     *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v;
   };
+  // row r's next row, from lane + 16 (grp 3: grp 0's next iteration)
+  auto next_row = [&](int i) { return shfl4(grp == 0 ? o[i + 1] : o[i], up); };
 #pragma unroll
-  for (int i = 1; i < kTwIters; i++) {
-    const int need = 4 * i + 3 + 397 + 1;  // rows up to 4 i + 3 + 397 final
+  for (int i = 1; i < kTwIters; i += 2) {
+    const bool two = i + 1 < kTwIters;
+    const int need = 4 * (two ? i + 1 : i) + 3 + 397 + 1;  // rows up to the pair's last r + 397 final
     if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need);
-    const uint4 t0 = shfl4(o[i], up), t1 = shfl4(o[i + 1], up);
-    twist_row(i, grp < 3 ? t0 : t1);
+    const uint4 n0 = next_row(i);
+    if (two) {
+      const uint4 n1 = next_row(i + 1);
+      twist_row(i, n0);
+      twist_row(i + 1, n1);
+    } else {
+      twist_row(i, n0);
+    }
+    if (i == 1) P2_PHASE(36, tz);
   }
+  P2_PHASE(37, tz);
   p2_wait(s_done, 1);
+  P2_PHASE(38, tz);
   if (grp == 0) o[0] = make_uint4(0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u);
   if (grp == 1) o[0] = make_uint4(s_row1[c4], s_row1[c4 + 1], s_row1[c4 + 2], s_row1[c4 + 3]);
-  const uint4 t0 = shfl4(o[0], up), t1 = shfl4(o[1], up);
-  twist_row(0, grp < 3 ? t0 : t1);
+  twist_row(0, next_row(0));
   // (rows 224..623 keep pass 2's words: the current generation's tail)
 }
 
@@ -1605,7 +1633,7 @@ __device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
   // each stage's episode and decision (and P2c's for the twist wave), read
   // before the barrier, so before any wave rewrites a tag
   const int k = w < 3 ? w : 2;
-  const int e = act ? a.ep_in[b] + 9 - k : 0;
+  const int e = act ? a.ep_in[b] + kP2Last - 2 - k : 0;
   const bool ok = act && a.s_tag[2 + k][b] == e * 8 + 2 + k;
   __syncthreads();
   if (w == 0) p2_third<0>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
@@ -1632,7 +1660,7 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
   const int d0 = kP2DrawsPer * stage, d1 = stage == 3 ? a.draws : min(a.draws, d0 + kP2DrawsPer);
-  const int e = act ? a.ep_in[b] + 6 - stage : 0;
+  const int e = act ? a.ep_in[b] + kP2Last - 5 - stage : 0;
   const uint32_t *slot = a.s_mt[5 + stage];
   int32_t *cur = a.s_cur[5 + stage] + b;
   const P2Draw &in = a.x_r[stage > 0 ? stage - 1 : 0];
@@ -1669,7 +1697,7 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
       dd[3] = v[u].w;
     }
   }
-  P2_PHASE(25 + stage, t0);  // window staged
+  P2_PHASE(28 + stage, t0);  // window staged
   if (!act) return;
   if (!ok) {
     out.tag[b] = -1;
@@ -1708,8 +1736,20 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
   out.tag[b] = e * 8 + stage + 1;
 }
 
-// draw-X blocks: D1 (wave 0), D2 (wave 1), P1b (wave 2); draw-Y blocks: D3,
-// D4 (waves 0, 1).  Each draw wave stages its own window and reads only it.
+// the rule hashes of D4's episode (read by the play stages in the next
+// kP2Play calls)
+__device__ __forceinline__ void p2_hashes(const P2Args &a, int b) {
+  const size_t nr = (size_t)a.nrow;
+  const int e = a.ep_in[b] + kP2Last - 8;
+  const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
+#pragma unroll 1
+  for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
+  a.ht_w[b] = e;
+}
+
+// draw-X blocks: D1 (wave 0), D2 (wave 1), P1b (wave 2), the rule hashes
+// (wave 3); draw-Y blocks: D3, D4 (waves 0, 1), P1a (wave 2).  Each draw
+// wave stages its own window and reads only it.
 __device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b0 = blk * kBlock;
@@ -1718,6 +1758,8 @@ __device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
   } else if (w == 2 && b0 + lane < a.n) {
     if (y) p2_p1a(a, b0, lane);
     else p2_p1b(a, b0, lane);
+  } else if (w == 3 && !y && b0 + lane < a.n) {
+    p2_hashes(a, b0 + lane);
   }
 }
 
@@ -1751,12 +1793,11 @@ __device__ __forceinline__ PlayDraw2 p2_mid_get(const P2Mid &m, size_t nr, int b
                    MTR(slot, (int)nr, fc >= 0 ? fc : 0), cur + (size_t)nd * nr};
 }
 
-// play blocks: wave 2 playA (episode ep + 2), wave 1 playB (ep + 1), wave 0
-// playC (the rest of episode ep, or all of it), wave 3 the rule hashes of
-// episode ep + 3.  The three play stages run one code path (st = 2 - wave),
-// so the block's three playing waves share one copy of the ply loop in the
-// instruction cache (three inlined copies of it, ~50 KB each, thrashed the
-// cache the two CUs of a pair share).
+// play blocks: wave 3 - st runs play stage st on episode ep + kP2Play - 1 -
+// st (the last stage, wave 0: the rest of episode ep, or all of it).  The
+// stages run one code path (st wave-uniform), so the block's four waves
+// share one copy of the ply loop in the instruction cache (one inlined copy
+// per stage, ~50 KB each, thrashed the cache the two CUs of a pair share).
 __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
   __shared__ uint64_t s_lds_mask;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1768,88 +1809,75 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
 #ifdef HZ_DIAG
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  if (w == 3) {
-    if (act) {
-      const int e = a.ep_in[b] + 3;
-      const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
-#pragma unroll 1
-      for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
-      a.ht_w[b] = e;
-#ifdef HZ_DIAG
-      if (g_stamps) g_stamps[(size_t)b * kP2Stamps + 3] = __builtin_amdgcn_s_memtime() - t0;  // hashes
-#endif
+  const int st = __builtin_amdgcn_readfirstlane(kP2Play - 1 - w);  // 0 playA .. kP2Play - 1 the last
+  const bool last = st == kP2Play - 1;
+  bool lds_used = false;
+  if (act) {
+    const int e = last ? a.episode[b] : a.ep_in[b] + kP2Play - 1 - st;
+    const P2Draw &pl = a.pl_r[st];
+    const uint32_t *hsrc = a.h_r[st];
+    const int32_t *htag = a.ht_r[st];
+    uint32_t *slot = a.s_mt[9 + st] + b;
+    const int32_t *cur = a.s_cur[9 + st] + b;
+    const int g_end = last ? a.max_plies : min(a.cut[st], a.max_plies);
+    const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
+    // every input's loads issued together (used only if the tags match)
+    const int ptag = pl.tag[b], nd = pl.k[b];
+    const int mtag = st > 0 ? a.m_r[st - 1].tag[b] : e;
+    const uint32_t *hs = htag[b] == e ? hsrc + b : nullptr;
+    State s;
+    int g = 0;
+    PlayDraw2 draw = st == 0 ? PlayDraw2{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
+                                         MTR(slot, (int)nr, 0), cur + (size_t)nd * nr}
+                             : p2_mid_get(a.m_r[st - 1], nr, b, s, g, nd, slot, cur);
+    const bool prep = ptag == e * 8 + 4 && mtag == e;
+    if (prep) {
+      if (st == 0) {
+        if (__all(nd >= 5)) draw.scripted_reset(s);
+        else reset_state(s, draw);
+      }
+      P2_PHASE(16 + 3 * st, t0);
+      g += p2_plies(s, draw, g, g_end, rk, hs, nr);
+      P2_PHASE(17 + 3 * st, t0);
     }
-  } else {
-    const int st = __builtin_amdgcn_readfirstlane(2 - w);  // 0 playA, 1 playB, 2 playC
-    bool lds_used = false;
-    if (act) {
-      const int e = st == 2 ? a.episode[b] : a.ep_in[b] + 2 - st;
-      const P2Draw &pl = st == 0 ? a.pl_a : st == 1 ? a.pl_b : a.pl_c;
-      const P2Mid &mi = st == 1 ? a.m1_r : a.m2_r;
-      const uint32_t *hsrc = st == 0 ? a.h_a : st == 1 ? a.h_b : a.h_c;
-      const int32_t *htag = st == 0 ? a.ht_a : st == 1 ? a.ht_b : a.ht_c;
-      uint32_t *slot = a.s_mt[9 + st] + b;
-      const int32_t *cur = a.s_cur[9 + st] + b;
-      const int g_end = st == 0 ? min(a.cut1, a.max_plies) : st == 1 ? min(a.cut2, a.max_plies) : a.max_plies;
-      const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
-      // every input's loads issued together (used only if the tags match)
-      const int ptag = pl.tag[b], nd = pl.k[b];
-      const int mtag = st > 0 ? mi.tag[b] : e;
-      const uint32_t *hs = htag[b] == e ? hsrc + b : nullptr;
-      State s;
-      int g = 0;
-      PlayDraw2 draw = st == 0 ? PlayDraw2{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
-                                           MTR(slot, (int)nr, 0), cur + (size_t)nd * nr}
-                               : p2_mid_get(mi, nr, b, s, g, nd, slot, cur);
-      const bool prep = ptag == e * 8 + 4 && mtag == e;
+    if (!last) {
+      const P2Mid &mo = a.m_w[st];
+      if (prep) p2_mid_put(mo, nr, b, s, draw, g, e);
+      else mo.tag[b] = -1;
+    } else {
+      int cursor, src;
       if (prep) {
-        if (st == 0) {
-          if (__all(nd >= 5)) draw.scripted_reset(s);
-          else reset_state(s, draw);
-        }
-        P2_PHASE(16 + 3 * st, t0);
-        g += p2_plies(s, draw, g, g_end, rk, hs, nr);
-        P2_PHASE(17 + 3 * st, t0);
+        cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
+        src = 2 + a.s_idx_last;
+      } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
+        mt_seed(hz_lds + lane, kLdsStride, sd);
+        PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
+        reset_state(s, fb);
+        g = p2_plies(s, fb, 0, a.max_plies, rk, nullptr, nr);
+        cursor = fb.m.cursor();
+        src = -1;
+        lds_used = true;
       }
-      if (st < 2) {
-        const P2Mid &mo = st == 0 ? a.m1_w : a.m2_w;
-        if (prep) p2_mid_put(mo, nr, b, s, draw, g, e);
-        else mo.tag[b] = -1;
-      } else {
-        int cursor, src;
-        if (prep) {
-          cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
-          src = 2 + a.s_idx11;
-        } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
-          mt_seed(hz_lds + lane, kLdsStride, sd);
-          PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
-          reset_state(s, fb);
-          g = p2_plies(s, fb, 0, a.max_plies, rk, nullptr, nr);
-          cursor = fb.m.cursor();
-          src = -1;
-          lds_used = true;
-        }
-        a.episode[b] = e + 1;
-        if (score_pending(s.misc)) finish_game(s);
-        P2_PHASE(24, t0);
-        store_state(a.st, a.n, b, s);
-        a.pos[b] = cursor;
-        a.mt_src[b] = src;
-        a.ply[b] = g;
-        a.seed[b] = sd;
-        a.ep_out[b] = e + 1;
-        // the game this call completes, as hz_play's other pipeline counts it
-        if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
-        if (a.steps_done) a.steps_done[b] = g;
-      }
+      a.episode[b] = e + 1;
+      if (score_pending(s.misc)) finish_game(s);
+      P2_PHASE(27, t0);
+      store_state(a.st, a.n, b, s);
+      a.pos[b] = cursor;
+      a.mt_src[b] = src;
+      a.ply[b] = g;
+      a.seed[b] = sd;
+      a.ep_out[b] = e + 1;
+      // the game this call completes, as hz_play's other pipeline counts it
+      if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
+      if (a.steps_done) a.steps_done[b] = g;
+    }
 #ifdef HZ_DIAG
-      if (g_stamps) g_stamps[(size_t)b * kP2Stamps + w] = __builtin_amdgcn_s_memtime() - t0;  // playC, B, A
+    if (g_stamps) g_stamps[(size_t)b * kP2Stamps + w] = __builtin_amdgcn_s_memtime() - t0;  // last .. playA
 #endif
-    }
-    if (w == 0) {
-      const uint64_t lm = __ballot(lds_used);
-      if (lane == 0) s_lds_mask = lm;
-    }
+  }
+  if (w == 0) {
+    const uint64_t lm = __ballot(lds_used);
+    if (lane == 0) s_lds_mask = lm;
   }
   __syncthreads();
   const uint64_t lds_mask = s_lds_mask & actmask;
@@ -1870,11 +1898,11 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
   else if (role == 3) p2_seed(a, rb);
   else p2_draw(a, rb, role - 1);
 #ifdef HZ_DIAG
-  {  // wave durations per board, slot 4 role + wave: 0-3 play (C, B, A,
-     // hashes: stamped in p2_play, before its barrier), 4-6 draw X (D1, D2,
-     // P1b), 8-10 draw Y (D3, D4, P1a), 12-15 seed (P2a, P2b, P2c, twist)
+  {  // wave durations per board, slot 4 role + wave: 0-3 play (D, C, B, A:
+     // stamped in p2_play, before its barrier), 4-7 draw X (D1, D2, P1b,
+     // hashes), 8-10 draw Y (D3, D4, P1a), 12-15 seed (P2a, P2b, P2c, twist)
     const int w = threadIdx.x >> 6, bb = rb * kBlock + (threadIdx.x & 63);
-    const bool idle = (role == 1 && w == 3) || (role == 2 && w == 3);
+    const bool idle = role == 2 && w == 3;
     if (g_stamps && role > 0 && !idle && bb < a.n) g_stamps[(size_t)bb * kP2Stamps + 4 * role + w] = __builtin_amdgcn_s_memtime() - t0;
   }
 #endif
@@ -2037,8 +2065,8 @@ static void free_p2(hz_env *e) {
     f(d.c);
   };
   for (int k = 0; k < 3; k++) fd(e->p2_x[k][0]), fd(e->p2_x[k][1]);
-  for (int k = 0; k < 4; k++) fd(e->p2_pl[k]);
-  for (int k = 0; k < 2; k++)
+  for (int k = 0; k < kP2Ring; k++) fd(e->p2_pl[k]);
+  for (int k = 0; k < kP2Play - 1; k++)
     for (int j = 0; j < 2; j++) {
       P2Mid &m = e->p2_m[k][j];
       f(m.tag);
@@ -2046,7 +2074,7 @@ static void free_p2(hz_env *e) {
       f(m.q);
       f(m.i);
     }
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < kP2Ring; k++) {
     f(e->p2_h[k]);
     f(e->p2_h_tag[k]);
   }
@@ -2068,14 +2096,14 @@ static int p2_clear_tags(hz_env *e) {
     if (c(e->p2_s_tag[k])) return 1;
   for (int k = 0; k < 3; k++)
     if (c(e->p2_x[k][0].tag) || c(e->p2_x[k][1].tag)) return 1;
-  for (int k = 0; k < 4; k++)
+  for (int k = 0; k < kP2Ring; k++)
     if (c(e->p2_pl[k].tag) || c(e->p2_h_tag[k])) return 1;
-  for (int k = 0; k < 2; k++)
+  for (int k = 0; k < kP2Play - 1; k++)
     if (c(e->p2_m[k][0].tag) || c(e->p2_m[k][1].tag)) return 1;
   return 0;
 }
 
-// allocated on first use: 12 stream slots of 2.5 KB per board plus ~1.6 KB
+// allocated on first use: 14 stream slots of 2.5 KB per board plus ~1.9 KB
 // of hand-offs per board
 static int alloc_p2(hz_env *e) {
   if (e->p2_s[0]) return 0;
@@ -2090,8 +2118,9 @@ static int alloc_p2(hz_env *e) {
            m(&d.c, nr * 4);
   };
   for (int k = 0; ok && k < 3; k++) ok = md(e->p2_x[k][0]) && md(e->p2_x[k][1]);
-  for (int k = 0; ok && k < 4; k++) ok = md(e->p2_pl[k]) && m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
-  for (int k = 0; ok && k < 2; k++)
+  for (int k = 0; ok && k < kP2Ring; k++)
+    ok = md(e->p2_pl[k]) && m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
+  for (int k = 0; ok && k < kP2Play - 1; k++)
     for (int j = 0; ok && j < 2; j++) {
       P2Mid &mm = e->p2_m[k][j];
       ok = m(&mm.tag, nr * 4) && m(&mm.st, 6 * nr * 8) && m(&mm.q, 4 * nr * 8) && m(&mm.i, 3 * nr * 4);
@@ -2109,9 +2138,8 @@ static int alloc_p2(hz_env *e) {
 
 // one hz_play call of pipeline 2 (k_play2).  Call c uses stream slot
 // (c - s) % kP2Stream for stage s; the D1 -> D2 -> D3 -> D4 hand-offs, P1a ->
-// P1b and playA -> playB -> playC by call parity; D4's script and the rule
-// hashes in rings of four (read by playA, playB, playC one, two and three
-// calls later).  Every slot written by call c is read by call c + 1 or later,
+// P1b and play stage st -> st + 1 by call parity; D4's script and the rule
+// hashes in rings of kP2Ring (read by play stage st st + 1 calls later).  Every slot written by call c is read by call c + 1 or later,
 // so launch order on the stream is the only synchronisation.
 static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32_t *steps_done) {
   if (alloc_p2(e)) return 1;
@@ -2132,8 +2160,7 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
   a.n = e->n;
   a.max_plies = max_plies;
   a.draws = e->seed_ahead;
-  a.cut1 = e->p2_cut1;
-  a.cut2 = e->p2_cut2;
+  for (int k = 0; k < kP2Play - 1; k++) a.cut[k] = e->p2_cut[k];
   a.seed_base = e->seed_base;
   a.nrow = (long)e->nrow;
   a.games_done = games_done;
@@ -2147,7 +2174,7 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
     a.s_tag[s] = e->p2_s_tag[sl(s)];
     a.s_cur[s] = e->p2_s_cur[sl(s)];
   }
-  a.s_idx11 = sl(11);
+  a.s_idx_last = sl(kP2Last);
   a.p1h_w = e->p2_p1h[r];
   a.p1h_r = e->p2_p1h[w];
   a.p2h_w = e->p2_p2h[r];
@@ -2158,27 +2185,24 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
     a.x_w[k] = e->p2_x[k][r];
     a.x_r[k] = e->p2_x[k][w];
   }
-  a.pl_w = e->p2_pl[c % 4];
-  a.pl_a = e->p2_pl[(c + 3) % 4];  // written by call c - 1
-  a.pl_b = e->p2_pl[(c + 2) % 4];  // c - 2
-  a.pl_c = e->p2_pl[(c + 1) % 4];  // c - 3
-  a.m1_w = e->p2_m[0][r];
-  a.m1_r = e->p2_m[0][w];
-  a.m2_w = e->p2_m[1][r];
-  a.m2_r = e->p2_m[1][w];
-  a.h_w = e->p2_h[c % 4];
-  a.ht_w = e->p2_h_tag[c % 4];
-  a.h_a = e->p2_h[(c + 3) % 4];
-  a.ht_a = e->p2_h_tag[(c + 3) % 4];
-  a.h_b = e->p2_h[(c + 2) % 4];
-  a.ht_b = e->p2_h_tag[(c + 2) % 4];
-  a.h_c = e->p2_h[(c + 1) % 4];
-  a.ht_c = e->p2_h_tag[(c + 1) % 4];
+  a.pl_w = e->p2_pl[c % kP2Ring];
+  a.h_w = e->p2_h[c % kP2Ring];
+  a.ht_w = e->p2_h_tag[c % kP2Ring];
+  for (int st = 0; st < kP2Play; st++) {  // written by call c - 1 - st
+    const int k = (c + kP2Ring - 1 - st) % kP2Ring;
+    a.pl_r[st] = e->p2_pl[k];
+    a.h_r[st] = e->p2_h[k];
+    a.ht_r[st] = e->p2_h_tag[k];
+  }
+  for (int st = 0; st < kP2Play - 1; st++) {
+    a.m_w[st] = e->p2_m[st][r];
+    a.m_r[st] = e->p2_m[st][w];
+  }
   const int nblk = grid_for(e->n);
   hipLaunchKernelGGL(k_play2, dim3(4 * nblk), dim3(kStageThreads), kResetLds, e->stream, a, nblk);
   if (int err = launch_err()) return err;
   e->lazy = 1;
-  e->calls2 = (c + 1) % (kP2Stream * 4);  // (a multiple of every ring length)
+  e->calls2 = (c + 1) % (kP2Stream * kP2Ring * 2);  // (a multiple of every ring length)
   e->primed = 0;  // the other pipeline's episode prediction is stale now
   return 0;
 }
@@ -2250,15 +2274,16 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   {  // hz_play's pipeline: 2 by default, HZ_PIPELINE=1 for the first (hz_env_set_pipeline)
     const char *pv = getenv("HZ_PIPELINE");
     e->pipeline = pv && atoi(pv) == 1 ? 1 : 2;
-    // HZ_P2_CUTS="a,b": pipeline 2's play stage boundaries (plies; multiples of 8)
-    e->p2_cut1 = 24;
-    e->p2_cut2 = 48;
+    // HZ_P2_CUTS="a,b,c": pipeline 2's play stage boundaries (plies,
+    // increasing multiples of 8; the turn pairs of the ply loop stay whole)
+    e->p2_cut[0] = 24;
+    e->p2_cut[1] = 40;
+    e->p2_cut[2] = 56;
     const char *cv = getenv("HZ_P2_CUTS");
-    int c1, c2;
-    if (cv && sscanf(cv, "%d,%d", &c1, &c2) == 2 && c1 > 0 && c2 > c1 && c1 % 8 == 0 && c2 % 8 == 0) {
-      e->p2_cut1 = c1;
-      e->p2_cut2 = c2;
-    }
+    int c[3];
+    if (cv && sscanf(cv, "%d,%d,%d", &c[0], &c[1], &c[2]) == 3 && c[0] > 0 && c[1] > c[0] && c[2] > c[1] &&
+        c[0] % 8 == 0 && c[1] % 8 == 0 && c[2] % 8 == 0)
+      for (int k = 0; k < 3; k++) e->p2_cut[k] = c[k];
   }
   if (!ok) {
     hz_env_destroy(e);

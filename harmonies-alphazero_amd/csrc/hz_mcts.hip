@@ -183,6 +183,9 @@ __device__ __forceinline__ void wave_argmax(double &best, int &bi) {
 __device__ __forceinline__ int32_t edge_hint_of(int e0, int ne, bool term) {
   return (int32_t)((uint32_t)e0 << 8 | (term ? (uint32_t)kHintTerm : 0u) | (uint32_t)ne);
 }
+// Fresh: the edges' N and W are read past the CU's L1 (relaxed agent-scope
+// loads), for a walk in the launch whose backup just added to them at L2
+template <bool Fresh = false>
 __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
                                              float cpuct) {
   int32_t *cnt = m.counts + (size_t)b * 4;
@@ -213,16 +216,24 @@ __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, 
     float p0 = 0, p1 = 0;
     // each edge's child and hint are read with its statistics (one memory
     // round trip per level)
+    auto ld_n = [&](size_t e) {
+      return Fresh ? __hip_atomic_load(&m.edge_n[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : m.edge_n[e];
+    };
+    auto ld_w = [&](size_t e) {
+      return Fresh ? __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long *>(&m.edge_w[e]),
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                   : m.edge_w[e];
+    };
     if (lane < ne) {
-      n0 = m.edge_n[eb + e0 + lane];
-      w0 = m.edge_w[eb + e0 + lane];
+      n0 = ld_n(eb + e0 + lane);
+      w0 = ld_w(eb + e0 + lane);
       p0 = m.edge_p[eb + e0 + lane];
       c0 = m.edge_child[eb + e0 + lane];
       h0 = m.edge_hint[eb + e0 + lane];
     }
     if (lane + kWave < ne) {
-      n1 = m.edge_n[eb + e0 + lane + kWave];
-      w1 = m.edge_w[eb + e0 + lane + kWave];
+      n1 = ld_n(eb + e0 + lane + kWave);
+      w1 = ld_w(eb + e0 + lane + kWave);
       p1 = m.edge_p[eb + e0 + lane + kWave];
       c1 = m.edge_child[eb + e0 + lane + kWave];
       h1 = m.edge_hint[eb + e0 + lane + kWave];
@@ -323,23 +334,36 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
 // workgroup 0 writes the count, the eval counter and the slots of the boards
 // that need no network.
 constexpr int kGEWaves = 4, kGERows = 2 * kGEWaves, kGEThreads = kGEWaves * kWave, kGELoads = 16;
+constexpr int kBoardFloats = 38 * 35, kGlobFloats = 42;  // one encoded state (hz_encode.hpp)
 __global__ void __launch_bounds__(kGEThreads) k_gather_encode(hz_mcts m, int32_t *__restrict__ rows,
                                                                int32_t *__restrict__ count,
                                                                float *__restrict__ board, float *__restrict__ glob) {
   __shared__ uint64_t smask[kGEWaves][76];
   __shared__ float sval[kGEWaves][76];
   __shared__ int32_t wsum[kGEWaves];
+  __shared__ int32_t s_gidx[kGERows];  // this workgroup's rows' leaves (gidx_c's entries), for its encoder waves
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int per = (m.n + kGEThreads - 1) / kGEThreads;
   const int b0 = t * per < m.n ? t * per : m.n, b1 = b0 + per < m.n ? b0 + per : m.n;
   const int r0 = (int)blockIdx.x * kGERows;
+  // up to 4096 boards (per <= kGELoads) the thread's leaf flags stay in
+  // registers from the count to the row assignment: one round trip, not two
+  const bool one = per <= kGELoads;
+  int gk[kGELoads];
   int c = 0;
-  for (int base = b0; base < b1; base += kGELoads) {  // one pass up to 4096 boards: all loads in flight
-    int g[kGELoads];
+  if (one) {
 #pragma unroll
-    for (int k = 0; k < kGELoads; k++) g[k] = base + k < b1 ? m.leaf_gidx[base + k] : -1;
+    for (int k = 0; k < kGELoads; k++) gk[k] = b0 + k < b1 ? m.leaf_gidx[b0 + k] : -1;
 #pragma unroll
-    for (int k = 0; k < kGELoads; k++) c += g[k] >= 0;
+    for (int k = 0; k < kGELoads; k++) c += gk[k] >= 0;
+  } else {
+    for (int base = b0; base < b1; base += kGELoads) {  // all of a pass's loads in flight
+      int g[kGELoads];
+#pragma unroll
+      for (int k = 0; k < kGELoads; k++) g[k] = base + k < b1 ? m.leaf_gidx[base + k] : -1;
+#pragma unroll
+      for (int k = 0; k < kGELoads; k++) c += g[k] >= 0;
+    }
   }
   // exclusive prefix of the per-thread counts: wave scan, then the waves' totals
   int incl = c;
@@ -358,19 +382,26 @@ __global__ void __launch_bounds__(kGEThreads) k_gather_encode(hz_mcts m, int32_t
   }
   int r = before + incl - c;  // rank of the thread's first needed board
   const bool first = blockIdx.x == 0;
-  if (first || (r < r0 + kGERows && r + c > r0)) {
-    for (int b = b0; b < b1; b++) {
-      const int g = m.leaf_gidx[b];
-      if (g >= 0) {
-        if (r >= r0 && r < r0 + kGERows) {
-          m.slot[b] = r;
-          m.gidx_c[r] = g;
-          if (rows) rows[r] = b;
-        }
-        r++;
-      } else if (first) {
-        m.slot[b] = -1;
+  auto assign = [&](int b, int g) {
+    if (g >= 0) {
+      if (r >= r0 && r < r0 + kGERows) {
+        m.slot[b] = r;
+        m.gidx_c[r] = g;
+        s_gidx[r - r0] = g;
+        if (rows) rows[r] = b;
       }
+      r++;
+    } else if (first) {
+      m.slot[b] = -1;
+    }
+  };
+  if (first || (r < r0 + kGERows && r + c > r0)) {
+    if (one) {
+#pragma unroll
+      for (int k = 0; k < kGELoads; k++)
+        if (b0 + k < b1) assign(b0 + k, gk[k]);
+    } else {
+      for (int b = b0; b < b1; b++) assign(b, m.leaf_gidx[b]);
     }
   }
   if (first && t == 0) {
@@ -378,8 +409,10 @@ __global__ void __launch_bounds__(kGEThreads) k_gather_encode(hz_mcts m, int32_t
     if (m.eval_ctr) m.eval_ctr[0] += total;  // one thread of one workgroup, stream-ordered
   }
   if (r0 >= total) return;
-  __syncthreads();  // the workgroup's gidx_c entries (global, written above) are visible to all its threads
-  encode_pair<true>(m.node_state, 1, 6, m.gidx_c, total, board, glob, lane, r0 + 2 * w, smask[w], sval[w]);
+  __syncthreads();  // s_gidx complete
+  // the workgroup's rows from 0: its leaves from LDS, its outputs from row r0
+  encode_pair<true>(m.node_state, 1, 6, s_gidx, total - r0, board + (size_t)r0 * kBoardFloats,
+                    glob + (size_t)r0 * kGlobFloats, lane, 2 * w, smask[w], sval[w]);
 }
 
 // --------------------------------- select + gather + encode for small batches
@@ -619,17 +652,13 @@ static_assert(sizeof(uint64_t) * kChildLds * 6 >= sizeof(uint32_t) * kMT, "the s
 
 // expand_leaf (MCTS.py:151-218) + back_fill (:220-266) + the root Dirichlet
 // mix (:308-327).  noise[b*69 + i] is the i-th legal move's Dirichlet sample.
-template <int Waves>  // minimum waves per SIMD the register allocation must allow (3: none forced)
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
-                                                         int32_t *__restrict__ mtcur,
-                                                         const float *__restrict__ policy,
-                                                         const float *__restrict__ value,
-                                                         const double *__restrict__ noise, double eps,
-                                                         float one_minus_eps, int testing,
-                                                         const int32_t *__restrict__ row_of, int prio) {
-  __shared__ ExpandLds L;
-  int b = blockIdx.x;
-  int lane = threadIdx.x;
+// (board b, one wave; the kernel below adds the next simulation's select)
+__device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts &m, uint32_t *__restrict__ mtw,
+                                                    int32_t *__restrict__ mtcur, const float *__restrict__ policy,
+                                                    const float *__restrict__ value,
+                                                    const double *__restrict__ noise, double eps,
+                                                    float one_minus_eps, int testing,
+                                                    const int32_t *__restrict__ row_of, int prio, int b, int lane) {
   HZ_XSTAMP(0)
   HZ_XFLAG(10, 0)
   int leaf = m.leaf[b];
@@ -945,6 +974,33 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
   HZ_XFLAG(11, d)
 }
 
+// Sel: the wave then walks its board's tree for the next simulation
+// (select_board, as k_select would in the next launch): the walk starts
+// while the path it just backed up is hot in L2, and a simulation has one
+// launch fewer.  Same tree, same leaf, same path: the board's wave does in
+// one kernel what two consecutive kernels did.
+template <int Waves, bool Sel>  // Waves: minimum waves per SIMD the register allocation must allow (3: none forced)
+__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
+                                                         int32_t *__restrict__ mtcur,
+                                                         const float *__restrict__ policy,
+                                                         const float *__restrict__ value,
+                                                         const double *__restrict__ noise, double eps,
+                                                         float one_minus_eps, int testing,
+                                                         const int32_t *__restrict__ row_of, int prio,
+                                                         const uint8_t *__restrict__ active, float cpuct) {
+  __shared__ ExpandLds L;
+  expand_backup_board(L, m, mtw, mtcur, policy, value, noise, eps, one_minus_eps, testing, row_of, prio,
+                      (int)blockIdx.x, (int)threadIdx.x);
+  if (Sel) {
+    __builtin_amdgcn_s_setprio(0);
+    // the walk reads N and W past L1: the backup's adds were done at L2 (the
+    // wave's own stores and adds to an address stay in order; an agent-scope
+    // fence here, i.e. an L2 writeback and invalidate per wave, made the
+    // launch 223 us instead of 38)
+    select_board<true>(m, (int)blockIdx.x, (int)threadIdx.x, active, cpuct);
+  }
+}
+
 // ------------------------------------------------------------- root noise
 // The self-play root noise of get_best_action_and_pi (MCTS.py:314-316:
 // np.random.dirichlet([alpha] * L) over the L legal moves) and the tau = 1
@@ -1151,7 +1207,8 @@ int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, 
 }
 
 static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
-                         double eps, int32_t testing, const int32_t *slot) {
+                         double eps, int32_t testing, const int32_t *slot, bool sel = false,
+                         const uint8_t *active = nullptr, float cpuct = 0.f) {
   if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
   float ome = (float)(1.0 - eps);
   // default: registers capped for four waves per SIMD (38 VGPRs spilled;
@@ -1166,12 +1223,17 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
     const char *e = getenv("HZ_EXPAND_PRIO");
     return e && atoi(e) == 0 ? 0 : 1;
   }();
-  if (waves == 4)
-    hipLaunchKernelGGL(k_expand_backup<4>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio);
-  else
-    hipLaunchKernelGGL(k_expand_backup<3>, dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env),
-                       hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio);
+#define HZ_EXPAND_LAUNCH(W, S)                                                                                 \
+  hipLaunchKernelGGL((k_expand_backup<W, S>), dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env), \
+                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio, active, cpuct)
+  if (waves == 4) {
+    if (sel) HZ_EXPAND_LAUNCH(4, true);
+    else HZ_EXPAND_LAUNCH(4, false);
+  } else {
+    if (sel) HZ_EXPAND_LAUNCH(3, true);
+    else HZ_EXPAND_LAUNCH(3, false);
+  }
+#undef HZ_EXPAND_LAUNCH
   return launch_err();
 }
 
@@ -1183,6 +1245,12 @@ int hz_mcts_expand_backup(hz_mcts *m, hz_env *env, const float *policy, const fl
 int hz_mcts_expand_backup_gathered(hz_mcts *m, hz_env *env, const float *policy, const float *value,
                                    const double *noise, double eps, int32_t testing) {
   return m ? expand_backup(m, env, policy, value, noise, eps, testing, m->slot) : -1;
+}
+
+int hz_mcts_expand_backup_select(hz_mcts *m, hz_env *env, const float *policy, const float *value,
+                                 const double *noise, double eps, int32_t testing, const uint8_t *active,
+                                 float cpuct) {
+  return m ? expand_backup(m, env, policy, value, noise, eps, testing, m->slot, true, active, cpuct) : -1;
 }
 
 int hz_root_noise(const int32_t *count, int32_t n, uint64_t seed, uint64_t board_base, uint64_t move, double alpha,

@@ -55,6 +55,7 @@ _SIGS = {
     "hz_mcts_set_dedup_walk": ([_vp, _c.c_int32], _c.c_int),
     "hz_mcts_select_gather": ([_vp, _vp, _c.c_float, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_mcts_expand_backup_gathered": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
+    "hz_mcts_expand_backup_select": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32, _vp, _c.c_float], _c.c_int),
     "hz_mcts_result": ([_vp, _vp], _c.c_int),
     "hz_root_noise": ([_vp, _c.c_int32, _c.c_uint64, _c.c_uint64, _c.c_uint64, _c.c_double, _vp, _vp, _vp],
                       _c.c_int),

@@ -26,6 +26,7 @@ class BatchedEnv:
         if not self._h:
             raise nat.NativeError("hz_env_create failed")
         self.seed_base = seed_base
+        self.epoch = 0  # bumped by every call that can start games (reset, rollout, import_state)
         self._mask = torch.zeros(self.n, 3, dtype=torch.int64, device=self.device)
         self._count = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         self._status = torch.zeros(self.n, dtype=torch.int32, device=self.device)
@@ -57,7 +58,7 @@ class BatchedEnv:
         nat.check(nat.lib().hz_env_set_seed_ahead(self._h, int(draws) if enable else 0), "hz_env_set_seed_ahead")
 
     def set_pipeline(self, pipeline):
-        """hz_play's pipeline: 2 (the default) = every game spread over twelve
+        """hz_play's pipeline: 2 (the default) = every game spread over thirteen
         consecutive calls (k_play2), 1 = chance-ahead (k_rollout); results
         are identical either way (hz_env_set_pipeline)."""
         L = nat.lib()
@@ -69,6 +70,7 @@ class BatchedEnv:
     def reset(self, sel=None, seeds=None):
         """HarmoniesGameState() on every board (or on boards where sel != 0)."""
         self._sync_stream()
+        self.epoch += 1
         if sel is not None:
             sel = sel.to(device=self.device, dtype=torch.uint8).contiguous()
         if seeds is not None:
@@ -159,6 +161,7 @@ class BatchedEnv:
         """Fused rule-driven play of up to max_plies plies per board
         (reset=True: start every board's next game first, in the same launch)."""
         self._sync_stream()
+        self.epoch += 1
         traj = None
         if record:
             traj = (torch.zeros(max_plies, WORDS, self.n, dtype=torch.int64, device=self.device),
@@ -188,6 +191,7 @@ class BatchedEnv:
 
     def import_state(self, state, mt=None, mt_index=None):
         self._sync_stream()
+        self.epoch += 1
         state = state.to(device=self.device, dtype=torch.int64).contiguous()
         if mt is not None:
             mt = mt.to(device=self.device, dtype=torch.int32).contiguous()

@@ -19,6 +19,8 @@ the first count[0] (a device int32) are live and rows[j] is row j's board:
 no host round trip per simulation (BatchedPredictor's HIP kernels take
 count as their live-row bound).
 """
+import os
+
 import torch
 
 from . import _native as nat
@@ -57,6 +59,9 @@ class BatchedMCTS:
         # children of :189-194 are not edges) are added on the device to
         # edges_total (two small launches per search, no host read)
         self.count_edges = False
+        # the next simulation's select inside each expand/backup launch
+        # (search(); HZ_FUSE_SELECT=0 runs them as separate launches)
+        self.fuse_select = os.environ.get("HZ_FUSE_SELECT", "1") != "0"
         self.edges_total = torch.zeros(1, dtype=torch.int64, device=d)
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
         self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
@@ -116,6 +121,20 @@ class BatchedMCTS:
         fn = nat.lib().hz_mcts_expand_backup_gathered if gathered else nat.lib().hz_mcts_expand_backup
         nat.check(fn(self._h, self.env.handle, nat.ptr(policy), nat.ptr(value), nat.ptr(noise), float(eps),
                      int(bool(testing))), "hz_mcts_expand_backup")
+
+    def expand_backup_select(self, policy, value, cpuct, active=None, noise=None, eps=0.25, testing=True):
+        """expand_backup(gathered=True), then the next simulation's select in
+        the same launch (hz_mcts_expand_backup_select)."""
+        if policy.numel() == 0:
+            policy, value = self._nil_pol, self._nil_val
+        policy = policy.to(dtype=torch.float32).contiguous()
+        value = value.reshape(-1).to(dtype=torch.float32).contiguous()
+        if noise is not None:
+            noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
+        nat.check(nat.lib().hz_mcts_expand_backup_select(self._h, self.env.handle, nat.ptr(policy), nat.ptr(value),
+                                                         nat.ptr(noise), float(eps), int(bool(testing)),
+                                                         nat.ptr(active), float(cpuct)),
+                  "hz_mcts_expand_backup_select")
 
     def result(self):
         nat.check(nat.lib().hz_mcts_result(self._h, nat.ptr(self.visits)), "hz_mcts_result")
@@ -210,6 +229,17 @@ class BatchedMCTS:
             for _ in range(total - 1):
                 g.replay()
             return self._finish()
+        if gather and total > 1 and self.n > 32 and self.fuse_select:
+            # the next simulation's select rides in each expand/backup launch
+            board, glob, rows, count = self.select_gather(cpuct, active)
+            for s in range(total):
+                policy, value = self._evaluate(evaluator, device_rows, board, glob, rows, count, max_rows)
+                if s + 1 < total:
+                    self.expand_backup_select(policy, value, cpuct, active, noise, eps, testing)
+                    board, glob, rows, count = self.gather_leaves()
+                else:
+                    self.expand_backup(policy, value, noise, eps, testing, gathered=True)
+            return self._finish()
         for _ in range(total):
             if not gather:
                 self.select(cpuct, active)
@@ -219,18 +249,19 @@ class BatchedMCTS:
                 self.expand_backup(policy, value, noise, eps, testing)
                 continue
             board, glob, rows, count = self.select_gather(cpuct, active)  # (adds count to eval_rows)
-            if device_rows:
-                if max_rows is not None:
-                    board, glob = board[:max_rows], glob[:max_rows]
-                policy, value = evaluator(board, glob, rows, count)
-            else:
-                k = int(count.item())  # one host read per simulation
-                if k:
-                    policy, value = evaluator(board[:k], glob[:k])
-                else:
-                    policy, value = self._nil_pol, self._nil_val
+            policy, value = self._evaluate(evaluator, device_rows, board, glob, rows, count, max_rows)
             self.expand_backup(policy, value, noise, eps, testing, gathered=True)
         return self._finish()
+
+    def _evaluate(self, evaluator, device_rows, board, glob, rows, count, max_rows):
+        if device_rows:
+            if max_rows is not None:
+                board, glob = board[:max_rows], glob[:max_rows]
+            return evaluator(board, glob, rows, count)
+        k = int(count.item())  # one host read per simulation
+        if k:
+            return evaluator(board[:k], glob[:k])
+        return self._nil_pol, self._nil_val
 
     def _finish(self):
         """Root visits of the search just run, after making sure no leaf

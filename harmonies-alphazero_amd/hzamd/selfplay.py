@@ -63,6 +63,14 @@ class SelfPlay:
         self.keep_noise = False
         self.noise_log = []
         self.step_counter = 0
+        # move() holds the host back only after its search is queued: the
+        # previous move's step status and active-board count come back
+        # through a pinned buffer and an event recorded after that step
+        self._n_active = self.n  # an upper bound on the active boards (sizes the network's launches) ...
+        self._n_active_epoch = -1  # ... while the env's epoch (no game started since) is this
+        self._flags = torch.zeros(2, dtype=torch.int64, pin_memory=self.device.type == "cuda")
+        self._flags_ev = None
+        self._bad_dev = None
 
     def move(self, ply, done=None):
         """One ply for every board that is still playing: search, choose,
@@ -76,10 +84,11 @@ class SelfPlay:
         noise, u = self.noise.draw(self.step_counter, count, cfg["dirichlet_alpha"])
         self.step_counter += 1
         # the leaf batch holds at most one row per active board: size the
-        # network's launches by that (late in the games most boards are done)
-        n_active = max(1, int(active.sum()))
+        # network's launches by that (late in the games most boards are done);
+        # an upper bound from an earlier move, so no host read waits here
         v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
-                             eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=n_active)
+                             eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=max(1, self._active_bound()))
+        self.check_steps()  # the previous move's step, done long before this search runs
         explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
         act = choose_actions(v, explore, u)
         if self.keep_noise:
@@ -87,9 +96,31 @@ class SelfPlay:
         act = torch.where(active, act, torch.full_like(act, -1)).to(torch.int16)
         status = env.step(act)
         bad = active & (status != 0)
-        if bool(bad.any()):
-            raise RuntimeError(f"self-play step failed on boards {torch.nonzero(bad).flatten().tolist()[:8]}")
+        # read back by the next move (or check_steps()) after its search is queued
+        flags = torch.stack([bad.sum(dtype=torch.int64), (~env.done()).sum(dtype=torch.int64)])
+        self._flags.copy_(flags, non_blocking=True)
+        self._flags_ev = torch.cuda.Event() if d.type == "cuda" else None
+        if self._flags_ev is not None:
+            self._flags_ev.record()
+        self._bad_dev = bad
+        self._flags_epoch = env.epoch
         return st, v, active
+
+    def _active_bound(self):
+        return self._n_active if self.env.epoch == self._n_active_epoch else self.n
+
+    def check_steps(self):
+        """Raise RuntimeError if the last move's env step failed on a board
+        (waits for that step only); updates the active-board bound."""
+        if self._bad_dev is None:
+            return
+        if self._flags_ev is not None:
+            self._flags_ev.synchronize()
+        nbad, nact = (int(x) for x in self._flags.tolist())
+        bad, self._bad_dev = self._bad_dev, None
+        self._n_active, self._n_active_epoch = nact, self._flags_epoch
+        if nbad:
+            raise RuntimeError(f"self-play step failed on boards {torch.nonzero(bad).flatten().tolist()[:8]}")
 
     def play(self, reset=True):
         """Play one game on every board; returns the device records."""
@@ -103,7 +134,11 @@ class SelfPlay:
         valid = torch.zeros(T, n, dtype=torch.bool, device=d)
         done = env.done()
         ply = 0
-        while ply < T and not bool(done.all()):
+        while ply < T:
+            n_active = int((~done).sum())  # (one host read per ply: the loop stops exactly)
+            if n_active == 0:
+                break
+            self._n_active, self._n_active_epoch = n_active, env.epoch
             st, v, active = self.move(ply, done)
             states[ply] = st
             players[ply] = ((st[5] >> 41) & 1).to(torch.int8)
@@ -111,6 +146,7 @@ class SelfPlay:
             visits[ply] = v
             done = env.done()
             ply += 1
+        self.check_steps()
         final = env.export_state()
         return {"states": states[:ply], "players": players[:ply], "visits": visits[:ply],
                 "valid": valid[:ply], "final": final, "plies": ply}

@@ -140,8 +140,8 @@ int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_s
 int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
 /* hz_play's pipeline: 2 (the default; HZ_PIPELINE=1 in the environment at
  * hz_env_create makes 1 the default) = every board's game spread over
- * twelve consecutive calls, one stage per call (seeding pass 1 in two
- * stages, pass 2 in three, four draw stages, three play stages), all twelve
+ * thirteen consecutive calls, one stage per call (seeding pass 1 in two
+ * stages, pass 2 in three, four draw stages, four play stages), all thirteen
  * running in each launch on different episodes; 1 = the chance-ahead
  * pipeline above.  Same results either way; pipeline 2 applies to calls with
  * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
@@ -212,6 +212,15 @@ int hz_mcts_expand_backup(hz_mcts *mcts, hz_env *env, const float *policy, const
  * hz_mcts_gather_leaves (board b reads row j where rows[j] = b) */
 int hz_mcts_expand_backup_gathered(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
                                    const double *noise, double eps, int32_t testing);
+/* hz_mcts_expand_backup_gathered followed by the next simulation's
+ * hz_mcts_select(active, cpuct), in one launch (each board's wave walks its
+ * tree right after its backup; same leaves and paths as the two calls).
+ * A search then runs select once, and per simulation gather_leaves, the
+ * network and this (the last simulation: hz_mcts_expand_backup_gathered).
+ * Replaces the select of MCTS.py:297-305's next iteration. */
+int hz_mcts_expand_backup_select(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
+                                 const double *noise, double eps, int32_t testing, const uint8_t *active,
+                                 float cpuct);
 /* Self-play root noise (MCTS.py:314-316, np.random.dirichlet([alpha] * L)
  * over the L = count[b] legal moves, in legal-move order) into noise[n][69]
  * (zeros past L) and the tau = 1 move-choice uniform (MCTS.py:411,

@@ -191,25 +191,25 @@ def test_play_seed_ahead_pipeline(Env, ahead, draws):
 
 @pytest.mark.parametrize("draws", [24, 19, 3, 0])
 def test_play_pipeline2(Env, draws):
-    """hz_play's second pipeline (k_play2: seeding pass 1 in two halves, pass
-    2 in two halves, four draw stages, three play stages, one stage per call
-    on eleven episodes at once): fourteen consecutive calls (the first ten
-    fill the stages, from the eleventh every board replays a fully prepared
-    episode), an hz_reset + hz_rollout (re-primes: the hand-off slots then
-    hold stale episodes), then fourteen more calls; every game, ply count and
+    """hz_play's second pipeline (k_play2: seeding pass 1 in two stages, pass
+    2 in three, four draw stages, four play stages, one stage per call on
+    thirteen episodes at once): sixteen consecutive calls (the first twelve
+    fill the stages, from the thirteenth every board replays a fully
+    prepared episode), an hz_reset + hz_rollout (re-primes: the hand-off
+    slots then hold stale episodes), then sixteen more calls; every game, ply count and
     stream bit-exact vs the oracle's episode.  draws < 19 runs games past
     their pile scripts onto the stream slots; 0 prepares no script at all."""
     n, base = 4096, 4242
     env = Env(n, seed_base=base, device=DEV)
     env.set_pipeline(2)
     env.set_seed_ahead(draws > 0, draws)
-    for ep in range(14):
+    for ep in range(16):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
     env.reset()
     _, steps, _ = env.rollout(200)
-    _check_episode(env, base, 14, steps)
-    for ep in range(15, 29):
+    _check_episode(env, base, 16, steps)
+    for ep in range(17, 33):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
 
@@ -222,7 +222,7 @@ def test_play_pipeline2_partial_block_and_switch(Env):
     env = Env(n, seed_base=base, device=DEV)
     env.set_pipeline(2)
     ep = 0
-    for pipe, calls in ((2, 13), (1, 2), (2, 13)):
+    for pipe, calls in ((2, 15), (1, 2), (2, 15)):
         env.set_pipeline(pipe)
         for _ in range(calls):
             _, steps, _ = env.rollout(200, reset=True)
@@ -363,7 +363,7 @@ def test_encoder_odd_counts_and_empty_slots(Env):
                 assert (b[k] == f["boards"][j]).all() and (g[k] == f["globs"][j]).all(), (m, k)
 
 
-@pytest.mark.parametrize("pipeline,calls", [(1, 3), (2, 13)])
+@pytest.mark.parametrize("pipeline,calls", [(1, 3), (2, 15)])
 def test_play_partial_blocks(Env, pipeline, calls):
     """100 boards (a partial 64-board block in every role of the launch):
     consecutive hz_play calls (pipeline 2: until episodes are fully
