@@ -414,6 +414,31 @@ alignas(16) __constant__ int16_t kX6ClassRow[18][16] = {
     {168, 217, 98, 203, 224, 273, 266, 259, 252, 189, 238, 231, 28, 133, 182, 63},  // ML+BL
     {216, 41, 146, 195, 272, 265, 258, 251, 188, 237, 230, 223, 76, 181, 6, 111},  // MR+TR
 };
+// kX6ClassRowBlk: the same classes with round 3's row placement, for the
+// fused residual block: there kX6ClassRow's bank-conflict-free placement
+// measured 1.1 % slower per 4,096-row forward (2.303 vs 2.289 ms, same box,
+// alternating processes, bit-identical; profiles/r04/blk3/fwd_ab.log): the
+// block's LDS energy saved came back as a lower clock elsewhere
+alignas(16) __constant__ int16_t kX6ClassRowBlk[18][16] = {
+    {8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 22, 23, 24, 25, 26, 43},  // MM
+    {44, 45, 46, 47, 50, 51, 52, 53, 54, 57, 58, 59, 60, 61, 78, 79},  // MM
+    {80, 81, 82, 85, 86, 87, 88, 89, 92, 93, 94, 95, 96, 113, 114, 115},  // MM
+    {116, 117, 120, 121, 122, 123, 124, 127, 128, 129, 130, 131, 148, 149, 150, 151},  // MM
+    {1, 2, 3, 4, 5, 36, 37, 38, 39, 40, 71, 72, 73, 74, 75, 106},  // TM
+    {107, 108, 109, 110, 141, 142, 143, 144, 145, 176, 177, 178, 179, 180, 211, 212},  // TM
+    {29, 30, 31, 32, 33, 64, 65, 66, 67, 68, 99, 100, 101, 102, 103, 134},  // BM
+    {7, 14, 21, 42, 49, 56, 77, 84, 91, 112, 119, 126, 147, 154, 161, 182},  // ML
+    {13, 20, 27, 48, 55, 62, 83, 90, 97, 118, 125, 132, 153, 160, 167, 188},  // MR
+    {152, 155, 156, 157, 158, 159, 162, 163, 164, 165, 166, 183, 184, 185, 186, 187},  // MM
+    {190, 191, 192, 193, 194, 197, 198, 199, 200, 201, 218, 219, 220, 221, 222, 225},  // MM
+    {226, 227, 228, 229, 232, 233, 234, 235, 236, 253, 254, 255, 256, 257, 260, 261},  // MM
+    {262, 263, 264, 267, 268, 269, 270, 271, -1, -1, -1, -1, -1, -1, -1, -1},  // MM
+    {213, 214, 215, 246, 247, 248, 249, 250, 0, 35, 70, 105, 140, 175, 210, 245},  // TM
+    {135, 136, 137, 138, 169, 170, 171, 172, 173, 204, 205, 206, 207, 208, 239, 240},  // BM
+    {241, 242, 243, 274, 275, 276, 277, 278, 34, 69, 104, 139, 174, 209, 244, 279},  // BM
+    {189, 196, 217, 224, 231, 252, 259, 266, 28, 63, 98, 133, 168, 203, 238, 273},  // ML
+    {195, 202, 223, 230, 237, 258, 265, 272, 6, 41, 76, 111, 146, 181, 216, 251},  // MR
+};
 // kX6ClassSel: the block taps some of whose rows (the corner cells) read
 // off the board: only those need the zero-region redirect
 constexpr uint32_t kX6ClassSel[3][9] = {
@@ -944,6 +969,11 @@ constexpr int x6_class_blocks(int h, int tap) {
 // the other buffer as the HBM staging does.
 // LDS: two chunk buffers + E (280 rows x 32 fp32) = 162,304 B.
 template <bool Block>
+__device__ __forceinline__ const int16_t (*x6_tab())[16] {
+  if constexpr (Block) return kX6ClassRowBlk;
+  return kX6ClassRow;
+}
+template <bool Block>
 __global__ void __launch_bounds__(256, 1)
     k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                    const float *__restrict__ res, float *__restrict__ out, int32_t batch,
@@ -1060,7 +1090,7 @@ __global__ void __launch_bounds__(256, 1)
   // the first K-step's B fragments, under whose latency the setup runs
   int rtab[kRBT];
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) rtab[rb] = kX6ClassRow[rh * kRBT + rb][lane & 15];
+  for (int rb = 0; rb < kRBT; rb++) rtab[rb] = x6_tab<Block>()[rh * kRBT + rb][lane & 15];
   stage_issue(0);
   bf16x8 b[3][NCB], bn[3][NCB];
   bissue(b, 0);
@@ -1118,7 +1148,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int cb = 0; cb < NCB; cb++) b1v[cb] = bias[64 * chf + 16 * cb + (lane & 15)];
     uint2 rows[kRBT];  // the lane's 4 rows of each row block, all loads in flight at once
 #pragma unroll
-    for (int rb = 0; rb < kRBT; rb++) rows[rb] = *(const uint2 *)&kX6ClassRow[rh * kRBT + rb][4 * kg];
+    for (int rb = 0; rb < kRBT; rb++) rows[rb] = *(const uint2 *)&x6_tab<Block>()[rh * kRBT + rb][4 * kg];
     // chf is wave-uniform: one branch; a padding row (-1) writes to the
     // dummy cell / row 280, so no value takes a branch of its own
     auto put_all = [&](auto chfc) __attribute__((always_inline)) {
@@ -1278,7 +1308,7 @@ __global__ void __launch_bounds__(256, 1)
   const size_t gbase = (size_t)s0 * 35 * 128;
   int erow[kRBT];  // the lane's output row of each block (transposed tiles: lane -> row lane >> 2)
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) erow[rb] = kX6ClassRow[rh * kRBT + rb][lane >> 2];
+  for (int rb = 0; rb < kRBT; rb++) erow[rb] = x6_tab<Block>()[rh * kRBT + rb][lane >> 2];
   auto orow = [&](int rb) -> int {
     const int row = erow[rb];
     return row >= 0 && row < nrow ? row : -1;

@@ -227,6 +227,48 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
     assert bool((v1[~act_b.cpu()] == 0).all())
 
 
+def test_fused_select_equals_separate_launches():
+    """search() runs each simulation's select inside the previous one's
+    expand/backup launch (hz_mcts_expand_backup_select) above 32 boards;
+    with fuse_select off the two are separate launches.  Same roots, noise
+    and streams: identical visit counts, tree sizes, leaf rows per
+    simulation and next CPython word of every board (self-play settings,
+    mid-game positions, 20 % of the boards inactive)."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    from hzamd.selfplay import NoiseSource
+    n, base, sims = 1000, 321, 24
+    g = torch.Generator().manual_seed(3)
+    active = (torch.rand(n, generator=g) > 0.2).to(DEV)
+    out = []
+    for fuse in (True, False):
+        env = BatchedEnv(n, seed_base=base, device=DEV)
+        env.reset()
+        for p in range(20 + (base % 7)):
+            mask, count = env.legal_mask()
+            env.step(env.rule_actions(mask, count))
+        act_b = active & ~env.done()
+        _, count = env.legal_mask()
+        noise, _ = NoiseSource(base, DEV).draw(5, count, 0.4)
+        mcts = BatchedMCTS(env, sims)
+        mcts.fuse_select = fuse
+        rows = []
+
+        class DeviceRows:
+            device_rows = True
+
+            def __call__(self, board, glob, r, count):
+                rows.append(count.clone())
+                return stub_evaluator(board, glob)
+        v = mcts.search(DeviceRows(), 2.0, active=act_b, noise=noise, eps=0.25, testing=False).clone()
+        st, mt, idx = env.export_state(with_mt=True)
+        out.append((v.cpu(), mcts.stats().clone().cpu(), torch.cat(rows).cpu(), mt.cpu(), idx.cpu()))
+        mcts.close()
+        env.close()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
     """BASELINE config 3's search at full size: 4096 boards at assorted game
     positions, 200 simulations, self-play settings (testing=False: the root
