@@ -1172,7 +1172,7 @@ struct P2Args {
   int s_idx_last;             // the last play stage's slot index (materialize: mt_src = 2 + index)
   uint32_t *p1h_w;            // [nrow] P1a -> P1b: pass 1's last value
   const uint32_t *p1h_r;
-  uint32_t *p2h_w;            // [2][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word
+  uint32_t *p2h_w;            // [3][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word, row 2's final word
   const uint32_t *p2h_r;
   uint32_t *p3h_w;            // [2][nrow] P2b -> P2c: the same
   const uint32_t *p3h_r;
@@ -1429,14 +1429,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, i
   const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
 }
+// twist_word(cur, next, far) = far ^ twist_part(cur, next): the part of row
+// r's next-generation word that rows r and r + 1 decide
+__device__ __forceinline__ uint32_t twist_part(uint32_t cur, uint32_t next) {
+  const uint32_t y = (cur & 0x80000000U) | (next & 0x7fffffffU);
+  return (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
+}
+// What a pass-2 step stores: its final word to its row (kP2Final), the same
+// and over the pass-1 word in LDS (kP2Keep, P2c), or the previous row's
+// twist part (kP2Part: rows 2-223, which only the twist reads)
+enum { kP2Final = 0, kP2Keep = 1, kP2Part = 2 };
 // steps [G0, G1) of pass 2 (G1 - G0 a multiple of 8) on the lane's LDS
-// column, pass-1 words read 8 steps ahead (rows below G1), final words to
-// the slot (buffer stores: voffset the lane, soffset the row) and, with
-// KeepLds, over the pass-1 words in LDS as well (in place: the read-ahead is
-// always past the rows written), publishing progress every 8 steps
-template <int G0, int G1, bool KeepLds>
+// column, pass-1 words read 8 steps ahead (rows below G1), stores to the
+// slot (buffer stores: voffset the lane, soffset the row) as Mode says (in
+// LDS in place: the read-ahead is always past the rows written), with
+// kP2Keep publishing progress every 8 steps
+template <int G0, int G1, int Mode>
 __device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev,
                                         int *prog) {
+  constexpr bool KeepLds = Mode == kP2Keep;
   static_assert((G1 - G0) % 8 == 0, "groups of eight");
   uint32_t *l = hz_lds + lane;
   constexpr int S = kLdsStride;
@@ -1449,14 +1460,15 @@ __device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int
 #pragma unroll
     for (int u = 0; u < 8; u++) nx[u] = l[(g + 8 + u < G1 ? g + 8 + u : G1 - 1) * S];
     const uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
-    const int soff = __builtin_amdgcn_readfirstlane(g * row_bytes);
+    const int soff = __builtin_amdgcn_readfirstlane((Mode == kP2Part ? g - 1 : g) * row_bytes);
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       // (cur ^ p) - (g + u) as one v_xad_u32 with the offset in an SGPR
       const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
       uint32_t v;
       asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
-      __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, soff + u * row_bytes, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(Mode == kP2Part ? twist_part(prev, v) : v, rs, lane * 4,
+                                            soff + u * row_bytes, 0);
       if (KeepLds) l[(g + u) * S] = v;
       prev = v;
     }
@@ -1466,31 +1478,35 @@ __device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int
   }
 }
 // the last steps [G, G1) one by one
-template <int G, int G1, bool KeepLds>
+template <int G, int G1, int Mode>
 __device__ __forceinline__ void p2_tail(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev) {
 #pragma unroll
   for (int i = G; i < G1; i++) {
     const uint32_t v = (hz_lds[i * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, 0);
-    if (KeepLds) hz_lds[i * kLdsStride + lane] = v;
+    if (Mode == kP2Part) __builtin_amdgcn_raw_buffer_store_b32(twist_part(prev, v), rs, lane * 4, (i - 1) * row_bytes, 0);
+    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, 0);
+    if (Mode == kP2Keep) hz_lds[i * kLdsStride + lane] = v;
     prev = v;
   }
 }
 
-// P2a (seed blocks, wave 0): episode ep + 9, whose pass 1 completed in the
-// previous call; P2b (wave 1): ep + 8; P2c (wave 2, with wave 3's twist):
-// ep + 7.  Each hands (prev, pass 1's row-1 word) to the next.  (e, ok: the
-// board's episode and whether the stage's input is this episode's, read by
-// every wave of the block before its barrier, so before P2c rewrites its
-// tag.)
+// P2a (seed blocks, wave 0): the seed blocks' P2a episode, whose pass 1
+// completed in the previous call; P2b (wave 1) the next older; P2c (wave 2,
+// with wave 3's twist) the one before.  Each hands (prev, pass 1's row-1
+// word, row 2's final word) to the next.  Rows 2-223 of the slot are read
+// only by the twist, which needs from each row r only its twist part
+// (rows r and r + 1's words): P2a and P2b store that instead of the final
+// word (one step late, when row r + 1 is known), so the twist is one xor
+// per word with the far row.  (e, ok: the board's episode and whether the
+// stage's input is this episode's, read by every wave of the block before
+// its barrier, so before P2c rewrites its tag.)
 template <int K>  // 0 P2a, 1 P2b, 2 P2c
-__device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int e, bool ok, uint32_t *s_row1,
-                                         int *s_done, int *s_prog) {
+__device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int e, bool ok, int *s_prog) {
   const int b = b0 + lane;
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
   if (!__any(ok)) {
-    if (K == 2) p2_publish(s_done, 2);  // (the twist wave's wait ends: nothing to twist)
+    if (K == 2) p2_publish(s_prog, kMT + 1);  // (the twist wave's waits end: nothing to twist)
     return;
   }
   uint32_t *slot = a.s_mt[2 + K];
@@ -1502,7 +1518,7 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
 #ifdef HZ_DIAG
   if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 32 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
 #endif
-  uint32_t prev, first1;
+  uint32_t prev, first1, row2;
   if (K == 0) {
     first1 = hz_lds[1 * kLdsStride + lane];
     prev = first1;
@@ -1510,136 +1526,125 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
     const uint32_t *h = K == 1 ? a.p2h_r : a.p3h_r;
     prev = act ? h[b] : 0u;
     first1 = act ? h[nr + b] : 0u;
+    row2 = act ? h[2 * nr + b] : 0u;
   }
   const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
   const int row_bytes = (int)(nr * 4);
-  constexpr int G0 = K == 0 ? 2 : R0;
-  constexpr int G = G0 + 8 * ((R1 - G0) / 8);
-  p2_span<G0, G, K == 2>(lane, rs, row_bytes, prev, s_prog);
-  p2_tail<G, R1, K == 2>(lane, rs, row_bytes, prev);
+  if (K == 0) {  // step 2: row 2's final word, handed on (row 1's part needs row 1, P2c's last step)
+    row2 = (hz_lds[2 * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 2U;
+    prev = row2;
+    constexpr int G = 3 + 8 * ((kP2aEnd - 3) / 8);
+    p2_span<3, G, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 2 ..
+    p2_tail<G, kP2aEnd, kP2Part>(lane, rs, row_bytes, prev);    // .. 207
+  } else if (K == 1) {
+    static_assert(kAheadTwist + 1 - kP2aEnd == 16, "P2b's part steps: two groups");
+    p2_span<kP2aEnd, kAheadTwist + 1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 208-223
+    __builtin_amdgcn_raw_buffer_store_b32(prev, rs, lane * 4, kAheadTwist * row_bytes, 0);  // row 224's final word
+    static_assert((kP2bEnd - kAheadTwist - 1) % 8 == 0, "P2b's final steps: groups of eight");
+    p2_span<kAheadTwist + 1, kP2bEnd, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+  } else {
+    // rows 0 and 1 of the next generation are P2c's own last words: their
+    // far rows (397, 398: P2b's) loaded now, used after the chain
+    const uint32_t f0 = act ? slot[(size_t)397 * nr + b] : 0u, f1 = act ? slot[(size_t)398 * nr + b] : 0u;
+    constexpr int G = kP2bEnd + 8 * ((kMT - kP2bEnd) / 8);
+    p2_span<kP2bEnd, G, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_tail<G, kMT, kP2Keep>(lane, rs, row_bytes, prev);
+    p2_publish(s_prog, kMT);
+    const uint32_t row1 = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
+    // mt[0] = 0x80000000 after init_by_array; row 1's next row is row 2
+    __builtin_amdgcn_raw_buffer_store_b32(f0 ^ twist_part(0x80000000u, row1), rs, lane * 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(f1 ^ twist_part(row1, row2), rs, lane * 4, row_bytes, 0);
+  }
   if (K < 2) {
     if (ok) {
       uint32_t *h = K == 0 ? a.p2h_w : a.p3h_w;
       h[b] = prev;
       h[nr + b] = first1;
+      h[2 * nr + b] = row2;
       a.s_tag[2 + K][b] = e * 8 + 3 + K;
     }
-  } else {
-    p2_publish(s_prog, kMT);
-    s_row1[lane] = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
-    p2_publish(s_done, 1);
-    if (ok) a.s_tag[4][b] = e * 8 + 5;
+  } else if (ok) {
+    a.s_tag[4][b] = e * 8 + 5;
   }
 }
 
 // The twist (seed blocks, wave 3): rows [0, kAheadTwist) of the next
-// generation into P2c's slot (the stream at cursor kMTAhead): row r from
-// rows r, r + 1 (P2a's and P2b's, written to HBM by the two previous calls;
-// rows 0 and 1 from P2c) and r + 397 (P2b's below row 417, from HBM; P2c's
-// from LDS).  Lane: four boards, rows grp + 4 i, grp = lane / 16, so
-// iteration i covers rows 4 i .. 4 i + 3 and row r + 1 sits 16 lanes on
-// (one shuffle per row: each lane exposes the word its reader needs, grp 0
-// the next iteration's).  The wave loads its HBM rows at once, twists rows
-// 4-223 two iterations (one publish of P2c's) per wait as P2c publishes rows
-// 417+ (s_prog), with the pair's LDS operations issued together, and rows
-// 0-3 once P2c's last step has made row 1 (s_done).  All its loads precede
-// its stores, so no row is overwritten before it was read.  (Measured: the
-// loop runs at about P2c's pace, ~365 cycles per four rows, so the wave
-// ends as long after P2c as its loads take to land; replacing the old words
-// by their far-row-independent parts first, in any layout, cost more than
-// it saved: profiles/r04/p2/.)
+// generation into P2c's slot (the stream at cursor kMTAhead): row r's new
+// word is the far row r + 397 (P2b's below row 417, from HBM; P2c's from
+// LDS) xor row r's twist part, which P2a and P2b left in the slot (rows
+// 2-223).  Lane: four boards, rows grp + 4 i, grp = lane / 16, so iteration
+// i needs P2c's rows up to 4 i + 400 and follows P2c's progress (s_prog),
+// two iterations per publish of P2c's; rows 0 and 1 (from row 1, P2c's last
+// step, and row 2's final word) are P2c's own.  All its loads precede its
+// stores.  (Before the parts, the wave shuffled each row's
+// successor in from the next lane group and ran at ~350 cycles per
+// iteration, ending ~8 k cycles after P2c: profiles/r04/p2/.)
 constexpr int kTwIters = kAheadTwist / 4;
 constexpr int kTwHbm = (kP2bEnd - 397 + 3) / 4;  // iterations whose rows r + 397 are P2b's (HBM)
-__device__ __forceinline__ uint4 shfl4(const uint4 &v, int src) {
-  return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+__device__ __forceinline__ uint4 xor4(const uint4 &a, const uint4 &b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
-__device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool any, uint32_t *s_row1, int *s_done,
-                                         int *s_prog) {
+__device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool any, int *s_prog) {
   if (!any) return;
   const size_t nr = (size_t)a.nrow;
   uint32_t *slot = a.s_mt[4];
-  const int grp = lane >> 4, c4 = (lane & 15) * 4, up = (lane + 16) & 63;
-  const uint32_t *colh = slot + b0 + c4;
+  const int grp = lane >> 4, c4 = (lane & 15) * 4;
+  uint32_t *col = slot + b0 + c4;
+  auto row = [&](int r) { return *reinterpret_cast<const uint4 *>(col + (size_t)r * nr); };
+  auto store = [&](int r, const uint4 &v) { *reinterpret_cast<uint4 *>(col + (size_t)r * nr) = v; };
 #ifdef HZ_DIAG
   const int b = b0 + lane;
   const uint64_t tz = __builtin_amdgcn_s_memtime();
 #endif
-  uint4 o[kTwIters + 1], fh[kTwHbm];
+  uint4 pt[kTwIters], fh[kTwHbm];
 #pragma unroll
-  for (int i = 0; i <= kTwIters; i++) {
+  for (int i = 0; i < kTwIters; i++) {
     const int r = grp + 4 * i;
-    if (r >= 2) o[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
+    pt[i] = r >= 2 ? row(r) : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < kTwHbm; i++) {
     const int r = grp + 4 * i + 397;
-    if (r < kP2bEnd) fh[i] = *reinterpret_cast<const uint4 *>(colh + (size_t)r * nr);
+    fh[i] = r < kP2bEnd ? row(r) : make_uint4(0, 0, 0, 0);
   }
   int have = p2_wait(s_prog, kP2bEnd + 8);
   P2_PHASE(35, tz);
-  auto twist_row = [&](int i, const uint4 &n1) {
+  auto far = [&](int i) -> uint4 {
     const int r = grp + 4 * i;
-    uint4 f;
-    if (i < kTwHbm && r + 397 < kP2bEnd) {
-      f = fh[i < kTwHbm ? i : 0];
-    } else {
-      const uint32_t *d = hz_lds + (r + 397) * kLdsStride + c4;
-      f = make_uint4(d[0], d[1], d[2], d[3]);
-    }
-    uint4 v;
-    v.x = twist_word(o[i].x, n1.x, f.x);
-    v.y = twist_word(o[i].y, n1.y, f.y);
-    v.z = twist_word(o[i].z, n1.z, f.z);
-    v.w = twist_word(o[i].w, n1.w, f.w);
-    *reinterpret_cast<uint4 *>(slot + (size_t)r * nr + b0 + c4) = v;
+    if (i < kTwHbm && r + 397 < kP2bEnd) return fh[i < kTwHbm ? i : 0];
+    const uint32_t *d = hz_lds + (r + 397) * kLdsStride + c4;
+    return make_uint4(d[0], d[1], d[2], d[3]);
   };
-  // row r's next row, from lane + 16 (grp 3: grp 0's next iteration)
-  auto next_row = [&](int i) { return shfl4(grp == 0 ? o[i + 1] : o[i], up); };
 #pragma unroll
-  for (int i = 1; i < kTwIters; i += 2) {
-    const bool two = i + 1 < kTwIters;
-    const int need = 4 * (two ? i + 1 : i) + 3 + 397 + 1;  // rows up to the pair's last r + 397 final
+  for (int i = 0; i < kTwIters; i += 2) {
+    const int need = 4 * (i + 1) + 3 + 397 + 1;  // the pair's far rows final
     if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need);
-    const uint4 n0 = next_row(i);
-    if (two) {
-      const uint4 n1 = next_row(i + 1);
-      twist_row(i, n0);
-      twist_row(i + 1, n1);
-    } else {
-      twist_row(i, n0);
-    }
-    if (i == 1) P2_PHASE(36, tz);
+    const uint4 f0 = far(i), f1 = far(i + 1);
+    if (i > 0 || grp >= 2) store(grp + 4 * i, xor4(f0, pt[i]));
+    store(grp + 4 * (i + 1), xor4(f1, pt[i + 1]));
+    if (i == 0) P2_PHASE(36, tz);
   }
   P2_PHASE(37, tz);
-  p2_wait(s_done, 1);
-  P2_PHASE(38, tz);
-  if (grp == 0) o[0] = make_uint4(0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u);
-  if (grp == 1) o[0] = make_uint4(s_row1[c4], s_row1[c4 + 1], s_row1[c4 + 2], s_row1[c4 + 3]);
-  twist_row(0, next_row(0));
   // (rows 224..623 keep pass 2's words: the current generation's tail)
 }
 
 // seed blocks: waves 0-2 P2a, P2b, P2c; wave 3 the twist of P2c's episode
 __device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
-  __shared__ uint32_t s_row1[kBlock];
-  __shared__ int s_done, s_prog;
+  __shared__ int s_prog;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b0 = blk * kBlock, b = b0 + lane;
   const bool act = b < a.n;
-  if (tid == 0) {
-    s_done = 0;
-    s_prog = 0;
-  }
+  if (tid == 0) s_prog = 0;
   // each stage's episode and decision (and P2c's for the twist wave), read
   // before the barrier, so before any wave rewrites a tag
   const int k = w < 3 ? w : 2;
   const int e = act ? a.ep_in[b] + kP2Last - 2 - k : 0;
   const bool ok = act && a.s_tag[2 + k][b] == e * 8 + 2 + k;
   __syncthreads();
-  if (w == 0) p2_third<0>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
-  else if (w == 1) p2_third<1>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
-  else if (w == 2) p2_third<2>(a, b0, lane, e, ok, s_row1, &s_done, &s_prog);
-  else p2_twist(a, b0, lane, __any(ok), s_row1, &s_done, &s_prog);
+  if (w == 0) p2_third<0>(a, b0, lane, e, ok, &s_prog);
+  else if (w == 1) p2_third<1>(a, b0, lane, e, ok, &s_prog);
+  else if (w == 2) p2_third<2>(a, b0, lane, e, ok, &s_prog);
+  else p2_twist(a, b0, lane, __any(ok), &s_prog);
 }
 
 // a draw stage: draws [d0, d1) of episode e on its stream slot, from an LDS
@@ -2126,7 +2131,7 @@ static int alloc_p2(hz_env *e) {
       ok = m(&mm.tag, nr * 4) && m(&mm.st, 6 * nr * 8) && m(&mm.q, 4 * nr * 8) && m(&mm.i, 3 * nr * 4);
     }
   for (int k = 0; ok && k < 2; k++)
-    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 2 * nr * 4) && m(&e->p2_p3h[k], 2 * nr * 4) &&
+    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 3 * nr * 4) && m(&e->p2_p3h[k], 3 * nr * 4) &&
          m(&e->p2_ep[k], nr * 4);
   if (!ok || p2_clear_tags(e)) {
     free_p2(e);
@@ -2275,14 +2280,15 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
     const char *pv = getenv("HZ_PIPELINE");
     e->pipeline = pv && atoi(pv) == 1 ? 1 : 2;
     // HZ_P2_CUTS="a,b,c": pipeline 2's play stage boundaries (plies,
-    // increasing multiples of 8; the turn pairs of the ply loop stay whole)
+    // increasing multiples of 4: whole turns; a stage that starts at player
+    // 1's turn plays single plies up to the next turn pair)
     e->p2_cut[0] = 24;
     e->p2_cut[1] = 40;
     e->p2_cut[2] = 56;
     const char *cv = getenv("HZ_P2_CUTS");
     int c[3];
     if (cv && sscanf(cv, "%d,%d,%d", &c[0], &c[1], &c[2]) == 3 && c[0] > 0 && c[1] > c[0] && c[2] > c[1] &&
-        c[0] % 8 == 0 && c[1] % 8 == 0 && c[2] % 8 == 0)
+        c[0] % 4 == 0 && c[1] % 4 == 0 && c[2] % 4 == 0)
       for (int k = 0; k < 3; k++) e->p2_cut[k] = c[k];
   }
   if (!ok) {

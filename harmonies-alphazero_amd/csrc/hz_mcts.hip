@@ -333,7 +333,9 @@ __global__ void __launch_bounds__(kGatherThreads) k_gather(hz_mcts m, int32_t *_
 // Rows, slots, gidx_c and the count are exactly k_gather's (board order);
 // workgroup 0 writes the count, the eval counter and the slots of the boards
 // that need no network.
-constexpr int kGEWaves = 4, kGERows = 2 * kGEWaves, kGEThreads = kGEWaves * kWave, kGELoads = 16;
+// 8 waves (16 rows) per workgroup: 14.3 us per sim step at 4096 boards against 16.0 with 4 and 16.4 with 16
+// (profiles/r04/tree/r4p_ge*): fewer workgroups scan the flags, the encoders keep 2048 waves
+constexpr int kGEWaves = 8, kGERows = 2 * kGEWaves, kGEThreads = kGEWaves * kWave, kGELoads = 16;
 constexpr int kBoardFloats = 38 * 35, kGlobFloats = 42;  // one encoded state (hz_encode.hpp)
 __global__ void __launch_bounds__(kGEThreads) k_gather_encode(hz_mcts m, int32_t *__restrict__ rows,
                                                                int32_t *__restrict__ count,
