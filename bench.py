@@ -594,30 +594,49 @@ def selfplay_probe(args, dev, rank, world):
     active0 = ~sp.env.done()
     sp.keep_noise = True
     sp.noise_log.clear()
-    ev.reset()
-    ev.calls, ev.snap_at, ev.snap = 0, sims // 2, None  # the NN guard's leaf batch: mid first timed move
-    # -- leg 1: per move at the full leaf batch
-    recs = []
-    if dd():
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.sp_moves):
-        recs.append(sp.move(args.sp_warmup + k))
-    torch.cuda.synchronize(dev)
-    if dd():
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    nn_ms = ev.ms()
-    rows = int(ev.rows.item())
-    board_moves = int(sum(int(a.sum().item()) for _, _, a in recs))
-    env_steps = int(ev.edges.item()) + board_moves  # expansion children + real moves
+    step0 = sp.step_counter
+
+    # -- leg 1: per move at the full leaf batch.  The same moves run twice
+    # from the same positions (states, streams and noise keys restored:
+    # every result is the same): first as the workload alone, which gives
+    # the move time, then with a HIP event pair around every leaf
+    # evaluation, which gives the network's time; the pairs' markers add
+    # ~10 us per simulation to a move (tools/event_cost.py,
+    # profiles/r04/event_cost.json), which the first pass leaves out
+    def timed_moves(evaluator):
+        sp.evaluator = evaluator
+        recs = []
+        if dd():
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.sp_moves):
+            recs.append(sp.move(args.sp_warmup + k))
+        torch.cuda.synchronize(dev)
+        if dd():
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        sp.check_steps()
+        return recs, dt
+
+    recs, elapsed = timed_moves(ev.pred)
     noise0 = sp.noise_log[0][0].clone()
     sp.keep_noise = False
     sp.noise_log.clear()
+    sp.env.import_state(*roots)
+    sp.step_counter = step0
+    ev.reset()
+    ev.calls, ev.snap_at, ev.snap = 0, sims // 2, None  # the NN guard's leaf batch: mid first timed move
+    recs_i, elapsed_i = timed_moves(ev)
+    sp.evaluator = ev
+    nn_ms = ev.ms()
+    rows = int(ev.rows.item())
+    board_moves = int(sum(int(a.sum().item()) for _, _, a in recs))
+    assert board_moves == int(sum(int(a.sum().item()) for _, _, a in recs_i))
+    env_steps = int(ev.edges.item()) + board_moves  # expansion children + real moves
     sims_done = board_moves * sims
     if dd():
-        elapsed = all_reduce([elapsed], dist.ReduceOp.MAX)[0]
+        elapsed, elapsed_i = all_reduce([elapsed, elapsed_i], dist.ReduceOp.MAX)
         sims_all, rows_all, env_all = (int(x) for x in all_reduce([sims_done, rows, env_steps], dist.ReduceOp.SUM))
     else:
         sims_all, rows_all, env_all = sims_done, rows, env_steps
@@ -642,6 +661,10 @@ def selfplay_probe(args, dev, rank, world):
                "env_steps_per_s_per_move_leg": env_all / elapsed,
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
                "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
+               "ms_per_move_instrumented": elapsed_i / args.sp_moves * 1e3,
+               "per_move_basis": "ms_per_move: the timed moves alone; nn_ms_per_move: the same moves replayed from "
+                                 "the same positions with a HIP event pair around every leaf evaluation "
+                                 "(ms_per_move_instrumented is that pass's move time); tree = the difference",
                "nn_rows_evaluated": rows, "sims": sims_done,
                "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": emu_peak, "unit": "TFLOP/s",
                                "frac": nn_tf / emu_peak if nn_tf else None,
