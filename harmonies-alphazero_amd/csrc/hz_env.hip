@@ -1399,25 +1399,41 @@ __device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
 // cut into thirds rather than made cheaper per step.
 constexpr int kP2aEnd = 209, kP2bEnd = 417;
 constexpr int kTwKeep = 397;  // P2c's final rows from here on stay in LDS (the twist reads rows 397-620)
+// Rows [R0, R1) of the wave's 64 boards staged from the slot into LDS, in
+// two halves: p2_load issues the 16-B loads (four boards of a row per lane,
+// four rows per instruction) into registers, p2_put writes them to LDS.  A
+// pass-2 stage stages its first piece, issues the next piece's loads and
+// runs its chain over the first piece while they land: two thirds of the
+// staging reads leave the launch's opening burst, where every stage's first
+// inputs arrive.
 template <int R0, int R1>
-__device__ __forceinline__ void p2_stage(const uint32_t *__restrict__ slot, size_t nr, int b0, int lane) {
-  constexpr int U = (R1 - R0 + 3) / 4;  // 16-B loads: four boards of a row per lane, four rows per instruction
+struct P2Piece {
+  uint4 v[(R1 - R0 + 3) / 4];
+};
+template <int R0, int R1>
+__device__ __forceinline__ void p2_load(P2Piece<R0, R1> &pc, const uint32_t *__restrict__ slot, size_t nr, int b0,
+                                        int lane) {
+  constexpr int U = (R1 - R0 + 3) / 4;
   const int c4 = (lane & 15) * 4;
-  uint4 v[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int r = R0 + 4 * u + (lane >> 4);
-    if (r < R1) v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+    if (r < R1) pc.v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
   }
+}
+template <int R0, int R1>
+__device__ __forceinline__ void p2_put(const P2Piece<R0, R1> &pc, int lane) {
+  constexpr int U = (R1 - R0 + 3) / 4;
+  const int c4 = (lane & 15) * 4;
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int r = R0 + 4 * u + (lane >> 4);
     if (r < R1) {
       uint32_t *d = hz_lds + r * kLdsStride + c4;
-      d[0] = v[u].x;
-      d[1] = v[u].y;
-      d[2] = v[u].z;
-      d[3] = v[u].w;
+      d[0] = pc.v[u].x;
+      d[1] = pc.v[u].y;
+      d[2] = pc.v[u].z;
+      d[3] = pc.v[u].w;
     }
   }
   // (a wave's LDS operations execute in order: its later reads see these)
@@ -1513,8 +1529,19 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
 #ifdef HZ_DIAG
   const uint64_t tq = __builtin_amdgcn_s_memtime();
 #endif
-  constexpr int R0 = K == 0 ? 1 : K == 1 ? kP2aEnd : kP2bEnd, R1 = K == 0 ? kP2aEnd : K == 1 ? kP2bEnd : kMT;
-  p2_stage<R0, R1>(slot, nr, b0, lane);
+  // the stage's rows in three pieces, P0 staged now; each later piece's
+  // loads issued before the chain runs over the piece before it
+  constexpr int P0 = K == 0 ? 1 : K == 1 ? kP2aEnd : kP2bEnd;
+  constexpr int P1 = K == 0 ? 67 : K == 1 ? 289 : 481;
+  constexpr int P2 = K == 0 ? 139 : K == 1 ? 353 : 553;
+  constexpr int P3 = K == 0 ? kP2aEnd : K == 1 ? kP2bEnd : kMT;
+  {
+    P2Piece<P0, P1> pc;
+    p2_load(pc, slot, nr, b0, lane);
+    p2_put(pc, lane);
+  }
+  P2Piece<P1, P2> pc1;
+  p2_load(pc1, slot, nr, b0, lane);
 #ifdef HZ_DIAG
   if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 32 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
 #endif
@@ -1530,24 +1557,39 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
   }
   const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
   const int row_bytes = (int)(nr * 4);
-  if (K == 0) {  // step 2: row 2's final word, handed on (row 1's part needs row 1, P2c's last step)
+  P2Piece<P2, P3> pc2;
+  if constexpr (K == 0) {  // step 2: row 2's final word, handed on (row 1's part needs row 1, P2c's last step)
     row2 = (hz_lds[2 * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 2U;
     prev = row2;
-    constexpr int G = 3 + 8 * ((kP2aEnd - 3) / 8);
-    p2_span<3, G, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 2 ..
+    p2_span<3, P1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 2 ..
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Part>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    constexpr int G = P2 + 8 * ((kP2aEnd - P2) / 8);
+    p2_span<P2, G, kP2Part>(lane, rs, row_bytes, prev, s_prog);
     p2_tail<G, kP2aEnd, kP2Part>(lane, rs, row_bytes, prev);    // .. 207
-  } else if (K == 1) {
+  } else if constexpr (K == 1) {
     static_assert(kAheadTwist + 1 - kP2aEnd == 16, "P2b's part steps: two groups");
     p2_span<kP2aEnd, kAheadTwist + 1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 208-223
     __builtin_amdgcn_raw_buffer_store_b32(prev, rs, lane * 4, kAheadTwist * row_bytes, 0);  // row 224's final word
-    static_assert((kP2bEnd - kAheadTwist - 1) % 8 == 0, "P2b's final steps: groups of eight");
-    p2_span<kAheadTwist + 1, kP2bEnd, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+    p2_span<kAheadTwist + 1, P1, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    p2_span<P2, kP2bEnd, kP2Final>(lane, rs, row_bytes, prev, s_prog);
   } else {
     // rows 0 and 1 of the next generation are P2c's own last words: their
     // far rows (397, 398: P2b's) loaded now, used after the chain
     const uint32_t f0 = act ? slot[(size_t)397 * nr + b] : 0u, f1 = act ? slot[(size_t)398 * nr + b] : 0u;
-    constexpr int G = kP2bEnd + 8 * ((kMT - kP2bEnd) / 8);
-    p2_span<kP2bEnd, G, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_span<kP2bEnd, P1, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    constexpr int G = P2 + 8 * ((kMT - P2) / 8);
+    p2_span<P2, G, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
     p2_tail<G, kMT, kP2Keep>(lane, rs, row_bytes, prev);
     p2_publish(s_prog, kMT);
     const uint32_t row1 = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
@@ -1596,6 +1638,11 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
   const int b = b0 + lane;
   const uint64_t tz = __builtin_amdgcn_s_memtime();
 #endif
+  // (the wave has ~16 k cycles of slack: its 4 MB of loads wait until P2c is
+  // 64 rows in, out of the launch's opening burst, where every other
+  // stage's inputs arrive)
+  int have = p2_wait(s_prog, kP2bEnd + 64);
+  P2_PHASE(35, tz);
   uint4 pt[kTwIters], fh[kTwHbm];
 #pragma unroll
   for (int i = 0; i < kTwIters; i++) {
@@ -1607,8 +1654,6 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
     const int r = grp + 4 * i + 397;
     fh[i] = r < kP2bEnd ? row(r) : make_uint4(0, 0, 0, 0);
   }
-  int have = p2_wait(s_prog, kP2bEnd + 8);
-  P2_PHASE(35, tz);
   auto far = [&](int i) -> uint4 {
     const int r = grp + 4 * i;
     if (i < kTwHbm && r + 397 < kP2bEnd) return fh[i < kTwHbm ? i : 0];
