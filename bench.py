@@ -485,6 +485,7 @@ def bench_selfplay(args, dev, rank, world):
     if dd():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sp.check_steps()  # the last timed move's env step (move() reports one move late)
     nn_ms = ev.ms()
     rows = int(ev.rows.item())
     env_steps = int(ev.edges.item()) + int(sum(int(m) for m in moves))  # expansion children + real moves
@@ -525,8 +526,8 @@ def bench_selfplay_games(args, sp, ev, dev, rank, world, sims):
     ev.reset()
     orig_move = sp.move
 
-    def move(ply, done=None):  # progress on stderr (a long run must not look hung)
-        out = orig_move(ply, done)
+    def move(ply, done=None, **kw):  # progress on stderr (a long run must not look hung)
+        out = orig_move(ply, done, **kw)
         if ply % 8 == 0:
             print(f"[config3 full game] ply {ply}", file=sys.stderr, flush=True)
         return out
@@ -712,8 +713,8 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
     n = sp.n
     orig_move = sp.move
 
-    def move(ply, done=None):  # progress on stderr: a long run must not look hung
-        out = orig_move(ply, done)
+    def move(ply, done=None, **kw):  # progress on stderr: a long run must not look hung
+        out = orig_move(ply, done, **kw)
         if ply % 16 == 0:
             print(f"[selfplay game] rank {rank} ply {ply}", file=sys.stderr, flush=True)
         return out

@@ -33,6 +33,7 @@ struct hz_mcts {
   int32_t n, max_nodes, max_edges, hcap, max_depth;
   int32_t exact_keys;
   int32_t dedup_walk;    // hz_mcts_set_dedup_walk (tests): every sibling dedup takes the serial walk
+  int32_t gather_mode;   // hz_mcts_set_gather_encode: -1 process default (HZ_GATHER_ENCODE), 0 layered, 1 fused
   hipStream_t stream;
   uint64_t *node_state;  // [n][max_nodes][6]
   uint64_t *node_key;    // [n][max_nodes][8] canonical key (a probe compares it whole: no key rebuilt)
@@ -180,6 +181,9 @@ __device__ __forceinline__ void wave_argmax(double &best, int &bi) {
 #pragma unroll
   for (int o = 16; o < kWave; o <<= 1) argmax_take(__shfl_xor(best, o), __shfl_xor(bi, o), best, bi);
 }
+// edge_hint = first edge << 8 | terminal << 7 | edge count: the first edge
+// must fit in 24 bits, so hz_mcts_create refuses max_nodes >= kMaxNodesHint
+constexpr int32_t kMaxNodesHint = 1 << 24;
 __device__ __forceinline__ int32_t edge_hint_of(int e0, int ne, bool term) {
   return (int32_t)((uint32_t)e0 << 8 | (term ? (uint32_t)kHintTerm : 0u) | (uint32_t)ne);
 }
@@ -998,7 +1002,11 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
     // the walk reads N and W past L1: the backup's adds were done at L2 (the
     // wave's own stores and adds to an address stay in order; an agent-scope
     // fence here, i.e. an L2 writeback and invalidate per wave, made the
-    // launch 223 us instead of 38)
+    // launch 223 us instead of 38).  The workgroup-scope release fence makes
+    // the backup's atomic adds complete (s_waitcnt vmcnt(0) on gfx950, no
+    // cache maintenance) before the walk's loads issue, so the walk does not
+    // rest on same-address requests reaching L2 in issue order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     select_board<true>(m, (int)blockIdx.x, (int)threadIdx.x, active, cpuct);
   }
 }
@@ -1097,6 +1105,7 @@ extern "C" {
 
 hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream) {
   if (n_boards <= 0 || max_nodes < 2 || max_depth < 1) return nullptr;
+  if (max_nodes >= kMaxNodesHint) return nullptr;  // edge ids (max_edges = max_nodes) must fit edge_hint_of
   if (install_comp_table()) return nullptr;  // terminal expansions score boards
   hz_mcts *m = (hz_mcts *)calloc(1, sizeof(hz_mcts));
   if (!m) return nullptr;
@@ -1108,6 +1117,7 @@ hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, 
   m->hcap = h;
   m->max_depth = max_depth;
   m->exact_keys = exact_keys;
+  m->gather_mode = -1;
   m->stream = (hipStream_t)stream;
   size_t n = (size_t)n_boards, N = n * max_nodes, E = n * m->max_edges;
   bool ok = alloc(&m->node_state, N * 6) && alloc(&m->node_key, N * 8) && alloc(&m->node_e0, N) &&
@@ -1153,6 +1163,12 @@ int hz_mcts_set_dedup_walk(hz_mcts *m, int32_t on) {
   return 0;
 }
 
+int hz_mcts_set_gather_encode(hz_mcts *m, int32_t mode) {
+  if (!m || mode < -1 || mode > 1) return -1;
+  m->gather_mode = mode;
+  return 0;
+}
+
 int hz_mcts_set_stream(hz_mcts *m, void *stream) {
   if (!m) return -1;
   m->stream = (hipStream_t)stream;
@@ -1194,10 +1210,11 @@ int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, 
   if (!m || !count || (!board && !glob)) return -1;
   // default: k_gather_encode (one launch); HZ_GATHER_ENCODE=0: k_gather + the
   // encoder launches (same results)
-  static const bool fused = [] {
+  static const bool fused_default = [] {
     const char *e = getenv("HZ_GATHER_ENCODE");
     return !(e && atoi(e) == 0);
   }();
+  const bool fused = m->gather_mode < 0 ? fused_default : m->gather_mode == 1;
   if (fused && board && glob) {
     hipLaunchKernelGGL(k_gather_encode, dim3((m->n + kGERows - 1) / kGERows), dim3(kGEThreads), 0, m->stream, *m,
                        rows, count, board, glob);

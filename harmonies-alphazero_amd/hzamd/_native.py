@@ -53,6 +53,7 @@ _SIGS = {
     "hz_mcts_gather_leaves": ([_vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_mcts_set_eval_counter": ([_vp, _vp], _c.c_int),
     "hz_mcts_set_dedup_walk": ([_vp, _c.c_int32], _c.c_int),
+    "hz_mcts_set_gather_encode": ([_vp, _c.c_int32], _c.c_int),
     "hz_mcts_select_gather": ([_vp, _vp, _c.c_float, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_mcts_expand_backup_gathered": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
     "hz_mcts_expand_backup_select": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32, _vp, _c.c_float], _c.c_int),

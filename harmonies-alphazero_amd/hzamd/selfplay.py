@@ -72,12 +72,23 @@ class SelfPlay:
         self._flags_ev = None
         self._bad_dev = None
 
-    def move(self, ply, done=None):
+    def move(self, ply, done=None, _bound=None):
         """One ply for every board that is still playing: search, choose,
-        step.  Returns (state words before the move, visits, active mask)."""
+        step.  Returns (state words before the move, visits, active mask).
+
+        A step failure of this move is reported by the next move() or by
+        check_steps(): a caller that stops after a move must end with
+        check_steps().  `done` (optional) is the caller's finished-board mask;
+        the network's launches are then sized for every board, since the
+        active-board bound kept from the last step holds only for the env's
+        own done() (play() passes its bound for the mask it computed)."""
         env, n, d, cfg = self.env, self.n, self.device, self.cfg
         testing = bool(cfg.get("testing", False))
-        done = env.done() if done is None else done
+        if done is None:
+            done = env.done()
+            bound = self._active_bound()  # done() only shrinks the active set between resets
+        else:
+            bound = n if _bound is None else int(_bound)
         active = ~done
         st = env.export_state()
         _, count = env.legal_mask()
@@ -87,7 +98,7 @@ class SelfPlay:
         # network's launches by that (late in the games most boards are done);
         # an upper bound from an earlier move, so no host read waits here
         v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
-                             eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=max(1, self._active_bound()))
+                             eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=max(1, bound))
         self.check_steps()  # the previous move's step, done long before this search runs
         explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
         act = choose_actions(v, explore, u)
@@ -139,7 +150,7 @@ class SelfPlay:
             if n_active == 0:
                 break
             self._n_active, self._n_active_epoch = n_active, env.epoch
-            st, v, active = self.move(ply, done)
+            st, v, active = self.move(ply, done, _bound=n_active)
             states[ply] = st
             players[ply] = ((st[5] >> 41) & 1).to(torch.int8)
             valid[ply] = active

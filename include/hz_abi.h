@@ -164,7 +164,9 @@ int hz_import_state(hz_env *env, const uint64_t *state, const uint32_t *mt, cons
  * order (the reference's order is set iteration order).
  * Transpositions are keyed like the reference's hash(state) (exact_keys = 0)
  * or by the exact canonical tuple (exact_keys = 1).  max_nodes bounds nodes
- * and edges per board per search (1 + sims * 69 never overflows). */
+ * and edges per board per search (1 + sims * 69 never overflows); it must be
+ * below 2^24 (edge ids are packed into 24 bits of the walk's hints), else
+ * create returns NULL. */
 typedef struct hz_mcts hz_mcts;
 hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream);
 void hz_mcts_destroy(hz_mcts *mcts);
@@ -200,6 +202,11 @@ int hz_mcts_set_eval_counter(hz_mcts *mcts, int64_t *counter);
  * the table leaves to the walk only on a hash collision), so tests can check
  * both give the same trees.  Off by default. */
 int hz_mcts_set_dedup_walk(hz_mcts *mcts, int32_t on);
+/* Test / A-B switch (no reference counterpart): how hz_mcts_gather_leaves
+ * runs on this handle: 1 = one k_gather_encode launch, 0 = k_gather + the
+ * encoder launches (same rows, slots, count and tensors), -1 = the process
+ * default (HZ_GATHER_ENCODE, fused unless it is 0). */
+int hz_mcts_set_gather_encode(hz_mcts *mcts, int32_t mode);
 /* expand_leaf (MCTS.py:151-218) with policy[n][143] (probabilities, as
  * ModelManager.predict returns them, model.py:81-110), root Dirichlet mix
  * (MCTS.py:308-327) when !testing using noise[n][69] (i-th legal move), then

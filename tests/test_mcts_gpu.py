@@ -355,3 +355,41 @@ def test_fused_select_gather_matches_separate_launches(n):
     assert torch.equal(b1[:k], b2[:k]) and torch.equal(g1[:k], g2[:k])
     mcts.close()
     env.close()
+
+
+def test_gather_encode_equals_layered_gather():
+    """hz_mcts_gather_leaves as one k_gather_encode launch (the default) and
+    as k_gather + the encoder launches (hz_mcts_set_gather_encode(h, 0)):
+    identical rows, count and encoded board/glob tensors, on a partial block
+    (1000 boards, 20 % inactive, grown trees with terminal leaves), and
+    identical visit counts after a whole search with each form (expand reads
+    each board's slot: a wrong slot changes the visits)."""
+    import hzamd._native as nat
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n = 1000
+    g = torch.Generator().manual_seed(11)
+    active = (torch.rand(n, generator=g) > 0.2).to(torch.uint8).to(DEV)
+    out = []
+    for mode in (1, 0):
+        env = BatchedEnv(n, seed_base=77, device=DEV)
+        env.reset()
+        for p in range(30):
+            mask, count = env.legal_mask()
+            env.step(env.rule_actions(mask, count))
+        mcts = BatchedMCTS(env, 24)
+        assert nat.lib().hz_mcts_set_gather_encode(mcts._h, mode) == 0
+        v = mcts.search(stub_evaluator, 2.0, active=active, sims=12).clone()
+        mcts.board.fill_(float("nan"))
+        mcts.glob.fill_(float("nan"))
+        mcts.select(2.0, active)
+        b, gl, r, c = (t.clone() for t in mcts.gather_leaves())
+        k = int(c.item())
+        torch.cuda.synchronize()
+        out.append((v.cpu(), k, r[:k].cpu(), b[:k].cpu(), gl[:k].cpu()))
+        mcts.close()
+        env.close()
+    (v1, k1, r1, b1, g1), (v0, k0, r0, b0, g0) = out
+    assert k1 == k0 and k1 > 0
+    assert torch.equal(v1, v0) and torch.equal(r1, r0)
+    assert torch.equal(b1, b0) and torch.equal(g1, g0)
