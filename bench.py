@@ -79,8 +79,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-off-compare", action="store_true",
                     help="skip the chance-ahead-off comparison run (profiling)")
-    ap.add_argument("--api-mode", action="store_true",
-                    help="also time the unfused per-ply API path (legal_mask/rule/step launches)")
+    ap.add_argument("--no-api-path", action="store_true",
+                    help="config 2: skip the per-ply API path leg (reset / legal+rule+step per ply / score graphs)")
+    ap.add_argument("--no-auto-reset", action="store_true",
+                    help="config 2: skip the steady-state auto-reset leg (hz_rollout auto_reset launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"))
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="1: one game at a time through the drop-in modules (profile_self_play.py); "
@@ -1136,6 +1138,7 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     kern_ms = ev0.elapsed_time(ev1) / K
+    env.check_errors()  # no pipeline wave gave up waiting in any launch so far (else NativeError)
 
     timed_steps, timed_games = int(steps_t.sum(dtype=torch.int64)), int(games_t.sum(dtype=torch.int64))
     longest = int(steps_t.max())
@@ -1181,9 +1184,8 @@ def main():
     if not args.no_off_compare:
         off_steps, off_elapsed = off_compare(env, one_launch, games, args, dev, world)
 
-    api = None
-    if args.api_mode and rank == 0:
-        api = api_mode(env, dev, stream)
+    api = None if args.no_api_path else api_path_leg(args, dev, rank, world)
+    auto = None if args.no_auto_reset else auto_reset_leg(args, dev, rank, world)
     enc = encoder_roofline(dev, n, args.seed_base) if rank == 0 else None
 
     # parity guard on every rank, over its own boards (global ids
@@ -1219,6 +1221,12 @@ def main():
             "metric": "self-play env-steps/sec + games/sec @4096 boards, 1/2/4/8 GPUs; bit-exact vs CPU",
             "value": value,
             "unit": "env-steps/s",
+            "headline_basis": "value = config 2: rule-driven env play (reset, legal mask, step, chance draws, "
+                              "final scoring) on 4096 boards/GPU, NO MCTS and no network; the self-play "
+                              "(config 3: 200-sim MCTS + network per move) figures are selfplay_env_steps_per_s "
+                              "and selfplay_games_per_s",
+            "selfplay_env_steps_per_s": (sp or {}).get("env_steps_per_s"),
+            "selfplay_games_per_s": (sp or {}).get("games_per_s"),
             "env_games_per_s": games_per_s,
             "env_games_basis": "rule-driven env games (config 2, no MCTS) per second; the self-play games/s "
                                "is selfplay.games_per_s",
@@ -1262,8 +1270,8 @@ def main():
             "parity": parity,
             "selfplay": sp,
         }
-        if api:
-            out["api_path"] = api
+        out["api_path"] = api
+        out["auto_reset"] = auto
         print(json.dumps(out))
     if args.no_selfplay:
         env.close()
@@ -1328,16 +1336,45 @@ def off_compare(env, one_launch, games, args, dev, world):
     return total, elapsed
 
 
-def api_mode(env, dev, stream, plies=MAX_PLIES, reps=5):
-    """Unfused path: per ply hz_legal_mask + hz_rule_actions + hz_step
-    (3 launches), then hz_score — captured once into a HIP graph."""
-    n = env.n
+def _oracle_check(env, n, base, ep, plies=None):
+    """Boards whose final state (and ply count) differ from the C oracle's
+    episode-ep game (test infrastructure: parity guard only)."""
+    import oracle
+    from hzamd.state import unpack_ref
+    got = env.export_state().cpu().numpy()
+    total, finals, ref_plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=ep)
+    bad = [b for b in range(n) if not (unpack_ref(got[:, b]) == finals[b]).all()]
+    return bad, total
+
+
+def api_path_leg(args, dev, rank, world, plies=MAX_PLIES, reps=10):
+    """The batched per-ply surface (harmonies_engine.py:145-298, :357-367) as
+    a caller of the reference API drives it: reset, then per ply
+    legal_actions -> the rule pick -> step, then score; one batch = every
+    board's whole game.  Each ply is one launch (hz_rule_ply: the three
+    calls' outputs, bit-identical), the batch one replayed HIP graph
+    (reset + `plies` ply launches + score); the three-launch form is timed
+    beside it.  Each replay's reset starts every board's next episode.  Env
+    steps per batch are the episodes' step counts (the C oracle's, for the
+    same seeds); the first and the last timed episodes' final states are
+    checked against it board by board."""
+    import oracle
+    from hzamd.env import BatchedEnv
+    n = args.boards
+    base = args.seed_base + rank * n
+    env = BatchedEnv(n, seed_base=base, device=dev)
     mask = torch.zeros(n, 3, dtype=torch.int64, device=dev)
     count = torch.zeros(n, dtype=torch.int32, device=dev)
     act = torch.zeros(n, dtype=torch.int16, device=dev)
     status = torch.zeros(n, dtype=torch.int32, device=dev)
 
-    def body():
+    def fused():
+        env.reset()
+        for _ in range(plies):
+            env.rule_ply(mask, count, act, status)
+        env.score()
+
+    def layered():
         env.reset()
         for _ in range(plies):
             env.legal_mask(mask, count)
@@ -1345,24 +1382,133 @@ def api_mode(env, dev, stream, plies=MAX_PLIES, reps=5):
             env.step(act, status)
         env.score()
 
-    body()
-    torch.cuda.synchronize(dev)
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            body()
-    torch.cuda.current_stream(dev).wait_stream(s)
-    g.replay()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    def graph_of(body):
+        body()  # (eager once: episode k)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        return g
+
+    episodes = [0]  # resets so far: the next batch plays episode episodes[0]
+
+    def timed(g):
         g.replay()
+        episodes[0] += 1
+        torch.cuda.synchronize(dev)
+        if dd():
+            dist.barrier()
+        e0 = episodes[0]
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        episodes[0] += reps
+        return dt, e0
+
+    g_l = graph_of(layered)
+    episodes[0] += 1
+    dt_l, _ = timed(g_l)
+    g_f = graph_of(fused)
+    episodes[0] += 1
+    bad_first = None
+    g_f.replay()  # (episode e_first, checked below)
+    e_first = episodes[0]
+    episodes[0] += 1
     torch.cuda.synchronize(dev)
-    dt = (time.perf_counter() - t0) / reps
-    return {"ms_per_batch": dt * 1e3, "launches_per_batch": 3 * plies + 2,
-            "note": "graph-captured per-ply launches over a 4096-board batch", "boards": n}
+    bad_first, _ = _oracle_check(env, n, base, e_first)
+    dt_f, e0 = timed(g_f)
+    e_last = episodes[0] - 1
+    bad_last, _ = _oracle_check(env, n, base, e_last)
+    steps = sum(int(oracle.play_rule_games(n, base, nthreads=8, episode=e)[0]) for e in range(e0, e0 + reps))
+    resets = n * reps
+    env.close()
+    bad = len(bad_first) + len(bad_last)
+    if dd():
+        dt_f, dt_l = all_reduce([dt_f, dt_l], dist.ReduceOp.MAX)
+        steps, resets, bad = (int(x) for x in all_reduce([steps, resets, bad], dist.ReduceOp.SUM))
+    assert bad == 0, f"api path: {bad} boards differ from the C oracle"
+    alg = steps * BYTES_PER_ENV_STEP + resets * BYTES_PER_RESET
+    gbs = alg / dt_f / 1e9
+    return {"env_steps_per_s": steps / dt_f, "games_per_s": resets / dt_f,
+            "ms_per_batch": dt_f / reps * 1e3, "launches_per_batch": plies + 2,
+            "ms_per_batch_three_launches": dt_l / reps * 1e3, "launches_per_batch_three_launches": 3 * plies + 2,
+            "env_steps_per_s_three_launches": steps / dt_l,
+            "boards": n, "plies_per_batch": plies, "batches_timed": reps,
+            "roofline": {"bound": "latency (one launch per ply: a board's ply is one lane's chain)",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "alg_bytes_per_batch": alg / reps / world,
+                         "basis": f"{BYTES_PER_ENV_STEP} B per env step + {BYTES_PER_RESET} B per reset over the "
+                                  "replayed graphs' wall time"},
+            "parity": f"final states of timed episodes {e0} and {e_last} (and {e_first} before timing): "
+                      f"{world * n}/{world * n} boards bit-exact vs C oracle each; env steps = the oracle's "
+                      "step counts of the timed episodes",
+            "note": "one HIP graph per batch: hz_reset, then per ply hz_rule_ply (get_legal_moves -> rule pick -> "
+                    "apply_move in one launch), then hz_score"}
+
+
+def auto_reset_leg(args, dev, rank, world, plies=MAX_PLIES, warmup=4, launches=40):
+    """Config 2 in steady-state auto-reset mode: hz_rollout(plies,
+    auto_reset=1) launch after launch, every board starting its next episode
+    as soon as a game ends (mid-launch), so every launch plays exactly
+    `plies` env steps per board.  Steps and games are counted on the device;
+    after the last launch every board's state and game count are checked
+    against the C oracle's restatement (or_play_rule_auto) of the whole run."""
+    import oracle
+    from hzamd.env import BatchedEnv
+    from hzamd.state import unpack_ref
+    n = args.boards
+    base = args.seed_base + rank * n
+    env = BatchedEnv(n, seed_base=base, device=dev)
+    env.reset()
+    # per-launch counters (hz_rollout writes each launch's games / steps)
+    games = torch.zeros(warmup + launches, n, dtype=torch.int32, device=dev)
+    steps = torch.zeros(warmup + launches, n, dtype=torch.int32, device=dev)
+    for i in range(warmup):
+        env.rollout(plies, auto_reset=True, games_done=games[i], steps_done=steps[i])
+    torch.cuda.synchronize(dev)
+    if dd():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + launches):
+        env.rollout(plies, auto_reset=True, games_done=games[i], steps_done=steps[i])
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    env.check_errors()
+    st = env.export_state().cpu().numpy()
+    g_all = games.sum(0).cpu().numpy()
+    total_games = int(g_all.sum())
+    all_steps = int(steps.sum(dtype=torch.int64))
+    timed_steps = int(steps[warmup:].sum(dtype=torch.int64))
+    timed_games = int(games[warmup:].sum(dtype=torch.int64))
+    ref_steps, finals, ref_games, _ = oracle.play_rule_auto(n, base, (warmup + launches) * plies, ep0=0, nthreads=8)
+    bad = sum(1 for b in range(n) if not ((unpack_ref(st[:, b]) == finals[b]).all() and g_all[b] == ref_games[b]))
+    bad += int(all_steps != ref_steps)
+    env.close()
+    if dd():
+        dt = all_reduce([dt], dist.ReduceOp.MAX)[0]
+        timed_steps, timed_games, bad = (int(x) for x in all_reduce([timed_steps, timed_games, bad],
+                                                                     dist.ReduceOp.SUM))
+    assert bad == 0, f"auto-reset leg: {bad} boards differ from the C oracle"
+    alg = timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET
+    gbs = alg / dt / 1e9
+    return {"env_steps_per_s": timed_steps / dt, "games_per_s": timed_games / dt,
+            "ms_per_launch": dt / launches * 1e3, "launches_timed": launches, "plies_per_launch": plies,
+            "boards": n, "kernel": "k_rollout<true, false>",
+            "roofline": {"bound": "latency (per-lane chains: plies and in-kernel seeding of the next episode)",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "alg_bytes_per_launch": alg / launches / world,
+                         "basis": f"{BYTES_PER_ENV_STEP} B per env step + {BYTES_PER_RESET} B per game started"},
+            "parity": f"after {warmup + launches} launches ({(warmup + launches) * plies} env steps per board, "
+                      f"{total_games} games ended on rank 0): {world * n}/{world * n} boards' states and game counts "
+                      "bit-exact vs the C oracle's auto-reset restatement",
+            "note": "hz_rollout(max_plies, auto_reset=1) continued launch after launch: a board whose game ends "
+                    "seeds and starts its next episode in the same launch"}
 
 
 if __name__ == "__main__":

@@ -82,6 +82,12 @@ struct hz_env {
   uint32_t *p2_h[5];         // [kRulePlies][nrow] rule hashes, a ring of five
   int32_t *p2_h_tag[5];      // [nrow] their episode
   int32_t *p2_ep[2];         // [nrow] episode counter each board ended the call with
+  // a pipeline wave that gives up waiting for its publisher (a bounded spin
+  // on an LDS progress counter) ORs a bit into *wait_err (kWaitErr*), so the
+  // host raises instead of trusting the call's streams (hz_env_set_error_word)
+  int32_t *wait_err_own;     // [1] the handle's own word
+  int32_t *wait_err;         // the word the kernels OR into (caller's or own)
+  int spin_limit;            // s_sleep rounds before a wait gives up (hz_env_set_spin_limit)
 };
 
 #ifdef HZ_DIAG
@@ -309,6 +315,47 @@ __global__ void __launch_bounds__(kBlock) k_rule(const uint64_t *__restrict__ se
   action[b] = L > 0 ? (int16_t)kth_action(m, rule_pick(seed[b], ply[b], L)) : (int16_t)-1;
 }
 
+// ------------------------------------------------ one ply of the surface
+// The per-ply API path in one launch: get_legal_moves -> the benchmark's
+// rule pick -> apply_move (harmonies_engine.py:145-298) for every board,
+// with the three calls' outputs written as hz_legal_mask, hz_rule_actions
+// and hz_step write them (bit-identical: the same device functions in the
+// same order).  One 48 B state load and store per board instead of two loads
+// and a store across three launches.
+__global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
+                                                int32_t *__restrict__ pos, int32_t *__restrict__ ply,
+                                                const uint64_t *__restrict__ seed, int n,
+                                                uint64_t *__restrict__ mask, int32_t *__restrict__ count,
+                                                int16_t *__restrict__ action, int32_t *__restrict__ status) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  State s = load_state(st, n, b);
+  uint64_t m[3];
+  int c = legal_mask(s, m);
+  if (game_done(s.misc)) { m[0] = m[1] = m[2] = 0; c = 0; }
+  if (mask) {
+    mask[(size_t)b * 3 + 0] = m[0];
+    mask[(size_t)b * 3 + 1] = m[1];
+    mask[(size_t)b * 3 + 2] = m[2];
+  }
+  if (count) count[b] = c;
+  const int p = ply[b];
+  const int a = c > 0 ? kth_action(m, rule_pick(seed[b], p, c)) : -1;
+  if (action) action[b] = (int16_t)a;
+  if (a < 0) {
+    if (status) status[b] = ST_NOOP;
+    return;
+  }
+  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
+  int r = step_state(s, a, d);
+  if (r == ST_OK) {
+    store_state(st, n, b, s);
+    pos[b] = d.m.cursor();
+    ply[b] = p + 1;
+  }
+  if (status) status[b] = r;
+}
+
 // ---------------------------------------------------------------- rollout
 // Lane-per-board with the block's 64 MT streams resident in LDS for the
 // whole call ([624][65] words, as in k_reset): every draw reads and twists at
@@ -486,12 +533,22 @@ static_assert(kD1Draws <= kAheadDraws && 9 * kD1Draws <= 192, "draw1's script si
 // one ring slot: the stream word-major (row r of board b at mt[r * nrow + b],
 // nrow = n rounded up to 64, so a wave's row is 256 contiguous bytes), and
 // per board the tag, draw1's script, cursors and draw count
+// wait-error bits (hz_env_set_error_word): a bounded wait gave up
+constexpr int32_t kWaitErrSeedRows = 1;  // k_rollout's seed stage: wave 0's pass-2 row progress
+constexpr int32_t kWaitErrP2Twist = 2;   // k_play2's twist wave: P2c's progress
+constexpr int kSpinLimitDefault = 1 << 22;
+__device__ __forceinline__ void wait_failed(int32_t *err, int32_t bit) {
+  if (err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct Ring {
   uint32_t *mt;
   int32_t *tag;   // [nrow] episode * 4 + stage (1 seeded, 2 draw1 done); -1 none
   uint64_t *pile; // [kAheadWords][nrow]
   int32_t *cur;   // [kD1Draws + 1][nrow] cursor before draw 0 and after each draw
   int32_t *k1;    // [nrow] draws draw1 completed
+  int32_t *err;   // the env's wait-error word (seed stage)
+  int spin;       // spin bound of the seed stage's row wait
 };
 
 // rows [r0, r1) of the block's 64 boards, word-major HBM -> LDS [row][65];
@@ -677,10 +734,14 @@ __device__ __forceinline__ void seed_stage(int blk, Ring rs, size_t nrow, const 
 #pragma unroll 1
     for (int r0 = 2; r0 < kOverlapEnd; r0 += kSeedChunk) {
       // wave 0 publishes every row up to kLastPub; the bound only guards
-      // against a hang should that ever change
-      for (int spin = 0; done < r0 + kSeedChunk && spin < (1 << 22); spin++) {
+      // against a hang should that ever change, and giving up is reported
+      for (int spin = 0; done < r0 + kSeedChunk && spin < rs.spin; spin++) {
         __builtin_amdgcn_s_sleep(1);
         done = __hip_atomic_load(&s_rows, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (done < r0 + kSeedChunk) {
+        done = r0 + kSeedChunk;  // (one report per chunk at most; the rows stored are then untrusted)
+        wait_failed(rs.err, kWaitErrSeedRows);
       }
       int r = r0 + ((tid - 64) >> 4);
       *reinterpret_cast<uint4 *>(out + (size_t)r * nrow) = row4(r);
@@ -1183,6 +1244,8 @@ struct P2Args {
   const uint32_t *h_r[kP2Play];
   int32_t *ht_w;                  // [nrow] their episode
   const int32_t *ht_r[kP2Play];
+  int32_t *err;                   // the env's wait-error word
+  int spin;                       // spin bound of the twist wave's waits
 };
 
 // PlayDraw for the prepared stages: the pile script in registers, then (a
@@ -1303,13 +1366,18 @@ __device__ __forceinline__ int p2_plies(State &s, Draw &draw, int g, int g_end, 
   return g - g0;
 }
 
-__device__ __forceinline__ int p2_wait(int *flag, int need) {
+__device__ __forceinline__ int p2_wait(int *flag, int need, int limit, int32_t *err) {
   int v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
   // every publisher reaches kMT + 1 (or kMT rows); the bound only guards
-  // against a hang should that ever change
-  for (int spin = 0; v < need && spin < (1 << 22); spin++) {
+  // against a hang should that ever change, and giving up is reported (the
+  // caller goes on with rows that may not be final: the host raises)
+  for (int spin = 0; v < need && spin < limit; spin++) {
     __builtin_amdgcn_s_sleep(1);
     v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (v < need) {
+    wait_failed(err, kWaitErrP2Twist);
+    v = kMT + 1;  // no further waits this launch
   }
   return v;
 }
@@ -1641,7 +1709,7 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
   // (the wave has ~16 k cycles of slack: its 4 MB of loads wait until P2c is
   // 64 rows in, out of the launch's opening burst, where every other
   // stage's inputs arrive)
-  int have = p2_wait(s_prog, kP2bEnd + 64);
+  int have = p2_wait(s_prog, kP2bEnd + 64, a.spin, a.err);
   P2_PHASE(35, tz);
   uint4 pt[kTwIters], fh[kTwHbm];
 #pragma unroll
@@ -1663,7 +1731,7 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
 #pragma unroll
   for (int i = 0; i < kTwIters; i += 2) {
     const int need = 4 * (i + 1) + 3 + 397 + 1;  // the pair's far rows final
-    if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need);
+    if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need, a.spin, a.err);
     const uint4 f0 = far(i), f1 = far(i + 1);
     if (i > 0 || grp >= 2) store(grp + 4 * i, xor4(f0, pt[i]));
     store(grp + 4 * (i + 1), xor4(f1, pt[i + 1]));
@@ -2210,6 +2278,8 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
   a.n = e->n;
   a.max_plies = max_plies;
   a.draws = e->seed_ahead;
+  a.err = e->wait_err;
+  a.spin = e->spin_limit;
   for (int k = 0; k < kP2Play - 1; k++) a.cut[k] = e->p2_cut[k];
   a.seed_base = e->seed_base;
   a.nrow = (long)e->nrow;
@@ -2336,6 +2406,10 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
         c[0] % 4 == 0 && c[1] % 4 == 0 && c[2] % 4 == 0)
       for (int k = 0; k < 3; k++) e->p2_cut[k] = c[k];
   }
+  ok = ok && hipMalloc(&e->wait_err_own, sizeof(int32_t)) == hipSuccess &&
+       hipMemset(e->wait_err_own, 0, sizeof(int32_t)) == hipSuccess;
+  e->wait_err = e->wait_err_own;
+  e->spin_limit = kSpinLimitDefault;
   if (!ok) {
     hz_env_destroy(e);
     return nullptr;
@@ -2346,6 +2420,7 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
 void hz_env_destroy(hz_env *e) {
   if (!e) return;
   free_p2(e);
+  if (e->wait_err_own) (void)hipFree(e->wait_err_own);
   for (int k = 0; k < 2; k++) {
     if (e->ahead_mt[k]) (void)hipFree(e->ahead_mt[k]);
     if (e->ahead_tag[k]) (void)hipFree(e->ahead_tag[k]);
@@ -2372,6 +2447,18 @@ void hz_env_destroy(hz_env *e) {
 }
 
 int32_t hz_env_size(const hz_env *e) { return e ? e->n : -1; }
+
+int hz_env_set_error_word(hz_env *e, int32_t *word) {
+  if (!e) return -1;
+  e->wait_err = word ? word : e->wait_err_own;
+  return 0;
+}
+
+int hz_env_set_spin_limit(hz_env *e, int32_t limit) {
+  if (!e || limit < 0) return -1;
+  e->spin_limit = limit ? limit : kSpinLimitDefault;
+  return 0;
+}
 
 int hz_env_set_pipeline(hz_env *e, int32_t pipeline) {
   if (!e || (pipeline != 1 && pipeline != 2)) return -1;
@@ -2429,6 +2516,14 @@ int hz_step(hz_env *e, const int16_t *action, int32_t *status) {
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_step, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
                      e->n, action, status);
+  return launch_err();
+}
+
+int hz_rule_ply(hz_env *e, uint64_t *mask, int32_t *count, int16_t *action, int32_t *status) {
+  if (!e) return -1;
+  if (int err = materialize(e)) return err;
+  hipLaunchKernelGGL(k_ply, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
+                     e->seed, e->n, mask, count, action, status);
   return launch_err();
 }
 
@@ -2491,7 +2586,10 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
   bool pipe = reset_first && e->seed_ahead > 0;
   int r = e->calls & 1, w = r ^ 1;
   int c3 = e->calls % kRing;
-  auto ring = [e](int k) { return Ring{e->ring_mt[k], e->ring_tag[k], e->ring_pile[k], e->ring_cur[k], e->ring_k1[k]}; };
+  auto ring = [e](int k) {
+    return Ring{e->ring_mt[k], e->ring_tag[k], e->ring_pile[k], e->ring_cur[k], e->ring_k1[k], e->wait_err,
+                e->spin_limit};
+  };
   if (pipe) {
     size_t n = (size_t)e->n;
     if (!e->primed) {

@@ -35,11 +35,14 @@ _SIGS = {
     "hz_end_turn": ([_vp, _vp], _c.c_int),
     "hz_encode": ([_vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_rule_actions": ([_vp, _vp, _vp, _vp], _c.c_int),
+    "hz_rule_ply": ([_vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_encode_states": ([_vp, _c.c_int64, _c.c_int64, _vp, _c.c_int32, _vp, _vp, _vp], _c.c_int),
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_play": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_env_set_seed_ahead": ([_vp, _c.c_int32], _c.c_int),
     "hz_env_set_pipeline": ([_vp, _c.c_int32], _c.c_int),
+    "hz_env_set_error_word": ([_vp, _vp], _c.c_int),
+    "hz_env_set_spin_limit": ([_vp, _c.c_int32], _c.c_int),
     "hz_greedy_actions": ([_vp, _vp, _vp], _c.c_int),
     "hz_export_state": ([_vp, _vp, _vp, _vp], _c.c_int),
     "hz_import_state": ([_vp, _vp, _vp, _vp], _c.c_int),

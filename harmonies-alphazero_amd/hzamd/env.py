@@ -31,6 +31,13 @@ class BatchedEnv:
         self._count = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         self._status = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         self._score = torch.zeros(self.n, 2, dtype=torch.int32, device=self.device)
+        # hz_play's wait-error word (hz_env_set_error_word): a pipeline wave
+        # that gave up waiting ORs a bit into it; rollout() looks at the last
+        # call's copy once it has landed, check_errors() waits for it
+        self.wait_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        nat.check(L.hz_env_set_error_word(self._h, nat.ptr(self.wait_err)), "hz_env_set_error_word")
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._err_ev = None
 
     # -- plumbing ----------------------------------------------------------
     def _sync_stream(self):
@@ -145,6 +152,14 @@ class BatchedEnv:
                   "hz_rule_actions")
         return out
 
+    def rule_ply(self, mask=None, count=None, action=None, status=None):
+        """legal_mask -> rule_actions -> step for every board in one launch
+        (hz_rule_ply); the given output tensors get what the three calls
+        would write."""
+        self._sync_stream()
+        nat.check(nat.lib().hz_rule_ply(self._h, nat.ptr(mask), nat.ptr(count), nat.ptr(action), nat.ptr(status)),
+                  "hz_rule_ply")
+
     def greedy_actions(self, sel=None, out=None):
         """choose_move_greedy (evaluation.py:137-196) for every board (or where
         sel != 0): int16 [n], -1 where finished / unselected.  Consumes the
@@ -173,7 +188,38 @@ class BatchedEnv:
         fn = nat.lib().hz_play if reset else nat.lib().hz_rollout
         nat.check(fn(self._h, int(max_plies), int(bool(auto_reset)), nat.ptr(ts), nat.ptr(tm), nat.ptr(ta),
                      nat.ptr(games_done), nat.ptr(steps_done)), "hz_play" if reset else "hz_rollout")
+        self._poll_errors()
         return games_done, steps_done, traj
+
+    def _poll_errors(self):
+        """After a rollout launch: if the previous launch's error-word copy has
+        landed, raise on it; then queue this launch's copy (no host wait)."""
+        ev = self._err_ev
+        if ev is not None and ev.query():
+            self._err_ev = None
+            self._raise_wait_error(int(self._err_host[0]))
+        if self._err_ev is None:
+            self._err_host.copy_(self.wait_err, non_blocking=True)
+            self._err_ev = torch.cuda.Event()
+            self._err_ev.record()
+
+    def _raise_wait_error(self, bits):
+        if bits:
+            self.wait_err.zero_()
+            raise nat.NativeError(
+                f"hz_play: a pipeline wave gave up waiting for its publisher (error bits {bits:#x}: 1 = seed-stage "
+                "rows, 2 = k_play2 twist); the streams of that call are not trustworthy")
+
+    def check_errors(self):
+        """Wait for the work queued so far and raise NativeError if any
+        hz_play / hz_rollout wait gave up since the last check."""
+        self._err_ev = None
+        bits = int(self.wait_err.item())
+        self._raise_wait_error(bits)
+
+    def set_spin_limit(self, limit):
+        """Test knob (hz_env_set_spin_limit): 0 = default bound."""
+        nat.check(nat.lib().hz_env_set_spin_limit(self._h, int(limit)), "hz_env_set_spin_limit")
 
     # -- state transfer -------------------------------------------------------
     def export_state(self, with_mt=False):

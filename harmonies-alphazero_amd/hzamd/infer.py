@@ -319,6 +319,12 @@ def _heads_fc(x, glob, hw, hb, fc, live=None, logits=True, probs=False):
     return lo, pr, v
 
 
+def _nhwc(x):
+    """channels_last (a no-op for MIOpen's NHWC output; PyTorch's own conv,
+    taken with cudnn disabled, returns NCHW)."""
+    return x.contiguous(memory_format=torch.channels_last)
+
+
 def _bias_act(x, b, res=None):
     """x = relu(x + b[c] (+ res)) in place over an NHWC activation."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)):
@@ -442,7 +448,7 @@ class FoldedNet(nn.Module):
         if self.stem_packed is not None:  # reads the NCHW board directly
             x = (_stem_x6_act if self.tower == "x6" else _stem_act)(board, self.stem_packed, b, live)
         else:
-            x = ep(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1), b)
+            x = ep(_nhwc(F.conv2d(board.contiguous(memory_format=torch.channels_last), w, None, padding=1)), b)
         B = board.shape[0]
         xs = None
         if self.resident is not None and B <= min(self.split_max, split_max_batch(board.device)):
@@ -460,8 +466,8 @@ class FoldedNet(nn.Module):
                 x = _conv3x3_act(y, p2, b2, x, live)
         else:
             for (w1, b1), (w2, b2) in self.blocks:
-                y = ep(F.conv2d(x, w1, None, padding=1), b1)
-                x = ep(F.conv2d(y, w2, None, padding=1), b2, x)
+                y = ep(_nhwc(F.conv2d(x, w1, None, padding=1)), b1)
+                x = ep(_nhwc(F.conv2d(y, w2, None, padding=1)), b2, x)
         if self.fc is not None:
             lo, pr, v = _heads_fc(x, glob, *self.heads, self.fc, live=live, logits=not probs, probs=probs)
             return (pr, v) if probs else (lo, v.unsqueeze(1))

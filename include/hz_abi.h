@@ -103,6 +103,14 @@ int hz_encode_states(const uint64_t *states, int64_t word_stride, int64_t item_s
  * ascending action order.  Writes action[b] (-1 if no legal move). */
 int hz_rule_actions(hz_env *env, const uint64_t *mask, const int32_t *count, int16_t *action);
 
+/* One ply of the per-ply surface for every board in ONE launch:
+ * get_legal_moves (harmonies_engine.py:145-208, as hz_legal_mask) -> the
+ * rule pick above (as hz_rule_actions) -> apply_move (:210-298, as hz_step).
+ * Each output pointer may be NULL; those given get exactly what the three
+ * separate calls would write (mask, count, action, status).  The batched
+ * API path's graph replays one of these per ply instead of three launches. */
+int hz_rule_ply(hz_env *env, uint64_t *mask, int32_t *count, int16_t *action, int32_t *status);
+
 /* evaluation.py:137-196 choose_move_greedy for every selected board (sel may
  * be NULL = all): the legal move whose resulting board scores highest for the
  * player to move, first strictly best in ascending action order.  Like the
@@ -147,6 +155,18 @@ int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
  * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
  * pipeline 1).  Returns -1 for a value other than 1 or 2. */
 int hz_env_set_pipeline(hz_env *env, int32_t pipeline);
+/* Both hz_play pipelines hand rows from one wave to another inside a block
+ * through an LDS progress counter; a waiting wave spins at most spin_limit
+ * s_sleep rounds.  A wait that gives up ORs a bit into the env's error word
+ * (1: the chance-ahead seed stage's row wait, 2: k_play2's twist wave) and
+ * the call's streams are then untrusted: the caller must raise.  word is a
+ * device int32 the caller reads (and clears) after a sync; NULL = the
+ * handle's own word.  No reference counterpart (the reference has no
+ * concurrency). */
+int hz_env_set_error_word(hz_env *env, int32_t *word);
+/* Test knob: the spin bound of those waits (0 = the default, 2^22 rounds);
+ * a bound of 1 makes waits give up almost at once. */
+int hz_env_set_spin_limit(hz_env *env, int32_t limit);
 
 /* ---- state transfer (Python facade and tests) --------------------------- */
 /* export: state[6][n] and, optionally, the MT streams in CPython getstate()

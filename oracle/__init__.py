@@ -66,6 +66,9 @@ def lib():
         L.or_play_rule_games_ep.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.or_play_rule_games_ep.restype = ctypes.c_int64
+        L.or_play_rule_auto.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.or_play_rule_auto.restype = ctypes.c_int64
         L.or_mcts_search.argtypes = [ctypes.c_void_p, P(MT), P(MctsCfg), ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.or_mcts_search.restype = ctypes.c_int
@@ -168,6 +171,18 @@ def play_rule_games(n, seed_base, nthreads=0, episode=0):
     total = lib().or_play_rule_games_ep(n, ctypes.c_uint64(seed_base), int(episode), _p(finals), _p(plies),
                                         _p(nxt), nthreads)
     return total, finals, plies, nxt
+
+
+def play_rule_auto(n, seed_base, plies, ep0=0, nthreads=0):
+    """hz_rollout(auto_reset) restated: every board plays `plies` rule-driven
+    env steps from episode ep0's reset, starting its next episode whenever a
+    game ends.  Returns (steps, finals [n, 78], games ended [n], episode [n])."""
+    finals = np.zeros((n, REFSTATE), np.int16)
+    games = np.zeros(n, np.int32)
+    ep = np.zeros(n, np.int32)
+    total = lib().or_play_rule_auto(n, ctypes.c_uint64(seed_base), int(ep0), int(plies), _p(finals), _p(games),
+                                    _p(ep), nthreads)
+    return total, finals, games, ep
 
 
 def mcts_search(st, m, sims, cpuct, eps=0.25, testing=True, tau0=15, ply=0, u=0.0, noise=None,

@@ -622,6 +622,57 @@ int64_t or_play_rule_games_ep(int n, uint64_t seed_base, int episode, int16_t *f
   return total;
 }
 
+/* Steady-state auto-reset play (hz_rollout with auto_reset, the env loop of
+ * a self-play worker that starts a new HarmoniesGameState() whenever a game
+ * ends, trainer.py:434-541 with the rule in place of the search): board b
+ * plays `plies` rule-driven env steps from its episode ep0's reset, starting
+ * episode e + 1 (seed_base + b + ((e + 1) << 32)) whenever episode e ends
+ * with steps left.  finals: the state after the last step; games: the games
+ * that ended within the steps; episode_out: the episode being played (or
+ * just ended) at the end.  Returns the steps taken (n * plies). */
+int64_t or_play_rule_auto(int n, uint64_t seed_base, int ep0, int64_t plies, int16_t *finals, int32_t *games,
+                          int32_t *episode_out, int nthreads) {
+  geom_init();
+  int64_t total = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : total)
+#endif
+  for (int b = 0; b < n; b++) {
+    int64_t left = plies;
+    int e = ep0, done = 0;
+    ostate s;
+    memset(&s, 0, sizeof(s));
+    for (;;) {
+      or_mt m;
+      uint64_t seed = seed_base + (uint64_t)b + ((uint64_t)(uint32_t)e << 32);
+      or_mt_seed(&m, seed);
+      int16_t st[78];
+      or_reset(&m, st);
+      from_ref(st, &s);
+      int ply = 0;
+      uint8_t mask[143];
+      while (left > 0 && !(s.game_over && s.winner != -2)) {
+        int L = legal_of(&s, mask);
+        if (!L) break;
+        uint64_t z = or_rule(seed, (uint64_t)ply);
+        int k = (int)(((z >> 32) * (uint64_t)L) >> 32);
+        step_state(&s, kth_legal(mask, k), &m);
+        ply++;
+        left--;
+        total++;
+      }
+      if (s.game_over && s.winner != -2) done++;
+      if (left <= 0) break;
+      e++;
+    }
+    if (finals) to_ref(&s, finals + (size_t)b * 78);
+    if (games) games[b] = done;
+    if (episode_out) episode_out[b] = e;
+  }
+  return total;
+}
+
 /* -------------------------------------------------------------------- MCTS
  * MCTS.py:8-441.  Node = state + ordered edge list; Edge = (player of the
  * in-node, action, child, N int, W/Q float64, P float32).  Transpositions are

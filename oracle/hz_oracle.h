@@ -54,6 +54,10 @@ int64_t or_play_rule_games(int n, uint64_t seed_base, int16_t *finals, int32_t *
                            uint32_t *next_word, int nthreads);
 int64_t or_play_rule_games_ep(int n, uint64_t seed_base, int episode, int16_t *finals, int32_t *plies,
                               uint32_t *next_word, int nthreads);
+/* Steady-state auto-reset play: `plies` env steps per board from episode
+ * ep0's reset, each ended game followed by the board's next episode. */
+int64_t or_play_rule_auto(int n, uint64_t seed_base, int ep0, int64_t plies, int16_t *finals, int32_t *games,
+                          int32_t *episode_out, int nthreads);
 
 /* MCTS (reference MCTS.py get_best_action_and_pi) with the deterministic stub
  * evaluator of tests/golden/make_golden.py, canonical (ascending action index)

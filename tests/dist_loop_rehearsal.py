@@ -22,6 +22,13 @@ def main(out, folder):
     from test_manager_cpu import MODEL_CFG
     from test_trainer_gpu import EVAL, MCTS, TRAIN
     torch.cuda.set_device(0)
+    if os.environ.get("HZ_DETERMINISTIC", "1") == "1":
+        # training in a fixed summation order (PyTorch's own conv kernels
+        # instead of MIOpen's, whose backward reductions vary run to run), so
+        # two runs of the loop over different backends end with the same
+        # weights and the broadcast can be compared bit for bit
+        torch.backends.cudnn.enabled = False
+        torch.use_deterministic_algorithms(True, warn_only=True)
     backend = os.environ.get("HZ_DIST_BACKEND", "gloo")  # "nccl" (RCCL): one rank only on a one-GPU box
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", 0))

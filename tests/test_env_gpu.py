@@ -212,6 +212,36 @@ def test_play_pipeline2(Env, draws):
     for ep in range(17, 33):
         _, steps, _ = env.rollout(200, reset=True)
         _check_episode(env, base, ep, steps)
+    env.check_errors()  # no wait gave up
+
+
+@pytest.mark.parametrize("pipeline", [2, 1])
+def test_play_wait_give_up_is_loud(pipeline):
+    """The pipelines' bounded waits (k_play2's twist wave following P2c, the
+    chance-ahead seed stage's writers following wave 0) report giving up:
+    with the spin bound forced to one round the waits give up, the env's
+    error word is set and check_errors() raises NativeError; with the
+    default bound (and after the error was taken) nothing is raised."""
+    from hzamd._native import NativeError
+    from hzamd.env import BatchedEnv
+    env = BatchedEnv(512, seed_base=5, device=DEV)
+    env.set_pipeline(pipeline)
+    for _ in range(3):
+        env.rollout(200, reset=True)
+    env.check_errors()
+    env.set_spin_limit(1)
+    with pytest.raises(NativeError, match="gave up waiting"):
+        for _ in range(14):
+            env.rollout(200, reset=True)
+        env.check_errors()
+    env.set_spin_limit(0)
+    torch.cuda.synchronize()
+    env.wait_err.zero_()
+    env.reset()
+    for _ in range(3):
+        env.rollout(200, reset=True)
+    env.check_errors()
+    env.close()
 
 
 def test_play_pipeline2_partial_block_and_switch(Env):
@@ -454,3 +484,36 @@ def test_mt_import_export_roundtrip_cpython(Env):
     s1 = oracle.step(st, 0, m)[1]
     env.step(acts)
     assert (states_of(env)[0] == s1).all()
+
+
+def test_rule_ply_equals_three_calls():
+    """hz_rule_ply (legal mask -> rule pick -> step in one launch) writes, ply
+    by ply, exactly what hz_legal_mask + hz_rule_actions + hz_step write
+    (mask, count, action, status), and leaves the same states and streams;
+    the final states are the C oracle's games (1000 boards: a partial
+    block; the env's second episode, so the reset counter is exercised)."""
+    from hzamd.env import BatchedEnv
+    n, base = 1000, 2024
+    envs = [BatchedEnv(n, seed_base=base, device=DEV) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        e.reset()
+    outs = [[torch.zeros(n, 3, dtype=torch.int64, device=DEV), torch.zeros(n, dtype=torch.int32, device=DEV),
+             torch.zeros(n, dtype=torch.int16, device=DEV), torch.zeros(n, dtype=torch.int32, device=DEV)]
+            for _ in range(2)]
+    for p in range(96):
+        m, c, a, s = outs[0]
+        envs[0].legal_mask(m, c)
+        envs[0].rule_actions(m, c, a)
+        envs[0].step(a, s)
+        envs[1].rule_ply(*outs[1])
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), p
+    st = [e.export_state(with_mt=True) for e in envs]
+    for x, y in zip(*st):
+        assert torch.equal(x, y)
+    _, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=1)
+    assert (states_of(envs[1]) == finals).all()
+    assert bool(envs[1].done().all())
+    for e in envs:
+        e.close()

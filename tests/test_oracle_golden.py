@@ -128,3 +128,34 @@ def test_greedy_games_match_reference():
             assert r == 0
         assert (s == f["finals"][g]).all() and oracle.is_game_over(s)
         assert oracle.mt_next32(m) == f["next_word"][g]
+
+
+def test_play_rule_auto_matches_stepwise_loop():
+    """or_play_rule_auto (the steady-state auto-reset oracle) equals the
+    step-by-step loop over the oracle's primitives (reset, legal, rule, step),
+    and its first game equals or_play_rule_games_ep's."""
+    n, base, plies = 12, 4321, 170
+    total, finals, games, ep = oracle.play_rule_auto(n, base, plies, ep0=2)
+    assert total == n * plies
+    _, first, first_plies, _ = oracle.play_rule_games(n, base, episode=2)
+    for b in range(n):
+        left, e, done = plies, 2, 0
+        while True:
+            seed = base + b + (e << 32)
+            m = oracle.mt_seed(seed)
+            s = oracle.reset(m)
+            ply = 0
+            while left > 0 and not oracle.is_game_over(s):
+                mask = oracle.legal(s)
+                L = int(mask.sum())
+                a = np.flatnonzero(mask)[((oracle.rule(seed, ply) >> 32) * L) >> 32]
+                s = oracle.step(s, int(a), m)[1]
+                ply += 1
+                left -= 1
+            done += int(oracle.is_game_over(s))
+            if e == 2 and oracle.is_game_over(s):
+                assert ply == first_plies[b] and (s == first[b]).all()
+            if left <= 0:
+                break
+            e += 1
+        assert (finals[b] == s).all() and games[b] == done and ep[b] == e, b
