@@ -45,6 +45,8 @@ import torch.distributed as dist  # noqa: E402
 BYTES_PER_ENV_STEP = 152   # 64 B state read + 64 B state write + 18 B mask + ~6 B RNG
 BYTES_PER_RESET = 2564     # 624x4 B MT init + idx + 64 B state
 BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
+TREE_BYTES_POLICY = 576    # f32 [143] policy + value row read per evaluated leaf
+TREE_BYTES_CHILD = 88      # per expansion child: 64 B state + 16 B edge + 8 B hash slot
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 # hz_play launches until every board replays a fully prepared episode, by
@@ -645,6 +647,22 @@ def selfplay_probe(args, dev, rank, world):
         sims_all, rows_all, env_all = sims_done, rows, env_steps
     per_move = elapsed / args.sp_moves
     nn_tf = fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None
+    # the tree kernels' roofline (per simulation, the leaf's
+    # encoded row written and its policy/value row read, and per expansion
+    # child its state, edge and hash slot), over the move time the network
+    # does not take (select, expand, backup, gather + encode, noise, choice)
+    edges = int(ev.edges.item())
+    tree_s = elapsed - nn_ms * 1e-3
+    tree_bytes = rows * (BYTES_PER_ENCODE + TREE_BYTES_POLICY) + edges * TREE_BYTES_CHILD
+    tree_gbs = tree_bytes / tree_s / 1e9 if tree_s > 0 else None
+    tree_roofline = {"bound": "latency (a wave per board walks, expands and backs up one path per simulation)",
+                     "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": tree_gbs / HBM_PEAK_GBS if tree_gbs else None,
+                     "alg_bytes_per_move": tree_bytes / args.sp_moves,
+                     "basis": f"{BYTES_PER_ENCODE} B encoded + {TREE_BYTES_POLICY} B policy/value read per "
+                              f"evaluated leaf ({rows} rows), {TREE_BYTES_CHILD} B per expansion child (state, key "
+                              f"digest, edge, hash slot; {edges} children), over the timed moves' time minus the "
+                              "network's (the path walks' ~16 B per edge level are left out)"}
     # the network's numerics in the measured run: rows of a timed leaf batch
     # against the checkpoint's network in float64 on the CPU
     nn_parity = nn_guard(ev, dev)
@@ -681,6 +699,7 @@ def selfplay_probe(args, dev, rank, world):
                                         f"{emu_peak:.1f} TFLOP/s; fp32_mfma_frac is the same figure against the "
                                         f"f32 MFMA's dense peak ({FP32_MFMA_PEAK_TFLOPS} TFLOP/s), which this path "
                                         "does not use"},
+               "tree_roofline": tree_roofline,
                "dtype": "fp32", "n_gpus": world, "network": ev.network, "parity": guard["parity"],
                "nn_parity": nn_parity}
         if game is not None:

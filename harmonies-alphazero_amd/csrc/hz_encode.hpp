@@ -186,6 +186,76 @@ __device__ __forceinline__ void encode_pair(const uint64_t *__restrict__ st, lon
   }
 }
 
+// One wave encodes one state (the six words at ns[0..5], AoS as a tree node
+// stores them) into its board row (1,330 floats, 8-B aligned: any row of
+// the batch) and its global row (42 floats): lanes 0-37 build the 38 channel
+// masks into the wave's LDS rows (smask / sval: 38 entries each), then the
+// row's 665 float2 are written contiguously.  The same masks, values and
+// element order as encode_pair (so the same bits).  The MCTS kernel that
+// selects a leaf encodes it with this in place of a separate gather launch.
+__device__ __forceinline__ void encode_one(const uint64_t *__restrict__ ns, float *__restrict__ board_row,
+                                           float *__restrict__ glob_row, int lane, uint64_t *smask, float *sval) {
+  if (lane < 38) {
+    const int ch = lane;
+    uint64_t mask;
+    float val;
+    if (ch < 36) {
+      const int p = ch >= 18 ? 1 : 0;
+      const int rem = ch - 18 * p;
+      const int sh = 32 * p;
+      const uint32_t b0 = (uint32_t)(ns[0] >> sh), b1 = (uint32_t)(ns[1] >> sh);
+      const uint32_t b2 = (uint32_t)(ns[2] >> sh), b3 = (uint32_t)(ns[3] >> sh);
+      uint32_t set = (uint32_t)(kCodeSetLo >> (13 * (rem < 4 ? rem : 0))) & 0x1FFFu;
+      set = rem >= 4 && rem < 8 ? (uint32_t)(kCodeSetMid >> (13 * (rem - 4))) & 0x1FFFu : set;
+      set = rem >= 8 && rem < 12 ? (uint32_t)(kCodeSetHi >> (13 * (rem - 8))) & 0x1FFFu : set;
+      set = rem >= 12 && rem < 16 ? (uint32_t)(kCodeSetTop >> (13 * (rem - 12))) & 0x1FFFu : set;
+      set = rem >= 16 ? (uint32_t)(kCodeSetEnd >> (13 * (rem - 16))) & 0x1FFFu : set;
+      const uint32_t n0 = ~b0, n1 = ~b1, n2 = ~b2, n3 = ~b3;
+      uint32_t m23 = 0;
+#pragma unroll
+      for (int code = 1; code < 13; code++) {
+        const uint32_t hit = ((code & 1) ? b0 : n0) & ((code & 2) ? b1 : n1) & ((code & 4) ? b2 : n2) &
+                             ((code & 8) ? b3 : n3);
+        m23 |= ((set >> code) & 1u) ? hit : 0u;
+      }
+      mask = to_grid35(m23);
+      val = 1.f;
+    } else {
+      const uint64_t misc = ns[5];
+      mask = kValid35;
+      if (ch == 36) {
+        val = (float)player_of(misc);
+      } else {
+        const int ph = phase_of(misc);
+        val = ph <= PH_P3 ? (float)((double)ph / 3.0) : 0.f;
+      }
+    }
+    smask[ch] = mask;
+    sval[ch] = val;
+  }
+  float gv = 0.f;
+  if (lane < 42) gv = glob_value(ns, 1, 6, nullptr, 0, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // float2 q = elements 2 q, 2 q + 1: channel c0, position y0 (q advances by
+  // 64: elements by 128 = 3 channels + 23 positions)
+  int c0 = (2 * lane) / 35, y0 = 2 * lane - 35 * c0;
+  for (int q = lane; q < 665; q += 64) {
+    const uint64_t ma = smask[c0], mb = smask[c0 + 1 < 38 ? c0 + 1 : c0];
+    const float va = sval[c0], vb = sval[c0 + 1 < 38 ? c0 + 1 : c0];
+    const float v0 = ((ma >> y0) & 1) ? va : 0.f;
+    const bool nxt = y0 + 1 >= 35;
+    const int p1 = nxt ? 0 : y0 + 1;
+    const float v1 = (((nxt ? mb : ma) >> p1) & 1) ? (nxt ? vb : va) : 0.f;
+    reinterpret_cast<float2 *>(board_row)[q] = make_float2(v0, v1);
+    c0 += 3;
+    y0 += 23;
+    if (y0 >= 35) { y0 -= 35; c0++; }
+  }
+  if (lane < 42) glob_row[lane] = gv;
+}
+
 template <bool Glob>
 __global__ void __launch_bounds__(256) k_encode_board(const uint64_t *__restrict__ st, long word_stride,
                                                       long item_stride, const int32_t *__restrict__ idx, int m,

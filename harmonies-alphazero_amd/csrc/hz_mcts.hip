@@ -189,16 +189,18 @@ __device__ __forceinline__ int32_t edge_hint_of(int e0, int ne, bool term) {
 }
 // Fresh: the edges' N and W are read past the CU's L1 (relaxed agent-scope
 // loads), for a walk in the launch whose backup just added to them at L2
+// Returns the leaf's encoder index (b * max_nodes + leaf, wave-uniform), -1
+// when the board is inactive or its leaf is terminal (no network row)
 template <bool Fresh = false>
-__device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
-                                             float cpuct) {
+__device__ __forceinline__ int select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
+                                            float cpuct) {
   int32_t *cnt = m.counts + (size_t)b * 4;
   if ((active && !active[b]) || cnt[0] == 0) {
     if (lane == 0) {
       m.leaf[b] = -1;
       m.leaf_gidx[b] = -1;
     }
-    return;
+    return -1;
   }
   size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
   int node = 0, d = 0;
@@ -274,12 +276,14 @@ __device__ __forceinline__ void select_board(const hz_mcts &m, int b, int lane, 
     term = (hint & kHintTerm) != 0;
     known = false;
   }
+  if (d == 0) term = game_done(m.node_state[(nb + node) * 6 + 5]);
+  const int gidx = term ? -1 : (int)(nb + node);
   if (lane == 0) {
     m.leaf[b] = node;
     m.depth[b] = d;
-    if (d == 0) term = game_done(m.node_state[(nb + node) * 6 + 5]);
-    m.leaf_gidx[b] = term ? -1 : (int)(nb + node);
+    m.leaf_gidx[b] = gidx;
   }
+  return gidx;
 }
 
 __global__ void __launch_bounds__(kWave) k_select(hz_mcts m, const uint8_t *__restrict__ active, float cpuct) {
@@ -719,7 +723,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
             if (i < kMT) L.mt[i] = v[k];
           }
         }
-        __syncthreads();
+        wave_lds_sync();
         HZ_XSTAMP(8)
         int bag = 0;
 #pragma unroll
@@ -736,10 +740,10 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
           }
           mtcur[b] = draw.m.cursor();
         }
-        __syncthreads();
+        wave_lds_sync();
         HZ_XSTAMP(9)
         for (int i = lane; i < kMT; i += kWave) g[i] = L.mt[i];  // stores: no round trip to wait for
-        __syncthreads();  // the stream copy is read before the children's states overwrite it
+        wave_lds_sync();  // the stream copy is read before the children's states overwrite it
       }
       HZ_XSTAMP(2)
       // the children's priors are loaded here, their latency hidden under
@@ -767,7 +771,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
           L.flag[c] = 0;
         }
       }
-      __syncthreads();
+      wave_lds_sync();
       HZ_XSTAMP(3)
       // the board's counters (written by this wave alone, at the end); loaded
       // after the children's rule work, whose registers they would have held
@@ -805,7 +809,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
           }
         }
       }
-      __syncthreads();
+      wave_lds_sync();
       HZ_XSTAMP(4)
       // ... and among the remaining children the first of equal keys creates
       // the node, later siblings reuse it (flag 3: child[c] = that sibling;
@@ -836,7 +840,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
         };
         const int s0 = new0 ? enter(h0, c0) : 0;
         const int s1 = new1 ? enter(h1, c1) : 0;
-        __syncthreads();
+        wave_lds_sync();
         auto same_key = [&](int f, int c) {
           bool eq = L.hash[f] == L.hash[c];
 #pragma unroll
@@ -879,7 +883,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
             if (open1 && dup1 < 0 && c2 < c1 && h1 == hc2 && same_key(c2, c1)) dup1 = c2;
           }
         }
-        __syncthreads();  // every lane has read the flags before any is rewritten
+        wave_lds_sync();  // every lane has read the flags before any is rewritten
         if (dup0 >= 0) {
           L.flag[c0] = 3;
           L.child[c0] = dup0;
@@ -889,7 +893,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
           L.child[c1] = dup1;
         }
       }
-      __syncthreads();
+      wave_lds_sync();
       // new nodes get consecutive ids in child order; edges keep child order
       int n_new = 0, n_edges = 0;
       for (int r = 0; r < 2; r++) {
@@ -903,7 +907,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
         n_new += __popcll(bn);
         n_edges += __popcll(be);
       }
-      __syncthreads();
+      wave_lds_sync();
       HZ_XSTAMP(5)
       if (base_n + n_new > m.max_nodes || base_e + n_edges > m.max_edges) {
         if (lane == 0) cnt[3] = 1;  // capacity exhausted: leave the leaf unexpanded
@@ -985,18 +989,45 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
 // while the path it just backed up is hot in L2, and a simulation has one
 // launch fewer.  Same tree, same leaf, same path: the board's wave does in
 // one kernel what two consecutive kernels did.
-template <int Waves, bool Sel>  // Waves: minimum waves per SIMD the register allocation must allow (3: none forced)
-__global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
+// Gather (with Sel): the wave then also takes its leaf's row of the next
+// leaf batch, if the leaf needs the network: the row is the next value of
+// count_out (one atomic add per such board: rows in arrival order, not board
+// order; every network row is computed independently of its batch, so the
+// results are the same bits), and the wave encodes its leaf into that row of
+// board/glob itself (encode_one).  This replaces the separate gather +
+// encode launch (k_gather_encode: every workgroup scanning every board's
+// leaf flag) by work spread over the waves that found the leaves.
+// count_out must be zero at launch; count_prev (the count of the batch this
+// launch consumed) is zeroed here for the launch after next, and added to
+// the eval counter first when add_prev (a count no gather kernel added).
+// BPW boards per workgroup (one wave each, each with its own LDS record; the
+// expansion synchronises its own wave only): with Gather, the workgroup's
+// boards take their rows with one atomic add (16 boards: 256 adds per
+// simulation at 4096 boards instead of 4096 to one address, which cost ~20
+// us of same-address serialisation at L2).
+template <int Waves, bool Sel, bool Gather = false, int BPW = 1>  // Waves: minimum waves per SIMD the register allocation must allow (3: none forced)
+__global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
                                                          int32_t *__restrict__ mtcur,
                                                          const float *__restrict__ policy,
                                                          const float *__restrict__ value,
                                                          const double *__restrict__ noise, double eps,
                                                          float one_minus_eps, int testing,
                                                          const int32_t *__restrict__ row_of, int prio,
-                                                         const uint8_t *__restrict__ active, float cpuct) {
-  __shared__ ExpandLds L;
-  expand_backup_board(L, m, mtw, mtcur, policy, value, noise, eps, one_minus_eps, testing, row_of, prio,
-                      (int)blockIdx.x, (int)threadIdx.x);
+                                                         const uint8_t *__restrict__ active, float cpuct,
+                                                         float *__restrict__ board, float *__restrict__ glob,
+                                                         int32_t *__restrict__ rows, int32_t *__restrict__ count_out,
+                                                         int32_t *__restrict__ count_prev, int add_prev) {
+  __shared__ ExpandLds Ls[BPW];
+  __shared__ int32_t s_need[BPW > 1 ? BPW : 1];
+  __shared__ int32_t s_base;
+  // (wave-uniform: the record's base is a scalar)
+  const int w = BPW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int lane = (int)threadIdx.x & (kWave - 1);
+  ExpandLds &L = Ls[w];
+  const int b = (int)blockIdx.x * BPW + w;
+  const bool live = BPW == 1 || b < m.n;
+  if (live)
+    expand_backup_board(L, m, mtw, mtcur, policy, value, noise, eps, one_minus_eps, testing, row_of, prio, b, lane);
   if (Sel) {
     __builtin_amdgcn_s_setprio(0);
     // the walk reads N and W past L1: the backup's adds were done at L2 (the
@@ -1007,7 +1038,48 @@ __global__ void __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(Wave
     // cache maintenance) before the walk's loads issue, so the walk does not
     // rest on same-address requests reaching L2 in issue order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    select_board<true>(m, (int)blockIdx.x, (int)threadIdx.x, active, cpuct);
+    const int g = live ? select_board<true>(m, b, lane, active, cpuct) : -1;
+    if constexpr (Gather) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (add_prev && m.eval_ctr) m.eval_ctr[0] += *count_prev;  // final: its batch was evaluated
+        *count_prev = 0;
+      }
+      int slot = -1;
+      if constexpr (BPW > 1) {
+        if (lane == 0) s_need[w] = g >= 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          int tot = 0;
+#pragma unroll
+          for (int k = 0; k < BPW; k++) tot += s_need[k];
+          s_base = tot ? atomicAdd(count_out, tot) : 0;
+        }
+        __syncthreads();
+        if (g >= 0) {
+          slot = s_base;
+          for (int k = 0; k < w; k++) slot += s_need[k];
+        }
+      } else if (g >= 0) {
+        if (lane == 0) slot = atomicAdd(count_out, 1);
+        slot = __builtin_amdgcn_readfirstlane(slot);
+      }
+      if (slot >= m.n) slot = -1;  // (count_out was not zero: never with the host's protocol)
+      if (live && lane == 0) {
+        m.slot[b] = slot;
+        if (slot >= 0) {
+          m.gidx_c[slot] = g;
+          if (rows) rows[slot] = b;
+        }
+      }
+      if (slot >= 0) {
+        // the leaf's words are in L2 (the walk just read its edges; the node
+        // state was written by an earlier expansion)
+        uint64_t *smask = &L.key[0][0];
+        float *sval = reinterpret_cast<float *>(&L.key[40][0]);
+        encode_one(m.node_state + (size_t)g * 6, board + (size_t)slot * kBoardFloats,
+                   glob + (size_t)slot * kGlobFloats, lane, smask, sval);
+      }
+    }
   }
 }
 
@@ -1225,9 +1297,15 @@ int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, 
   return launch_err();
 }
 
+// boards per workgroup of the gathering expand launch (one atomic add per workgroup)
+constexpr int kGatherBPW = 16;
+static_assert(kGatherBPW * sizeof(ExpandLds) <= 160 * 1024, "the workgroup's records fit the LDS");
+
 static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
                          double eps, int32_t testing, const int32_t *slot, bool sel = false,
-                         const uint8_t *active = nullptr, float cpuct = 0.f) {
+                         const uint8_t *active = nullptr, float cpuct = 0.f, float *board = nullptr,
+                         float *glob = nullptr, int32_t *rows = nullptr, int32_t *count_out = nullptr,
+                         int32_t *count_prev = nullptr, int add_prev = 0) {
   if (!m || !env || !policy || !value || hz_env_size(env) != m->n) return -1;
   float ome = (float)(1.0 - eps);
   // default: registers capped for four waves per SIMD (38 VGPRs spilled;
@@ -1242,15 +1320,20 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
     const char *e = getenv("HZ_EXPAND_PRIO");
     return e && atoi(e) == 0 ? 0 : 1;
   }();
-#define HZ_EXPAND_LAUNCH(W, S)                                                                                 \
-  hipLaunchKernelGGL((k_expand_backup<W, S>), dim3(m->n), dim3(kWave), 0, m->stream, *m, hz_env_mt_ptr(env), \
-                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio, active, cpuct)
+#define HZ_EXPAND_LAUNCH(W, S, G, BP)                                                                           \
+  hipLaunchKernelGGL((k_expand_backup<W, S, G, BP>), dim3((m->n + (BP) - 1) / (BP)), dim3(kWave * (BP)),        \
+                     0, m->stream, *m, hz_env_mt_ptr(env),                                                        \
+                     hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio, active, cpuct,     \
+                     board, glob, rows, count_out, count_prev, add_prev)
+  const bool gat = sel && count_out;
   if (waves == 4) {
-    if (sel) HZ_EXPAND_LAUNCH(4, true);
-    else HZ_EXPAND_LAUNCH(4, false);
+    if (gat) HZ_EXPAND_LAUNCH(4, true, true, kGatherBPW);
+    else if (sel) HZ_EXPAND_LAUNCH(4, true, false, 1);
+    else HZ_EXPAND_LAUNCH(4, false, false, 1);
   } else {
-    if (sel) HZ_EXPAND_LAUNCH(3, true);
-    else HZ_EXPAND_LAUNCH(3, false);
+    if (gat) HZ_EXPAND_LAUNCH(3, true, true, kGatherBPW);
+    else if (sel) HZ_EXPAND_LAUNCH(3, true, false, 1);
+    else HZ_EXPAND_LAUNCH(3, false, false, 1);
   }
 #undef HZ_EXPAND_LAUNCH
   return launch_err();
@@ -1270,6 +1353,15 @@ int hz_mcts_expand_backup_select(hz_mcts *m, hz_env *env, const float *policy, c
                                  const double *noise, double eps, int32_t testing, const uint8_t *active,
                                  float cpuct) {
   return m ? expand_backup(m, env, policy, value, noise, eps, testing, m->slot, true, active, cpuct) : -1;
+}
+
+int hz_mcts_expand_backup_select_gather(hz_mcts *m, hz_env *env, const float *policy, const float *value,
+                                        const double *noise, double eps, int32_t testing, const uint8_t *active,
+                                        float cpuct, float *board, float *glob, int32_t *rows, int32_t *count_out,
+                                        int32_t *count_prev, int32_t add_prev) {
+  if (!m || !board || !glob || !count_out || !count_prev || count_out == count_prev) return -1;
+  return expand_backup(m, env, policy, value, noise, eps, testing, m->slot, true, active, cpuct, board, glob, rows,
+                       count_out, count_prev, add_prev);
 }
 
 int hz_root_noise(const int32_t *count, int32_t n, uint64_t seed, uint64_t board_base, uint64_t move, double alpha,

@@ -968,12 +968,15 @@ constexpr int x6_class_blocks(int h, int tap) {
 // then conv2's chunks 0, 1, 2 stage chunk 1 (tmp), 2 (E) and 3 (tmp) into
 // the other buffer as the HBM staging does.
 // LDS: two chunk buffers + E (280 rows x 32 fp32) = 162,304 B.
-template <bool Block>
+// Cf (Block only): the fused block with the bank-conflict-free row table
+// kX6ClassRow instead of round 3's kX6ClassRowBlk (hz_resblock_x6_set_table;
+// the same bits: the table only places the rows)
+template <bool Block, bool Cf = false>
 __device__ __forceinline__ const int16_t (*x6_tab())[16] {
-  if constexpr (Block) return kX6ClassRowBlk;
+  if constexpr (Block && !Cf) return kX6ClassRowBlk;
   return kX6ClassRow;
 }
-template <bool Block>
+template <bool Block, bool Cf = false>
 __global__ void __launch_bounds__(256, 1)
     k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
                    const float *__restrict__ res, float *__restrict__ out, int32_t batch,
@@ -1090,7 +1093,7 @@ __global__ void __launch_bounds__(256, 1)
   // the first K-step's B fragments, under whose latency the setup runs
   int rtab[kRBT];
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) rtab[rb] = x6_tab<Block>()[rh * kRBT + rb][lane & 15];
+  for (int rb = 0; rb < kRBT; rb++) rtab[rb] = x6_tab<Block, Cf>()[rh * kRBT + rb][lane & 15];
   stage_issue(0);
   bf16x8 b[3][NCB], bn[3][NCB];
   bissue(b, 0);
@@ -1148,7 +1151,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int cb = 0; cb < NCB; cb++) b1v[cb] = bias[64 * chf + 16 * cb + (lane & 15)];
     uint2 rows[kRBT];  // the lane's 4 rows of each row block, all loads in flight at once
 #pragma unroll
-    for (int rb = 0; rb < kRBT; rb++) rows[rb] = *(const uint2 *)&x6_tab<Block>()[rh * kRBT + rb][4 * kg];
+    for (int rb = 0; rb < kRBT; rb++) rows[rb] = *(const uint2 *)&x6_tab<Block, Cf>()[rh * kRBT + rb][4 * kg];
     // chf is wave-uniform: one branch; a padding row (-1) writes to the
     // dummy cell / row 280, so no value takes a branch of its own
     auto put_all = [&](auto chfc) __attribute__((always_inline)) {
@@ -1308,7 +1311,7 @@ __global__ void __launch_bounds__(256, 1)
   const size_t gbase = (size_t)s0 * 35 * 128;
   int erow[kRBT];  // the lane's output row of each block (transposed tiles: lane -> row lane >> 2)
 #pragma unroll
-  for (int rb = 0; rb < kRBT; rb++) erow[rb] = x6_tab<Block>()[rh * kRBT + rb][lane >> 2];
+  for (int rb = 0; rb < kRBT; rb++) erow[rb] = x6_tab<Block, Cf>()[rh * kRBT + rb][lane >> 2];
   auto orow = [&](int rb) -> int {
     const int row = erow[rb];
     return row >= 0 && row < nrow ? row : -1;
@@ -1426,7 +1429,7 @@ static bool x6_w4() {
   return v;
 }
 
-template <bool Block>
+template <bool Block, bool Cf = false>
 static int launch_x6w4(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                        int32_t batch, const int32_t *live, void *stream, const void *wpack6_2 = nullptr,
                        const float *bias2 = nullptr, float *tmp = nullptr) {
@@ -1435,12 +1438,12 @@ static int launch_x6w4(const float *x, const void *wpack6, const float *bias, co
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
   if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
-    if (hipFuncSetAttribute((const void *)k_conv3x3_x6w4<Block>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void *)k_conv3x3_x6w4<Block, Cf>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return 1;
     init_mask.fetch_or(1ull << dev, std::memory_order_release);
   }
-  hipLaunchKernelGGL(k_conv3x3_x6w4<Block>, dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
+  hipLaunchKernelGGL((k_conv3x3_x6w4<Block, Cf>), dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
                      (const bf16x8 *)wpack6, bias, res, out, batch, live, (const bf16x8 *)wpack6_2, bias2, tmp);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
@@ -1460,6 +1463,20 @@ static bool x6_block() {
     int32_t want = e && atoi(e) == 0 ? 0 : 1, expect = -1;
     g_x6_block.compare_exchange_strong(expect, want);
     v = g_x6_block.load(std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+
+// the fused block's row table: 0 round 3's kX6ClassRowBlk, 1 the
+// bank-conflict-free kX6ClassRow (HZ_BLK_TABLE, hz_resblock_x6_set_table)
+static std::atomic<int32_t> g_x6_blk_cf{-1};
+static bool x6_blk_cf() {
+  int32_t v = g_x6_blk_cf.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("HZ_BLK_TABLE");
+    int32_t want = e && atoi(e) == 1 ? 1 : 0, expect = -1;
+    g_x6_blk_cf.compare_exchange_strong(expect, want);
+    v = g_x6_blk_cf.load(std::memory_order_relaxed);
   }
   return v == 1;
 }
@@ -1508,7 +1525,8 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
   if (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)out | (uintptr_t)tmp) & 15) return -1;
   if (batch == 0) return 0;
   if (hz_resblock_x6_fused(batch))
-    return launch_x6w4<true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp);
+    return x6_blk_cf() ? launch_x6w4<true, true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp)
+                       : launch_x6w4<true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp);
   const int rc = launch_x6<4, false>(x, w1, b1, nullptr, tmp, batch, live, stream);
   return rc ? rc : launch_x6<4, false>(tmp, w2, b2, x, out, batch, live, stream);
 }
@@ -1518,6 +1536,13 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
 extern "C" int hz_resblock_x6_set_fused(int32_t on) {
   if (on != 0 && on != 1) return -1;
   g_x6_block.store(on, std::memory_order_relaxed);
+  return 0;
+}
+
+// the fused block's row table (A/B and tests; the same bits either way)
+extern "C" int hz_resblock_x6_set_table(int32_t cf) {
+  if (cf != 0 && cf != 1) return -1;
+  g_x6_blk_cf.store(cf, std::memory_order_relaxed);
   return 0;
 }
 

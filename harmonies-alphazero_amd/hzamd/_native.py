@@ -60,6 +60,8 @@ _SIGS = {
     "hz_mcts_select_gather": ([_vp, _vp, _c.c_float, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_mcts_expand_backup_gathered": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32], _c.c_int),
     "hz_mcts_expand_backup_select": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32, _vp, _c.c_float], _c.c_int),
+    "hz_mcts_expand_backup_select_gather": ([_vp, _vp, _vp, _vp, _vp, _c.c_double, _c.c_int32, _vp, _c.c_float,
+                                             _vp, _vp, _vp, _vp, _vp, _c.c_int32], _c.c_int),
     "hz_mcts_result": ([_vp, _vp], _c.c_int),
     "hz_root_noise": ([_vp, _c.c_int32, _c.c_uint64, _c.c_uint64, _c.c_uint64, _c.c_double, _vp, _vp, _vp],
                       _c.c_int),
@@ -74,6 +76,7 @@ _SIGS = {
     "hz_resblock_x6_bias_act": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_resblock_x6_fused": ([_c.c_int32], _c.c_int32),
     "hz_resblock_x6_set_fused": ([_c.c_int32], _c.c_int),
+    "hz_resblock_x6_set_table": ([_c.c_int32], _c.c_int),
     "hz_tower_x6_resident": ([_vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split_max_batch": ([], _c.c_int32),

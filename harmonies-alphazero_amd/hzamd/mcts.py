@@ -50,6 +50,9 @@ class BatchedMCTS:
         self.counts = torch.zeros(self.n, 4, dtype=torch.int32, device=d)
         self.rows = torch.zeros(self.n, dtype=torch.int32, device=d)
         self.count = torch.zeros(1, dtype=torch.int32, device=d)
+        # the second leaf-count buffer of the fused gather (search(): the
+        # launch that consumes one count builds the next batch's in the other)
+        self.count_b = torch.zeros(1, dtype=torch.int32, device=d)
         self.eval_rows = torch.zeros(1, dtype=torch.int64, device=d)  # leaves evaluated, last search
         self.eval_rows_total = torch.zeros(1, dtype=torch.int64, device=d)  # ... all searches (one add each)
         # k_gather adds each simulation's gathered row count to it (no extra kernel)
@@ -62,6 +65,10 @@ class BatchedMCTS:
         # the next simulation's select inside each expand/backup launch
         # (search(); HZ_FUSE_SELECT=0 runs them as separate launches)
         self.fuse_select = os.environ.get("HZ_FUSE_SELECT", "1") != "0"
+        # ... and the next leaf batch's gather + encode too (each board that
+        # needs the network takes a row and encodes its leaf in that launch;
+        # HZ_FUSE_GATHER=0 keeps hz_mcts_gather_leaves' separate launch)
+        self.fuse_gather = os.environ.get("HZ_FUSE_GATHER", "1") != "0"
         self.edges_total = torch.zeros(1, dtype=torch.int64, device=d)
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
         self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
@@ -135,6 +142,24 @@ class BatchedMCTS:
                                                          nat.ptr(noise), float(eps), int(bool(testing)),
                                                          nat.ptr(active), float(cpuct)),
                   "hz_mcts_expand_backup_select")
+
+    def expand_backup_select_gather(self, policy, value, cpuct, active, noise, eps, testing, count_out, count_prev,
+                                    add_prev):
+        """expand_backup_select, then the next leaf batch in the same launch
+        (hz_mcts_expand_backup_select_gather): rows in arrival order into
+        self.board / self.glob / self.rows, its count into count_out (zero on
+        entry); count_prev (this batch's) is zeroed, and first added to the
+        eval counter when add_prev."""
+        if policy.numel() == 0:
+            policy, value = self._nil_pol, self._nil_val
+        policy = policy.to(dtype=torch.float32).contiguous()
+        value = value.reshape(-1).to(dtype=torch.float32).contiguous()
+        if noise is not None:
+            noise = noise.to(device=self.device, dtype=torch.float64).contiguous()
+        nat.check(nat.lib().hz_mcts_expand_backup_select_gather(
+            self._h, self.env.handle, nat.ptr(policy), nat.ptr(value), nat.ptr(noise), float(eps), int(bool(testing)),
+            nat.ptr(active), float(cpuct), nat.ptr(self.board), nat.ptr(self.glob), nat.ptr(self.rows),
+            nat.ptr(count_out), nat.ptr(count_prev), int(bool(add_prev))), "hz_mcts_expand_backup_select_gather")
 
     def result(self):
         nat.check(nat.lib().hz_mcts_result(self._h, nat.ptr(self.visits)), "hz_mcts_result")
@@ -231,14 +256,30 @@ class BatchedMCTS:
             return self._finish()
         if gather and total > 1 and self.n > 32 and self.fuse_select:
             # the next simulation's select rides in each expand/backup launch
+            # (and, fuse_gather, the gather + encode of its leaf batch: the
+            # two count buffers alternate, each zeroed by the launch after the
+            # one that filled it, so both are zero between searches)
+            fuse_gather = self.fuse_gather
+            if fuse_gather:
+                self.count_b.zero_()  # (defensive: a search cut short may have left it set)
             board, glob, rows, count = self.select_gather(cpuct, active)
+            bufs, cur = (self.count, self.count_b), 0
             for s in range(total):
                 policy, value = self._evaluate(evaluator, device_rows, board, glob, rows, count, max_rows)
                 if s + 1 < total:
-                    self.expand_backup_select(policy, value, cpuct, active, noise, eps, testing)
-                    board, glob, rows, count = self.gather_leaves()
+                    if fuse_gather:
+                        self.expand_backup_select_gather(policy, value, cpuct, active, noise, eps, testing,
+                                                         bufs[cur ^ 1], bufs[cur], add_prev=s > 0)
+                        cur ^= 1
+                        count = bufs[cur]
+                    else:
+                        self.expand_backup_select(policy, value, cpuct, active, noise, eps, testing)
+                        board, glob, rows, count = self.gather_leaves()
                 else:
                     self.expand_backup(policy, value, noise, eps, testing, gathered=True)
+            if fuse_gather:  # the last batch's count: no gather call added it
+                self.eval_rows += count
+                count.zero_()
             return self._finish()
         for _ in range(total):
             if not gather:

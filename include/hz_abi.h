@@ -148,8 +148,8 @@ int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_s
 int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
 /* hz_play's pipeline: 2 (the default; HZ_PIPELINE=1 in the environment at
  * hz_env_create makes 1 the default) = every board's game spread over
- * thirteen consecutive calls, one stage per call (seeding pass 1 in two
- * stages, pass 2 in three, four draw stages, four play stages), all thirteen
+ * thirteen consecutive calls, one stage per call (seeding pass 1 in one
+ * stage, pass 2 in two, five draw stages, five play stages), all thirteen
  * running in each launch on different episodes; 1 = the chance-ahead
  * pipeline above.  Same results either way; pipeline 2 applies to calls with
  * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
@@ -248,6 +248,19 @@ int hz_mcts_expand_backup_gathered(hz_mcts *mcts, hz_env *env, const float *poli
 int hz_mcts_expand_backup_select(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
                                  const double *noise, double eps, int32_t testing, const uint8_t *active,
                                  float cpuct);
+/* hz_mcts_expand_backup_select, then, in the same launch, the next leaf
+ * batch (hz_mcts_gather_leaves' outputs): each board whose new leaf needs
+ * the network takes the next row of *count_out (atomically: rows in
+ * arrival order, not board order; rows[j] = board of row j, as before) and
+ * encodes its leaf into board[j], glob[j].  *count_out must be 0 at launch;
+ * *count_prev (the count of the batch this launch consumes) is set to 0,
+ * after being added to the eval counter when add_prev != 0 (a count that no
+ * gather call added).  Every result (visits, trees, streams) equals the
+ * separate launches'; the evaluator must treat rows independently. */
+int hz_mcts_expand_backup_select_gather(hz_mcts *mcts, hz_env *env, const float *policy, const float *value,
+                                        const double *noise, double eps, int32_t testing, const uint8_t *active,
+                                        float cpuct, float *board, float *glob, int32_t *rows, int32_t *count_out,
+                                        int32_t *count_prev, int32_t add_prev);
 /* Self-play root noise (MCTS.py:314-316, np.random.dirichlet([alpha] * L)
  * over the L = count[b] legal moves, in legal-move order) into noise[n][69]
  * (zeros past L) and the tau = 1 move-choice uniform (MCTS.py:411,
@@ -307,6 +320,10 @@ int32_t hz_resblock_x6_fused(int32_t batch);
  * the one-launch form where it applies; 0: the two layered convs (A/B
  * measurements); results are bit-identical. */
 int hz_resblock_x6_set_fused(int32_t on);
+/* The one-launch form's row placement: 0 (the default, unless
+ * HZ_BLK_TABLE=1) round 3's row table, 1 the LDS-bank-conflict-free one the
+ * layered conv uses (A/B measurements; results are bit-identical). */
+int hz_resblock_x6_set_table(int32_t cf);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the

@@ -418,9 +418,12 @@ def test_resblock_x6_fused_equals_two_layered_convs(batch):
     prev = lib().hz_resblock_x6_fused(4096)
     assert lib().hz_resblock_x6_set_fused(1) == 0
     try:
-        _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6)
+        for table in (0, 1):  # both row placements of the one-launch form (hz_resblock_x6_set_table)
+            assert lib().hz_resblock_x6_set_table(table) == 0
+            _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6)
     finally:
         lib().hz_resblock_x6_set_fused(prev)
+        lib().hz_resblock_x6_set_table(0)
 
 
 def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):

@@ -184,7 +184,7 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
             k = int(count.item())
             self.calls.append(k)
             self.shapes.append(board.shape[0])
-            assert bool((rows[:k].diff() > 0).all())       # board order
+            assert rows[:k].unique().numel() == k           # one row per board (arrival order when fused)
             pol = torch.full((n, 143), float("nan"), device=DEV)
             val = torch.full((n,), float("nan"), device=DEV)
             p, v = stub_evaluator(board[:k], glob[:k])
@@ -229,11 +229,13 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
 
 def test_fused_select_equals_separate_launches():
     """search() runs each simulation's select inside the previous one's
-    expand/backup launch (hz_mcts_expand_backup_select) above 32 boards;
-    with fuse_select off the two are separate launches.  Same roots, noise
-    and streams: identical visit counts, tree sizes, leaf rows per
-    simulation and next CPython word of every board (self-play settings,
-    mid-game positions, 20 % of the boards inactive)."""
+    expand/backup launch above 32 boards, and (fuse_gather) the next leaf
+    batch's gather + encode there too, rows in arrival order.  Against
+    separate launches (select, gather + encode in board order): identical
+    visit counts, tree sizes, leaf rows per simulation, next CPython word of
+    every board, and every simulation's batch is the same set of boards with
+    bit-identical encoded rows (self-play settings, mid-game positions, 20 %
+    of the boards inactive)."""
     from hzamd.env import BatchedEnv
     from hzamd.mcts import BatchedMCTS, stub_evaluator
     from hzamd.selfplay import NoiseSource
@@ -241,7 +243,7 @@ def test_fused_select_equals_separate_launches():
     g = torch.Generator().manual_seed(3)
     active = (torch.rand(n, generator=g) > 0.2).to(DEV)
     out = []
-    for fuse in (True, False):
+    for fuse, fuse_gather in ((True, True), (True, False), (False, False)):
         env = BatchedEnv(n, seed_base=base, device=DEV)
         env.reset()
         for p in range(20 + (base % 7)):
@@ -252,21 +254,33 @@ def test_fused_select_equals_separate_launches():
         noise, _ = NoiseSource(base, DEV).draw(5, count, 0.4)
         mcts = BatchedMCTS(env, sims)
         mcts.fuse_select = fuse
-        rows = []
+        mcts.fuse_gather = fuse_gather
+        rows, batches = [], []
 
         class DeviceRows:
             device_rows = True
 
             def __call__(self, board, glob, r, count):
                 rows.append(count.clone())
+                k = int(count.item())
+                order = torch.argsort(r[:k])
+                batches.append((r[:k][order].clone(), board[:k][order].clone(), glob[:k][order].clone()))
                 return stub_evaluator(board, glob)
         v = mcts.search(DeviceRows(), 2.0, active=act_b, noise=noise, eps=0.25, testing=False).clone()
         st, mt, idx = env.export_state(with_mt=True)
-        out.append((v.cpu(), mcts.stats().clone().cpu(), torch.cat(rows).cpu(), mt.cpu(), idx.cpu()))
+        out.append((v.cpu(), mcts.stats().clone().cpu(), torch.cat(rows).cpu(), mt.cpu(), idx.cpu(),
+                    mcts.eval_rows.clone().cpu(), batches))
+        assert int(mcts.count.item()) == 0 or not fuse_gather
         mcts.close()
         env.close()
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+    for x in out[1:]:
+        for a, b in zip(out[0][:6], x[:6]):
+            assert torch.equal(a, b)
+        assert len(out[0][6]) == len(x[6]) == sims
+        for ba, bb in zip(out[0][6], x[6]):
+            for ta, tb in zip(ba, bb):
+                assert torch.equal(ta, tb)
+    assert int(out[0][5]) == int(out[0][2].sum())  # the eval counter holds every batch's rows
 
 
 def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
