@@ -690,28 +690,6 @@ struct MTR {
   }
 };
 
-// A stream in a quad-interleaved slot of k_play2 (word i of board b at
-// slot[(i >> 2) * 4 * nrow + 4 * b + (i & 3)]): w = slot + 4 b, s4 = 4 nrow.
-struct QuadPtr {
-  uint32_t* w;
-  int s4;
-  __device__ __forceinline__ uint32_t& operator[](int i) const { return w[(size_t)(i >> 2) * s4 + (i & 3)]; }
-};
-struct MTQ {
-  uint32_t* w;
-  int s4, pos, tw;
-  __device__ __forceinline__ MTQ(uint32_t* words, int s, int cursor)
-      : w(words), s4(s), pos(cursor & 0xFFFF), tw(cursor >> 16) {}
-  __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
-  __device__ __forceinline__ void prefetch() {}
-  __device__ __forceinline__ uint32_t next() {
-    if (pos >= kMT) { pos = 0; tw = 0; }
-    const QuadPtr q{w, s4};
-    if (pos >= tw) tw += twist_block(q, 1, tw);
-    return temper(q[pos++]);
-  }
-};
-
 template <class M>
 __device__ __forceinline__ uint32_t randbelow(M& m, uint32_t n) {
   if (!n) return 0;

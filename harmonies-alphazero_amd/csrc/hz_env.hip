@@ -69,16 +69,18 @@ struct hz_env {
   // spread over thirteen consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
   int calls2, primed2;
-  int p2_cut[4];             // the play stages' ply boundaries (HZ_P2_CUTS)
+  int p2_cut[3];             // the play stages' ply boundaries (HZ_P2_CUTS)
   uint32_t *p2_s[14];        // [624][nrow] stream slots (kP2Stream)
   int32_t *p2_s_tag[14];     // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
   int32_t *p2_s_cur[14];     // [kAheadDraws + 1][nrow] the slot's cursor before draw 0 and after each draw
-  uint32_t *p2_ph[2];        // [3][nrow] P2x -> P2y, by call parity
-  P2Draw p2_x[4][2];         // D1 -> D2 -> .. -> D5, by call parity
-  P2Draw p2_pl[6];           // D5 -> play0 .. play4: a ring of six
-  P2Mid p2_m[4][2];          // play0 -> play1 -> .. -> play4, by call parity
-  uint32_t *p2_h[6];         // [kRulePlies][nrow] rule hashes, a ring of six
-  int32_t *p2_h_tag[6];      // [nrow] their episode
+  uint32_t *p2_p1h[2];       // [nrow] P1a -> P1b
+  uint32_t *p2_p2h[2];       // [2][nrow] P2a -> P2b
+  uint32_t *p2_p3h[2];       // [2][nrow] P2b -> P2c
+  P2Draw p2_x[3][2];         // D1 -> D2 -> D3 -> D4, by call parity
+  P2Draw p2_pl[5];           // D4 -> playA, playB, playC, playD: a ring of five
+  P2Mid p2_m[3][2];          // playA -> playB -> playC -> playD, by call parity
+  uint32_t *p2_h[5];         // [kRulePlies][nrow] rule hashes, a ring of five
+  int32_t *p2_h_tag[5];      // [nrow] their episode
   int32_t *p2_ep[2];         // [nrow] episode counter each board ended the call with
   // a pipeline wave that gives up waiting for its publisher (a bounded spin
   // on an LDS progress counter) ORs a bit into *wait_err (kWaitErr*), so the
@@ -1154,60 +1156,48 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // hz_play's second pipeline (hz_env_set_pipeline(e, 2)).  Each of
 // k_rollout's roles runs one serial per-board chain of ~60 k cycles (a whole
 // game, a whole seeding, 16 pile draws), and a launch lasts as long as its
-// longest chain.  Here every board's episode is cut into thirteen stages,
-// one per consecutive hz_play call, and one launch runs all thirteen at
-// once, each on a different episode of the board (ep = the episode counter
-// the previous call left, p2_ep; stage s works on episode ep + 12 - s):
-//   s = 0  P1     seeding pass 1, steps 1-624          seed blocks, wave 3
-//   s = 1  P2x    pass 2, steps 2-312                  seed blocks, wave 0
-//   s = 2  P2y    pass 2, steps 313-624; rows 0-223    seed blocks, wave 1
-//                 of the next generation twisted       (twist: wave 2)
-//   s = 3  D1     pile draws 0-4                       draw-X blocks, wave 0
-//   s = 4  D2     draws 5-9                            draw-X blocks, wave 1
-//   s = 5  D3     draws 10-14                          draw-X blocks, wave 2
-//   s = 6  D4     draws 15-19                          draw-Y blocks, wave 0
-//   s = 7  D5     draws 20-23                          draw-Y blocks, wave 1
-//          (the episode's rule hashes meanwhile:       draw-X blocks, wave 3)
-//   s = 8  play0  plies [0, cut0)                      draw-Y blocks, wave 2
-//   s = 9  play1  plies [cut0, cut1)                   play blocks, wave 3
-//   s = 10 play2  plies [cut1, cut2)                   play blocks, wave 2
-//   s = 11 play3  plies [cut2, cut3)                   play blocks, wave 1
-//   s = 12 play4  the rest, final scoring, the board's play blocks, wave 0
-//                 state, cursor and counters
-// The stream slots are quad-interleaved (row r of board b at
-// slot[(r >> 2) * 4 * nrow + 4 * b + (r & 3)]): a lane's four consecutive
-// words are one 16-B access and a wave's 64 boards' quads are 1 KB
-// contiguous, so the seeding chains store one 16-B word per four steps
-// (a chain step with a b32 LDS read and a b32 store cost ~56 cycles, with
-// 16-B operations per four steps ~29: tools/alu_chain.py), which lets pass
-// 1 run as one stage and pass 2 as two, and frees the waves for a fifth draw
-// stage and a fifth play stage.
-// An episode's stream lives in one slot of a ring of kP2Stream from P1 to
-// play4 (and afterwards as the board's current stream until materialize or
+// longest chain.  Here every board's episode is cut into thirteen stages of
+// 20-30 k cycles, one per consecutive hz_play call, and one launch runs all
+// thirteen at once, each on a different episode of the board (ep = the
+// episode counter the previous call left, p2_ep; stage s works on episode
+// ep + 12 - s):
+//   s = 0  P1a   seeding pass 1, steps 1-312          draw-Y blocks, wave 2
+//   s = 1  P1b   pass 1, steps 313-624                draw-X blocks, wave 2
+//   s = 2  P2a   pass 2, steps 2-208                  seed blocks, wave 0
+//   s = 3  P2b   pass 2, steps 209-416                seed blocks, wave 1
+//   s = 4  P2c   pass 2, steps 417-624; rows 0-223    seed blocks, wave 2
+//                of the next generation twisted       (twist: wave 3)
+//   s = 5  D1    pile draws 0-5                       draw-X blocks, wave 0
+//   s = 6  D2    draws 6-11                           draw-X blocks, wave 1
+//   s = 7  D3    draws 12-17                          draw-Y blocks, wave 0
+//   s = 8  D4    draws 18-23                          draw-Y blocks, wave 1
+//          (the episode's rule hashes meanwhile:      draw-X blocks, wave 3)
+//   s = 9  playA plies [0, cut0)                      play blocks, wave 3
+//   s = 10 playB plies [cut0, cut1)                   play blocks, wave 2
+//   s = 11 playC plies [cut1, cut2)                   play blocks, wave 1
+//   s = 12 playD the rest, final scoring, the board's play blocks, wave 0
+//                state, cursor and counters
+// An episode's stream lives in one slot of a ring of kP2Stream from P1a to
+// playD (and afterwards as the board's current stream until materialize or
 // the next call); stage s of call c uses slot (c - s) mod kP2Stream.  A stage
 // uses an input only when its tag names the stage's episode, so a wrong
-// prediction costs time, never results: the stages skip the board and play4
+// prediction costs time, never results: the stages skip the board and playD
 // plays its whole game from scratch (seeding and drawing in LDS, like
 // k_rollout's unprepared boards).  The results are k_rollout's: the board ends
 // the call with episode ep's final state, cursor and counters, and
-// games_done / steps_done count that game (its first plies ran in the four
-// calls before, in play0 .. play3).  In steady state a call does every stage
-// once per board: one game's worth of work per board per call.
+// games_done / steps_done count that game (its first plies ran in the three
+// calls before, in playA, playB and playC).  In steady state a call does
+// every stage once per board: one game's worth of work per board per call.
 constexpr int kP2Win = 96;        // rows a draw stage stages, from its wave's lowest cursor
 constexpr int kP2WinRows = kP2Win + 24;  // LDS rows per window (a scan reads up to 23 rows past its cursor)
-constexpr int kP2Draw = 5;        // draw stages
-constexpr int kP2Play = 5;        // play stages
-constexpr int kP2FirstDraw = 3;   // stage of D1
-constexpr int kP2FirstPlay = kP2FirstDraw + kP2Draw;  // stage of play0
-constexpr int kP2Stages = kP2FirstPlay + kP2Play;     // 13
+constexpr int kP2Play = 4;        // play stages
+constexpr int kP2Stages = 9 + kP2Play;
 constexpr int kP2Last = kP2Stages - 1;  // stage s works on episode ep + kP2Last - s
-constexpr int kP2Ring = kP2Play + 1;    // D5's scripts and the rule hashes: read by the play stages 1..kP2Play calls later
-constexpr int kP2Stream = kP2Stages + 1;  // stream slots (the last play stage's slot stays the board's stream)
+constexpr int kP2Ring = kP2Play + 1;    // D4's scripts and the rule hashes: read by the play stages 1..kP2Play calls later
+constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: the last play stage's slot stays the board's stream)
+constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
 constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
-constexpr int kP2xEnd = 313;      // P2x: pass-2 steps [2, 313), P2y [313, 624) and the last one, at i = 1
-constexpr int kP2Quads = kMT / 4; // 156 quads per stream
-constexpr int kP2LdsY = 79;       // P2y's LDS quads start here (P2x's: 0-78, pass-1 rows 0-315)
-__device__ __forceinline__ constexpr int p2_draw_cut(int d) { return d >= kP2Draw ? kAheadDraws : 5 * d; }
+constexpr int kP1Split = 313;
 #ifdef HZ_DIAG
 constexpr int kP2Stamps = 48;  // stamp slots per board in k_play2 (tools/p2_roles.py)
 #define P2_PHASE(slot, t0)                                                                                       \
@@ -1220,11 +1210,10 @@ constexpr int kP2Stamps = 48;  // stamp slots per board in k_play2 (tools/p2_rol
 #define P2_PHASE(slot, t0) \
   do {                     \
   } while (0)
-#endif
-static_assert(p2_draw_cut(kP2Draw - 1) < kAheadDraws && p2_draw_cut(kP2Draw) == kAheadDraws, "draw stages cover the script");
-static_assert(3 * kP2WinRows * kLdsStride * 4 <= (int)kResetLds, "three windows per draw block");
-static_assert((kP2LdsY + kP2Quads - 78) * 64 * 16 <= (int)kResetLds, "P2x's and P2y's LDS quads fit");
-static_assert(kMT % 4 == 0, "whole quads");
+#endif     // pass 1: P1a runs steps [1, 313), P1b [313, 624) and the 624th
+static_assert(4 * kP2DrawsPer == kAheadDraws, "four draw stages cover the script");
+static_assert(2 * kP2WinRows * kLdsStride * 4 <= (int)kResetLds, "two windows per draw block");
+static_assert((kP1Split - 1) % 8 == 0 && (617 - kP1Split) % 8 == 0, "pass-1 halves in groups of eight");
 
 struct P2Args {
   uint64_t *st;
@@ -1238,14 +1227,18 @@ struct P2Args {
   int32_t *games_done, *steps_done, *mt_src;
   const int32_t *ep_in;
   int32_t *ep_out;
-  uint32_t *s_mt[kP2Stages];  // the stream slot of each stage this call (quad-interleaved)
-  int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 2 pass 1 / 3 P2x / 5 seeded, rows 0-223 twisted
+  uint32_t *s_mt[kP2Stages];  // the stream slot of each stage this call
+  int32_t *s_tag[kP2Stages];  // [nrow] episode * 8 + 1 P1a / 2 pass 1 / 3 P2a / 4 P2b / 5 seeded, rows 0-223 twisted
   int32_t *s_cur[kP2Stages];  // [kAheadDraws + 1][nrow] cursor before draw 0 and after each draw
   int s_idx_last;             // the last play stage's slot index (materialize: mt_src = 2 + index)
-  uint32_t *ph_w;             // [3][nrow] P2x -> P2y: pass 2's last value, pass 1's row-1 word, row 2's final word
-  const uint32_t *ph_r;
-  P2Draw x_w[kP2Draw - 1], x_r[kP2Draw - 1];  // D1 -> D2 -> .. -> D5 (tag: episode * 8 + stages done)
-  P2Draw pl_w, pl_r[kP2Play];     // D5's script: written this call; read by play stage st (st + 1 calls later)
+  uint32_t *p1h_w;            // [nrow] P1a -> P1b: pass 1's last value
+  const uint32_t *p1h_r;
+  uint32_t *p2h_w;            // [3][nrow] P2a -> P2b: pass 2's last value, pass 1's row-1 word, row 2's final word
+  const uint32_t *p2h_r;
+  uint32_t *p3h_w;            // [2][nrow] P2b -> P2c: the same
+  const uint32_t *p3h_r;
+  P2Draw x_w[3], x_r[3];      // D1 -> D2 -> D3 -> D4 (tag: episode * 8 + stages done)
+  P2Draw pl_w, pl_r[kP2Play];     // D4's script: written this call; read by play stage st (st + 1 calls later)
   P2Mid m_w[kP2Play - 1], m_r[kP2Play - 1];  // play stage st -> st + 1 (written / read this call)
   uint32_t *h_w;                  // [kRulePlies][nrow] rule hashes
   const uint32_t *h_r[kP2Play];
@@ -1261,7 +1254,7 @@ struct PlayDraw2 {
   uint64_t q0, q1, q2, q3;
   int d, nd;
   bool fell;
-  MTQ gm;                  // valid once fell
+  MTR gm;                  // valid once fell
   const int32_t *cur_nd;   // the slot's cursor after the last scripted draw (read when the script runs out)
   __device__ __forceinline__ uint32_t pop() {
     uint32_t p9 = (uint32_t)q0 & 0x1FFu;
@@ -1276,7 +1269,7 @@ struct PlayDraw2 {
   __device__ __forceinline__ uint32_t draw_one(uint64_t misc) {
     if (d < nd) return pop();
     if (!fell) {
-      gm = MTQ(gm.w, gm.s4, *cur_nd);
+      gm = MTR(gm.w, gm.stride, *cur_nd);
       fell = true;
     }
     uint32_t p9;
@@ -1392,434 +1385,455 @@ __device__ __forceinline__ void p2_publish(int *flag, int v) {
   asm volatile("" ::: "memory");
   __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// ---- quad-interleaved stream slots
-typedef uint32_t p2u4 __attribute__((ext_vector_type(4)));
-typedef uint32_t p2u3 __attribute__((ext_vector_type(3)));
-typedef uint32_t p2u2 __attribute__((ext_vector_type(2)));
-// the slot's quads of boards [b0, b0 + 64) as a buffer: lane l's quad of
-// rows [4 q, 4 q + 4) at voffset 16 l, soffset q * 16 nrow (a scalar: no
-// 64-bit address arithmetic in the chains)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_rsrc(uint32_t *slot, int b0, size_t nr) {
-  const uint64_t base = (uint64_t)(slot + 4 * (size_t)b0);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kP2Quads * 16 * nr - (size_t)b0 * 16));
-  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+// init_by_array's pass 1, steps [i0, i1) (i0 odd, groups of eight: odd
+// steps take key word kA, even ones kB), rows at w[i * ns]; step 1's value
+// goes to row 1 (the 624th step reads it back)
+// (wb = the slot's column of the wave's first board, wave-uniform, so a
+// row's address is a scalar base plus the lane: no 64-bit address
+// arithmetic per step in the chain)
+__device__ __forceinline__ void mt_pass1_span(uint32_t *__restrict__ wb, int lane, size_t ns, uint32_t kA, uint32_t kB,
+                                              int i0, int i1, uint32_t &prev) {
+  // init_genrand's table words a group ahead (scalar loads: their wait
+  // would otherwise sit in the chain once per group)
+  uint32_t iv[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[i0 + u];
+#pragma unroll 1
+  for (int g = i0; g < i1; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+      wb[(size_t)(g + u) * ns + lane] = v;
+      prev = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) iv[u] = nx[u];
+  }
 }
-__device__ __forceinline__ void p2_st4(__amdgpu_buffer_rsrc_t rs, int lane, int soff, uint32_t x, uint32_t y,
-                                       uint32_t z, uint32_t w) {
-  const p2u4 v = {x, y, z, w};
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, lane * 16, __builtin_amdgcn_readfirstlane(soff), 0);
-}
-__device__ __forceinline__ uint4 p2_ld4(__amdgpu_buffer_rsrc_t rs, int lane, int soff) {
-  const p2u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, __builtin_amdgcn_readfirstlane(soff), 0);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-// a lane's LDS quad k (the seed blocks stage pass-1 words in the slot's own
-// quad layout: 1 KB per quad row of the wave's 64 boards, 16-B accesses)
-__device__ __forceinline__ uint4 &p2_lq(int k, int lane) { return reinterpret_cast<uint4 *>(hz_lds)[k * 64 + lane]; }
-
 __device__ __forceinline__ void p2_keys(uint64_t seed, uint32_t &kA, uint32_t &kB) {
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   kA = key0;
   kB = key1 ? key1 + 1u : key0;
 }
 
-// P1 (seed blocks, wave 3): init_by_array's pass 1 (random.seed(int) ->
-// init_by_array(key), key = the seed's 32-bit words) in one chain: steps
-// 1-623 (odd steps key word kA, even ones kB), then the 624th at i = 1 (its
-// mt[0] = mt[623] is the chain's last value); one 16-B store per four
-// steps.  Row 0 is never read by pass 2.  No LDS.
-__device__ __forceinline__ void p2_p1(const P2Args &a, int b0, int lane) {
+// P1a (seed blocks, wave 0) and P1b (draw-X blocks, wave 2): no LDS
+__device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
   const int b = b0 + lane;
   const size_t nr = (size_t)a.nrow;
   const int e = a.ep_in[b] + kP2Last;
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
-  const __amdgpu_buffer_rsrc_t rs = p2_rsrc(a.s_mt[0], b0, nr);
-  const int qb = (int)(nr * 16);
   uint32_t prev = 19650218u;
-  auto step = [&](uint32_t iv, uint32_t k) {
-    const uint32_t v = (iv ^ ((prev ^ (prev >> 30)) * 1664525U)) + k;
+  mt_pass1_span(a.s_mt[0] + b0, lane, nr, kA, kB, 1, kP1Split, prev);
+  a.p1h_w[b] = prev;
+  a.s_tag[0][b] = e * 8 + 1;
+}
+__device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
+  const int b = b0 + lane;
+  const size_t nr = (size_t)a.nrow;
+  const int e = a.ep_in[b] + kP2Last - 1;
+  if (a.s_tag[1][b] != e * 8 + 1) return;
+  uint32_t kA, kB;
+  p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
+  uint32_t prev = a.p1h_r[b];
+  uint32_t *w = a.s_mt[1] + b;
+  mt_pass1_span(a.s_mt[1] + b0, lane, nr, kA, kB, kP1Split, 617, prev);
+#pragma unroll
+  for (int u = 0; u < 7; u++) {  // steps 617..623
+    const uint32_t v = (kInitGen.v[617 + u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
+    w[(size_t)(617 + u) * nr] = v;
     prev = v;
-    return v;
-  };
-  const uint32_t w1 = step(kInitGen.v[1], kA), w2 = step(kInitGen.v[2], kB), w3 = step(kInitGen.v[3], kA);
-  // init_genrand's table words a group ahead (scalar loads: their wait would
-  // otherwise sit in the chain once per group)
-  uint32_t iv[8];
-#pragma unroll
-  for (int u = 0; u < 8; u++) iv[u] = kInitGen.v[4 + u];
-#pragma unroll 1
-  for (int g = 4; g < 620; g += 8) {  // rows 4-619: two quads per group
-    uint32_t nx[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
-    const uint32_t v0 = step(iv[0], kB), v1 = step(iv[1], kA), v2 = step(iv[2], kB), v3 = step(iv[3], kA);
-    p2_st4(rs, lane, (g >> 2) * qb, v0, v1, v2, v3);
-    const uint32_t v4 = step(iv[4], kB), v5 = step(iv[5], kA), v6 = step(iv[6], kB), v7 = step(iv[7], kA);
-    p2_st4(rs, lane, ((g >> 2) + 1) * qb, v4, v5, v6, v7);
-#pragma unroll
-    for (int u = 0; u < 8; u++) iv[u] = nx[u];
   }
-  {  // rows 620-623 (iv: table words 620-623)
-    const uint32_t v0 = step(iv[0], kB), v1 = step(iv[1], kA), v2 = step(iv[2], kB), v3 = step(iv[3], kA);
-    p2_st4(rs, lane, (kP2Quads - 1) * qb, v0, v1, v2, v3);
-  }
-  // the 624th step at i = 1 (key j = 623 % keylen -> kB), prev = mt[623] = mt[0]
-  const uint32_t r1 = (w1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
-  p2_st4(rs, lane, 0, 0u, r1, w2, w3);
-  a.s_tag[0][b] = e * 8 + 2;
+  // mt[0] = mt[623]; the 624th step at i = 1 (key j = 623 % keylen -> kB)
+  w[nr] = (w[nr] ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+  a.s_tag[1][b] = e * 8 + 2;
 }
 
-// Pass 2 in two stages, P2x (steps 2-312) and P2y (313-623 and the last
-// step, at i = 1), in one seed block on disjoint LDS quads (the pass-1 words
-// of two different episodes).  Every step reads the next pass-1 word, too
-// close ahead for an HBM round trip, so each chain first stages its half of
-// the pass-1 words into LDS (16-B loads and LDS writes, all of a piece in
-// flight at once, the slot's own quad layout), then runs on 16-B LDS reads
-// two quads ahead and stores one 16-B word per four steps.  The stage's rows
-// come in three pieces, each next piece's loads issued before the chain runs
-// over the piece before it: two thirds of the staging reads leave the
-// launch's opening burst.  Rows 2-223 of the slot are read only by the
-// twist, which needs from each row r only its twist part (rows r and r + 1's
-// words): P2x stores that instead of the final word (one step late), so the
-// twist is one xor per word with the far row.  P2x hands (prev, pass 1's
-// row-1 word, row 2's final word) to P2y, which keeps its final words in LDS
-// for the twist and writes rows 0 and 1 of the next generation.
-// twist_word(cur, next, far) = far ^ twist_part(cur, next)
+// Pass 2 in three stages, P2a (steps 2-208), P2b (209-416) and P2c
+// (417-623 and the last step at i = 1), in one seed block on disjoint rows
+// of its [624][65] LDS array (the rows of three different episodes).  Every
+// step reads the next pass-1 word, too close ahead for an HBM round trip (a
+// chain reading the slot through a register ring stalled on the memory
+// counter: ~220 k cycles per half), so each chain first stages its third of
+// the pass-1 words into its own rows (all loads in flight at once), then
+// runs on LDS reads, storing each final word to the slot with a buffer store
+// (the row offset a scalar: no address arithmetic in the chain).  A chain
+// step costs ~70 cycles with one wave per SIMD (the four dependent VALU
+// operations of the recurrence plus the step's memory instructions; staging
+// transposed, four words per LDS access, changed nothing), so the chain is
+// cut into thirds rather than made cheaper per step.
+constexpr int kP2aEnd = 209, kP2bEnd = 417;
+constexpr int kTwKeep = 397;  // P2c's final rows from here on stay in LDS (the twist reads rows 397-620)
+// Rows [R0, R1) of the wave's 64 boards staged from the slot into LDS, in
+// two halves: p2_load issues the 16-B loads (four boards of a row per lane,
+// four rows per instruction) into registers, p2_put writes them to LDS.  A
+// pass-2 stage stages its first piece, issues the next piece's loads and
+// runs its chain over the first piece while they land: two thirds of the
+// staging reads leave the launch's opening burst, where every stage's first
+// inputs arrive.
+template <int R0, int R1>
+struct P2Piece {
+  uint4 v[(R1 - R0 + 3) / 4];
+};
+template <int R0, int R1>
+__device__ __forceinline__ void p2_load(P2Piece<R0, R1> &pc, const uint32_t *__restrict__ slot, size_t nr, int b0,
+                                        int lane) {
+  constexpr int U = (R1 - R0 + 3) / 4;
+  const int c4 = (lane & 15) * 4;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int r = R0 + 4 * u + (lane >> 4);
+    if (r < R1) pc.v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+  }
+}
+template <int R0, int R1>
+__device__ __forceinline__ void p2_put(const P2Piece<R0, R1> &pc, int lane) {
+  constexpr int U = (R1 - R0 + 3) / 4;
+  const int c4 = (lane & 15) * 4;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int r = R0 + 4 * u + (lane >> 4);
+    if (r < R1) {
+      uint32_t *d = hz_lds + r * kLdsStride + c4;
+      d[0] = pc.v[u].x;
+      d[1] = pc.v[u].y;
+      d[2] = pc.v[u].z;
+      d[3] = pc.v[u].w;
+    }
+  }
+  // (a wave's LDS operations execute in order: its later reads see these)
+}
+// the slot's columns of boards [b0, b0 + 64) as a buffer (rows of nr words)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, int b0, size_t nr) {
+  const uint64_t base = (uint64_t)(slot + b0);
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+// twist_word(cur, next, far) = far ^ twist_part(cur, next): the part of row
+// r's next-generation word that rows r and r + 1 decide
 __device__ __forceinline__ uint32_t twist_part(uint32_t cur, uint32_t next) {
   const uint32_t y = (cur & 0x80000000U) | (next & 0x7fffffffU);
   return (y >> 1) ^ ((y & 1U) ? 0x9908b0dfU : 0U);
 }
-__device__ __forceinline__ uint32_t p2_step(uint32_t p1, uint32_t &prev, int i) {
-  const uint32_t v = (p1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
-  prev = v;
-  return v;
-}
-// HBM quads [Q0, Q1) of the lane's board -> LDS quads from Q0 + D
-template <int Q0, int Q1>
-struct P2QPiece {
-  uint4 v[Q1 - Q0];
-};
-template <int Q0, int Q1>
-__device__ __forceinline__ void p2_qload(P2QPiece<Q0, Q1> &pc, __amdgpu_buffer_rsrc_t rs, int lane, int qb) {
+// What a pass-2 step stores: its final word to its row (kP2Final), the same
+// and over the pass-1 word in LDS (kP2Keep, P2c), or the previous row's
+// twist part (kP2Part: rows 2-223, which only the twist reads)
+enum { kP2Final = 0, kP2Keep = 1, kP2Part = 2 };
+// steps [G0, G1) of pass 2 (G1 - G0 a multiple of 8) on the lane's LDS
+// column, pass-1 words read 8 steps ahead (rows below G1), stores to the
+// slot (buffer stores: voffset the lane, soffset the row) as Mode says (in
+// LDS in place: the read-ahead is always past the rows written), with
+// kP2Keep publishing progress every 8 steps
+template <int G0, int G1, int Mode>
+__device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev,
+                                        int *prog) {
+  constexpr bool KeepLds = Mode == kP2Keep;
+  static_assert((G1 - G0) % 8 == 0, "groups of eight");
+  uint32_t *l = hz_lds + lane;
+  constexpr int S = kLdsStride;
+  uint32_t cur[8];
 #pragma unroll
-  for (int u = 0; u < Q1 - Q0; u++) pc.v[u] = p2_ld4(rs, lane, (Q0 + u) * qb);
-}
-template <int D, int Q0, int Q1>
-__device__ __forceinline__ void p2_qput(const P2QPiece<Q0, Q1> &pc, int lane) {
-#pragma unroll
-  for (int u = 0; u < Q1 - Q0; u++) p2_lq(Q0 + u + D, lane) = pc.v[u];
-  // (a wave's LDS operations execute in order: its later reads see these)
-}
-// groups k in [K0, K1) of four steps 4k .. 4k + 3 on LDS quads k + D, reads
-// two quads ahead.  Part: step 4k completes row 4k - 1's part (quad k - 1
-// stored), steps 4k + 1 .. 4k + 3 give rows 4k .. 4k + 2 (acc.x-z).  Final:
-// quad k's final words stored; Keep also writes them over the pass-1 quad
-// in LDS and publishes progress every two groups.
-enum { kP2Part = 0, kP2Final = 1, kP2Keep = 2 };
-template <int K0, int K1, int D, int Mode>
-__device__ __forceinline__ void p2_groups(int lane, __amdgpu_buffer_rsrc_t rs, int qb, uint32_t &prev, uint4 &acc,
-                                          int *prog) {
-  static_assert(Mode != kP2Keep || (K1 - K0) % 2 == 0, "Keep: pairs of groups");
-  uint4 p0 = p2_lq(K0 + D, lane), p1 = p2_lq((K0 + 1 < K1 ? K0 + 1 : K1 - 1) + D, lane);
+  for (int u = 0; u < 8; u++) cur[u] = l[(G0 + u) * S];
 #pragma unroll 2
-  for (int k = K0; k < K1; k++) {
-    const uint4 p2 = p2_lq((k + 2 < K1 ? k + 2 : K1 - 1) + D, lane);
-    const int i = 4 * k;
-    if constexpr (Mode == kP2Part) {
-      const uint32_t c = prev;
-      const uint32_t v0 = p2_step(p0.x, prev, i);
-      acc.w = twist_part(c, v0);
-      p2_st4(rs, lane, (k - 1) * qb, acc.x, acc.y, acc.z, acc.w);
-      const uint32_t v1 = p2_step(p0.y, prev, i + 1);
-      acc.x = twist_part(v0, v1);
-      const uint32_t v2 = p2_step(p0.z, prev, i + 2);
-      acc.y = twist_part(v1, v2);
-      const uint32_t v3 = p2_step(p0.w, prev, i + 3);
-      acc.z = twist_part(v2, v3);
-    } else {
-      const uint32_t v0 = p2_step(p0.x, prev, i), v1 = p2_step(p0.y, prev, i + 1);
-      const uint32_t v2 = p2_step(p0.z, prev, i + 2), v3 = p2_step(p0.w, prev, i + 3);
-      p2_st4(rs, lane, k * qb, v0, v1, v2, v3);
-      if constexpr (Mode == kP2Keep) {
-        p2_lq(k + D, lane) = make_uint4(v0, v1, v2, v3);
-        if ((k - K0) & 1) p2_publish(prog, 4 * k + 4);  // rows below final in LDS
-      }
+  for (int g = G0; g < G1; g += 8) {
+    uint32_t nx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nx[u] = l[(g + 8 + u < G1 ? g + 8 + u : G1 - 1) * S];
+    const uint32_t kneg = __builtin_amdgcn_readfirstlane(0u - (uint32_t)g);
+    const int soff = __builtin_amdgcn_readfirstlane((Mode == kP2Part ? g - 1 : g) * row_bytes);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      // (cur ^ p) - (g + u) as one v_xad_u32 with the offset in an SGPR
+      const uint32_t p = (prev ^ (prev >> 30)) * 1566083941U;
+      uint32_t v;
+      asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
+      __builtin_amdgcn_raw_buffer_store_b32(Mode == kP2Part ? twist_part(prev, v) : v, rs, lane * 4,
+                                            soff + u * row_bytes, 0);
+      if (KeepLds) l[(g + u) * S] = v;
+      prev = v;
     }
-    p0 = p1;
-    p1 = p2;
+    if (KeepLds) p2_publish(prog, g + 8);  // rows [G0, g + 8) final in LDS
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = nx[u];
+  }
+}
+// the last steps [G, G1) one by one
+template <int G, int G1, int Mode>
+__device__ __forceinline__ void p2_tail(int lane, __amdgpu_buffer_rsrc_t rs, int row_bytes, uint32_t &prev) {
+#pragma unroll
+  for (int i = G; i < G1; i++) {
+    const uint32_t v = (hz_lds[i * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+    if (Mode == kP2Part) __builtin_amdgcn_raw_buffer_store_b32(twist_part(prev, v), rs, lane * 4, (i - 1) * row_bytes, 0);
+    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, 0);
+    if (Mode == kP2Keep) hz_lds[i * kLdsStride + lane] = v;
+    prev = v;
   }
 }
 
-// P2x (seed blocks, wave 0): the episode whose pass 1 completed in the
-// previous call; pass-1 quads 0-78 (rows 0-315) on LDS quads 0-78.
-__device__ __forceinline__ void p2_x(const P2Args &a, int b0, int lane, int e, bool ok) {
-  if (!__any(ok)) return;
-  const int b = b0 + lane;
-  const size_t nr = (size_t)a.nrow;
-  const __amdgpu_buffer_rsrc_t rs = p2_rsrc(a.s_mt[1], b0, nr);
-  const int qb = (int)(nr * 16);
-#ifdef HZ_DIAG
-  const uint64_t tq = __builtin_amdgcn_s_memtime();
-#endif
-  {
-    P2QPiece<0, 27> pc;
-    p2_qload(pc, rs, lane, qb);
-    p2_qput<0>(pc, lane);
-  }
-  P2QPiece<27, 53> pc1;
-  p2_qload(pc1, rs, lane, qb);
-  P2_PHASE(32, tq);
-  // steps 2, 3 (rows 0 and 1 of the slot are P2y's: quad 0 gets rows 2, 3)
-  const uint4 q0 = p2_lq(0, lane);
-  const uint32_t first1 = q0.y;
-  uint32_t prev = first1;
-  const uint32_t row2 = p2_step(q0.z, prev, 2);
-  const uint32_t v3 = p2_step(q0.w, prev, 3);
-  uint4 acc = make_uint4(0u, 0u, twist_part(row2, v3), 0u);
-  {  // group 1: row 3's part completes quad 0 (rows 2, 3 only)
-    const uint4 p = p2_lq(1, lane);
-    const uint32_t v4 = p2_step(p.x, prev, 4);
-    const p2u2 h = {acc.z, twist_part(v3, v4)};
-    __builtin_amdgcn_raw_buffer_store_b64(h, rs, lane * 16 + 8, 0, 0);
-    const uint32_t v5 = p2_step(p.y, prev, 5);
-    acc.x = twist_part(v4, v5);
-    const uint32_t v6 = p2_step(p.z, prev, 6);
-    acc.y = twist_part(v5, v6);
-    const uint32_t v7 = p2_step(p.w, prev, 7);
-    acc.z = twist_part(v6, v7);
-  }
-  p2_groups<2, 27, 0, kP2Part>(lane, rs, qb, prev, acc, nullptr);  // parts of rows .. 107
-  p2_qput<0>(pc1, lane);
-  P2QPiece<53, 79> pc2;
-  p2_qload(pc2, rs, lane, qb);
-  p2_groups<27, 53, 0, kP2Part>(lane, rs, qb, prev, acc, nullptr);  // .. 211
-  p2_qput<0>(pc2, lane);
-  p2_groups<53, 56, 0, kP2Part>(lane, rs, qb, prev, acc, nullptr);  // .. 223 (acc: rows 220-222)
-  {  // group 56: row 223's part completes quad 55; row 224 on is final
-    const uint4 p = p2_lq(56, lane);
-    const uint32_t c = prev;
-    const uint32_t v0 = p2_step(p.x, prev, 224);
-    p2_st4(rs, lane, 55 * qb, acc.x, acc.y, acc.z, twist_part(c, v0));
-    const uint32_t v1 = p2_step(p.y, prev, 225), v2 = p2_step(p.z, prev, 226), v3b = p2_step(p.w, prev, 227);
-    p2_st4(rs, lane, 56 * qb, v0, v1, v2, v3b);
-  }
-  p2_groups<57, 78, 0, kP2Final>(lane, rs, qb, prev, acc, nullptr);  // rows 228-311
-  {  // step 312: row 312 (rows 313-315 of quad 78 are P2y's)
-    const uint32_t v = p2_step(p2_lq(78, lane).x, prev, 312);
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 16, __builtin_amdgcn_readfirstlane(78 * qb), 0);
-  }
-  if (ok) {
-    a.ph_w[b] = prev;
-    a.ph_w[nr + b] = first1;
-    a.ph_w[2 * nr + b] = row2;
-    a.s_tag[1][b] = e * 8 + 3;
-  }
-}
-
-// P2y (seed blocks, wave 1): pass-1 quads 78-155 on LDS quads 79-156; final
-// words kept in LDS (the twist reads rows 397-620), progress in *prog
-constexpr int kP2YD = kP2LdsY - 78;
-__device__ __forceinline__ void p2_y(const P2Args &a, int b0, int lane, int e, bool ok, int *prog) {
-  if (!__any(ok)) {
-    p2_publish(prog, kMT + 1);  // (the twist wave's waits end: nothing to twist)
-    return;
-  }
+// P2a (seed blocks, wave 0): the seed blocks' P2a episode, whose pass 1
+// completed in the previous call; P2b (wave 1) the next older; P2c (wave 2,
+// with wave 3's twist) the one before.  Each hands (prev, pass 1's row-1
+// word, row 2's final word) to the next.  Rows 2-223 of the slot are read
+// only by the twist, which needs from each row r only its twist part
+// (rows r and r + 1's words): P2a and P2b store that instead of the final
+// word (one step late, when row r + 1 is known), so the twist is one xor
+// per word with the far row.  (e, ok: the board's episode and whether the
+// stage's input is this episode's, read by every wave of the block before
+// its barrier, so before P2c rewrites its tag.)
+template <int K>  // 0 P2a, 1 P2b, 2 P2c
+__device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int e, bool ok, int *s_prog) {
   const int b = b0 + lane;
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
-  const __amdgpu_buffer_rsrc_t rs = p2_rsrc(a.s_mt[2], b0, nr);
-  const int qb = (int)(nr * 16);
+  if (!__any(ok)) {
+    if (K == 2) p2_publish(s_prog, kMT + 1);  // (the twist wave's waits end: nothing to twist)
+    return;
+  }
+  uint32_t *slot = a.s_mt[2 + K];
 #ifdef HZ_DIAG
   const uint64_t tq = __builtin_amdgcn_s_memtime();
 #endif
+  // the stage's rows in three pieces, P0 staged now; each later piece's
+  // loads issued before the chain runs over the piece before it
+  constexpr int P0 = K == 0 ? 1 : K == 1 ? kP2aEnd : kP2bEnd;
+  constexpr int P1 = K == 0 ? 67 : K == 1 ? 289 : 481;
+  constexpr int P2 = K == 0 ? 139 : K == 1 ? 353 : 553;
+  constexpr int P3 = K == 0 ? kP2aEnd : K == 1 ? kP2bEnd : kMT;
   {
-    P2QPiece<78, 104> pc;
-    p2_qload(pc, rs, lane, qb);
-    p2_qput<kP2YD>(pc, lane);
+    P2Piece<P0, P1> pc;
+    p2_load(pc, slot, nr, b0, lane);
+    p2_put(pc, lane);
   }
-  P2QPiece<104, 130> pc1;
-  p2_qload(pc1, rs, lane, qb);
-  P2_PHASE(33, tq);
-  uint32_t prev = act ? a.ph_r[b] : 0u;
-  const uint32_t first1 = act ? a.ph_r[nr + b] : 0u, row2 = act ? a.ph_r[2 * nr + b] : 0u;
-  uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-  {  // steps 313-315 (row 312 of quad 78 is P2x's)
-    const uint4 p = p2_lq(78 + kP2YD, lane);
-    const p2u3 v = {p2_step(p.y, prev, 313), p2_step(p.z, prev, 314), p2_step(p.w, prev, 315)};
-    __builtin_amdgcn_raw_buffer_store_b96(v, rs, lane * 16 + 4, __builtin_amdgcn_readfirstlane(78 * qb), 0);
+  P2Piece<P1, P2> pc1;
+  p2_load(pc1, slot, nr, b0, lane);
+#ifdef HZ_DIAG
+  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + 32 + K] = __builtin_amdgcn_s_memtime() - tq;  // staged
+#endif
+  uint32_t prev, first1, row2;
+  if (K == 0) {
+    first1 = hz_lds[1 * kLdsStride + lane];
+    prev = first1;
+  } else {
+    const uint32_t *h = K == 1 ? a.p2h_r : a.p3h_r;
+    prev = act ? h[b] : 0u;
+    first1 = act ? h[nr + b] : 0u;
+    row2 = act ? h[2 * nr + b] : 0u;
   }
-  p2_groups<79, 103, kP2YD, kP2Keep>(lane, rs, qb, prev, acc, prog);  // rows 316-411 (an even count of groups)
-  p2_qput<kP2YD>(pc1, lane);
-  P2QPiece<130, 156> pc2;
-  p2_qload(pc2, rs, lane, qb);
-  p2_groups<103, 129, kP2YD, kP2Keep>(lane, rs, qb, prev, acc, prog);  // .. 515
-  p2_qput<kP2YD>(pc2, lane);
-  p2_groups<129, 155, kP2YD, kP2Keep>(lane, rs, qb, prev, acc, prog);  // .. 619
-  {  // rows 620-623
-    const uint4 p = p2_lq(155 + kP2YD, lane);
-    const uint32_t v0 = p2_step(p.x, prev, 620), v1 = p2_step(p.y, prev, 621);
-    const uint32_t v2 = p2_step(p.z, prev, 622), v3 = p2_step(p.w, prev, 623);
-    p2_st4(rs, lane, 155 * qb, v0, v1, v2, v3);
-    p2_lq(155 + kP2YD, lane) = make_uint4(v0, v1, v2, v3);
+  const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
+  const int row_bytes = (int)(nr * 4);
+  P2Piece<P2, P3> pc2;
+  if constexpr (K == 0) {  // step 2: row 2's final word, handed on (row 1's part needs row 1, P2c's last step)
+    row2 = (hz_lds[2 * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 2U;
+    prev = row2;
+    p2_span<3, P1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 2 ..
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Part>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    constexpr int G = P2 + 8 * ((kP2aEnd - P2) / 8);
+    p2_span<P2, G, kP2Part>(lane, rs, row_bytes, prev, s_prog);
+    p2_tail<G, kP2aEnd, kP2Part>(lane, rs, row_bytes, prev);    // .. 207
+  } else if constexpr (K == 1) {
+    static_assert(kAheadTwist + 1 - kP2aEnd == 16, "P2b's part steps: two groups");
+    p2_span<kP2aEnd, kAheadTwist + 1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 208-223
+    __builtin_amdgcn_raw_buffer_store_b32(prev, rs, lane * 4, kAheadTwist * row_bytes, 0);  // row 224's final word
+    p2_span<kAheadTwist + 1, P1, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    p2_span<P2, kP2bEnd, kP2Final>(lane, rs, row_bytes, prev, s_prog);
+  } else {
+    // rows 0 and 1 of the next generation are P2c's own last words: their
+    // far rows (397, 398: P2b's) loaded now, used after the chain
+    const uint32_t f0 = act ? slot[(size_t)397 * nr + b] : 0u, f1 = act ? slot[(size_t)398 * nr + b] : 0u;
+    p2_span<kP2bEnd, P1, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc1, lane);
+    p2_load(pc2, slot, nr, b0, lane);
+    p2_span<P1, P2, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_put(pc2, lane);
+    constexpr int G = P2 + 8 * ((kMT - P2) / 8);
+    p2_span<P2, G, kP2Keep>(lane, rs, row_bytes, prev, s_prog);
+    p2_tail<G, kMT, kP2Keep>(lane, rs, row_bytes, prev);
+    p2_publish(s_prog, kMT);
+    const uint32_t row1 = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
+    // mt[0] = 0x80000000 after init_by_array; row 1's next row is row 2
+    __builtin_amdgcn_raw_buffer_store_b32(f0 ^ twist_part(0x80000000u, row1), rs, lane * 4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(f1 ^ twist_part(row1, row2), rs, lane * 4, row_bytes, 0);
   }
-  p2_publish(prog, kMT);
-  // the last step, at i = 1 (mt[0] = mt[623] = prev); then mt[0] =
-  // 0x80000000 and rows 0, 1 of the next generation: row 1's next row is
-  // row 2, the far rows are 397, 398 (this chain's)
-  const uint32_t row1 = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
-  const uint4 f = p2_lq(99 + kP2YD, lane);  // rows 396-399
-  const p2u2 h = {f.y ^ twist_part(0x80000000u, row1), f.z ^ twist_part(row1, row2)};
-  __builtin_amdgcn_raw_buffer_store_b64(h, rs, lane * 16, 0, 0);
-  if (ok) a.s_tag[2][b] = e * 8 + 5;
+  if (K < 2) {
+    if (ok) {
+      uint32_t *h = K == 0 ? a.p2h_w : a.p3h_w;
+      h[b] = prev;
+      h[nr + b] = first1;
+      h[2 * nr + b] = row2;
+      a.s_tag[2 + K][b] = e * 8 + 3 + K;
+    }
+  } else if (ok) {
+    a.s_tag[4][b] = e * 8 + 5;
+  }
 }
 
-// The twist (seed blocks, wave 2): rows [0, kAheadTwist) of the next
-// generation into P2y's slot (the stream at cursor kMTAhead): row r's new
-// word is the far row r + 397 (P2y's, from LDS) xor row r's twist part,
-// which P2x left in the slot (rows 2-223).  Lane = board, quad q = rows 4 q
-// .. 4 q + 3, whose far rows are the slot's quads q + 99 (rows 4 q + 397 ..
-// 399) and q + 100 (row 4 q + 400), in LDS once P2y has published past them; rows
-// 0 and 1 (from row 1, P2y's last step, and row 2's final word) are P2y's.
-// All its loads precede its stores.
-constexpr int kTwQuads = kAheadTwist / 4;  // 56
+// The twist (seed blocks, wave 3): rows [0, kAheadTwist) of the next
+// generation into P2c's slot (the stream at cursor kMTAhead): row r's new
+// word is the far row r + 397 (P2b's below row 417, from HBM; P2c's from
+// LDS) xor row r's twist part, which P2a and P2b left in the slot (rows
+// 2-223).  Lane: four boards, rows grp + 4 i, grp = lane / 16, so iteration
+// i needs P2c's rows up to 4 i + 400 and follows P2c's progress (s_prog),
+// two iterations per publish of P2c's; rows 0 and 1 (from row 1, P2c's last
+// step, and row 2's final word) are P2c's own.  All its loads precede its
+// stores.  (Before the parts, the wave shuffled each row's
+// successor in from the next lane group and ran at ~350 cycles per
+// iteration, ending ~8 k cycles after P2c: profiles/r04/p2/.)
+constexpr int kTwIters = kAheadTwist / 4;
+constexpr int kTwHbm = (kP2bEnd - 397 + 3) / 4;  // iterations whose rows r + 397 are P2b's (HBM)
 __device__ __forceinline__ uint4 xor4(const uint4 &a, const uint4 &b) {
   return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool any, int *s_prog) {
   if (!any) return;
   const size_t nr = (size_t)a.nrow;
-  const __amdgpu_buffer_rsrc_t rs = p2_rsrc(a.s_mt[2], b0, nr);
-  const int qb = (int)(nr * 16);
+  uint32_t *slot = a.s_mt[4];
+  const int grp = lane >> 4, c4 = (lane & 15) * 4;
+  uint32_t *col = slot + b0 + c4;
+  auto row = [&](int r) { return *reinterpret_cast<const uint4 *>(col + (size_t)r * nr); };
+  auto store = [&](int r, const uint4 &v) { *reinterpret_cast<uint4 *>(col + (size_t)r * nr) = v; };
 #ifdef HZ_DIAG
   const int b = b0 + lane;
   const uint64_t tz = __builtin_amdgcn_s_memtime();
 #endif
-  // (the wave has slack: its loads wait until P2y is 64 rows in, out of the
-  // launch's opening burst, where every other stage's inputs arrive)
-  int have = p2_wait(s_prog, kP2xEnd + 64, a.spin, a.err);
+  // (the wave has ~16 k cycles of slack: its 4 MB of loads wait until P2c is
+  // 64 rows in, out of the launch's opening burst, where every other
+  // stage's inputs arrive)
+  int have = p2_wait(s_prog, kP2bEnd + 64, a.spin, a.err);
   P2_PHASE(35, tz);
-  uint4 pt[kTwQuads];
+  uint4 pt[kTwIters], fh[kTwHbm];
 #pragma unroll
-  for (int q = 0; q < kTwQuads; q++) pt[q] = p2_ld4(rs, lane, q * qb);
-  uint4 A = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = 0; i < kTwIters; i++) {
+    const int r = grp + 4 * i;
+    pt[i] = r >= 2 ? row(r) : make_uint4(0, 0, 0, 0);
+  }
 #pragma unroll
-  for (int q = 0; q < kTwQuads; q += 2) {
-    const int need = 4 * (q + 1) + 401;  // the pair's far rows final (below need)
-    if (have < need) have = p2_wait(s_prog, need, a.spin, a.err);
-    if (q == 0) A = p2_lq(99 + kP2YD, lane);
-    const uint4 B = p2_lq(q + 100 + kP2YD, lane), C = p2_lq(q + 101 + kP2YD, lane);
-    const uint4 o0 = xor4(make_uint4(A.y, A.z, A.w, B.x), pt[q]);
-    const uint4 o1 = xor4(make_uint4(B.y, B.z, B.w, C.x), pt[q + 1]);
-    if (q == 0) {
-      const p2u2 h = {o0.z, o0.w};
-      __builtin_amdgcn_raw_buffer_store_b64(h, rs, lane * 16 + 8, 0, 0);
-    } else {
-      p2_st4(rs, lane, q * qb, o0.x, o0.y, o0.z, o0.w);
-    }
-    p2_st4(rs, lane, (q + 1) * qb, o1.x, o1.y, o1.z, o1.w);
-    if (q == 0) P2_PHASE(36, tz);
-    A = C;
+  for (int i = 0; i < kTwHbm; i++) {
+    const int r = grp + 4 * i + 397;
+    fh[i] = r < kP2bEnd ? row(r) : make_uint4(0, 0, 0, 0);
+  }
+  auto far = [&](int i) -> uint4 {
+    const int r = grp + 4 * i;
+    if (i < kTwHbm && r + 397 < kP2bEnd) return fh[i < kTwHbm ? i : 0];
+    const uint32_t *d = hz_lds + (r + 397) * kLdsStride + c4;
+    return make_uint4(d[0], d[1], d[2], d[3]);
+  };
+#pragma unroll
+  for (int i = 0; i < kTwIters; i += 2) {
+    const int need = 4 * (i + 1) + 3 + 397 + 1;  // the pair's far rows final
+    if (need > kP2bEnd && have < need) have = p2_wait(s_prog, need, a.spin, a.err);
+    const uint4 f0 = far(i), f1 = far(i + 1);
+    if (i > 0 || grp >= 2) store(grp + 4 * i, xor4(f0, pt[i]));
+    store(grp + 4 * (i + 1), xor4(f1, pt[i + 1]));
+    if (i == 0) P2_PHASE(36, tz);
   }
   P2_PHASE(37, tz);
   // (rows 224..623 keep pass 2's words: the current generation's tail)
 }
 
-// seed blocks: wave 0 P2x, wave 1 P2y, wave 2 the twist of P2y's episode,
-// wave 3 P1
+// seed blocks: waves 0-2 P2a, P2b, P2c; wave 3 the twist of P2c's episode
 __device__ __forceinline__ void p2_seed(const P2Args &a, int blk) {
   __shared__ int s_prog;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int b0 = blk * kBlock, b = b0 + lane;
   const bool act = b < a.n;
   if (tid == 0) s_prog = 0;
-  // each pass-2 stage's episode and decision (and P2y's for the twist
-  // wave), read before the barrier, so before any wave rewrites a tag
-  const int k = w == 0 ? 1 : 2;
-  const int e = act ? a.ep_in[b] + kP2Last - k : 0;
-  const bool ok = act && a.s_tag[k][b] == e * 8 + (k == 1 ? 2 : 3);
+  // each stage's episode and decision (and P2c's for the twist wave), read
+  // before the barrier, so before any wave rewrites a tag
+  const int k = w < 3 ? w : 2;
+  const int e = act ? a.ep_in[b] + kP2Last - 2 - k : 0;
+  const bool ok = act && a.s_tag[2 + k][b] == e * 8 + 2 + k;
   __syncthreads();
-  if (w == 0) p2_x(a, b0, lane, e, ok);
-  else if (w == 1) p2_y(a, b0, lane, e, ok, &s_prog);
-  else if (w == 2) p2_twist(a, b0, lane, __any(ok), &s_prog);
-  else if (act) p2_p1(a, b0, lane);
+  if (w == 0) p2_third<0>(a, b0, lane, e, ok, &s_prog);
+  else if (w == 1) p2_third<1>(a, b0, lane, e, ok, &s_prog);
+  else if (w == 2) p2_third<2>(a, b0, lane, e, ok, &s_prog);
+  else p2_twist(a, b0, lane, __any(ok), &s_prog);
 }
 
-// a draw stage d (stage kP2FirstDraw + d): draws [d0, d1) of its episode on
-// its stream slot, from an LDS window (at `base`) of kP2Win rows starting at
-// the wave's lowest start cursor (the wave's 64 boards' quads, staged
-// here); `in` (d > 0) holds the draws so far, `out` gets them plus these;
-// the cursors go to the slot's cursor table
+// a draw stage: draws [d0, d1) of episode e on its stream slot, from an LDS
+// window (at `base`) of kP2Win rows starting at the wave's lowest start
+// cursor (the wave's 64 boards, staged here); `in` (stage > 0) holds the
+// draws so far, `out` gets them plus these; the cursors go to the slot's
+// cursor table
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
   return v;
 }
-__device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane, int d, int base) {
+__device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane, int stage, int base) {
   const int b = b0 + lane;
 #ifdef HZ_DIAG
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
-  const int s = kP2FirstDraw + d;
-  const int d0 = p2_draw_cut(d), d1 = d == kP2Draw - 1 ? a.draws : min(a.draws, p2_draw_cut(d + 1));
-  const int e = act ? a.ep_in[b] + kP2Last - s : 0;
-  uint32_t *slot = a.s_mt[s];
-  int32_t *cur = a.s_cur[s] + b;
-  const P2Draw &in = a.x_r[d > 0 ? d - 1 : 0];
-  const P2Draw &out = d == kP2Draw - 1 ? a.pl_w : a.x_w[d];
-  bool ok = act && a.s_tag[s][b] == e * 8 + 5;
+  const int d0 = kP2DrawsPer * stage, d1 = stage == 3 ? a.draws : min(a.draws, d0 + kP2DrawsPer);
+  const int e = act ? a.ep_in[b] + kP2Last - 5 - stage : 0;
+  const uint32_t *slot = a.s_mt[5 + stage];
+  int32_t *cur = a.s_cur[5 + stage] + b;
+  const P2Draw &in = a.x_r[stage > 0 ? stage - 1 : 0];
+  const P2Draw &out = stage == 3 ? a.pl_w : a.x_w[stage];
+  bool ok = act && a.s_tag[5 + stage][b] == e * 8 + 5;
   int k0 = 0, c0 = kMTAhead;
   uint64_t bag = initial_bag(), q[kAheadWords] = {0, 0, 0, 0};
-  if (d > 0 && act) {  // (one round trip: used only if the tag matches)
+  if (stage > 0 && act) {  // (one round trip: used only if the tag matches)
     const int itag = in.tag[b];
     k0 = in.k[b];
     c0 = in.c[b];
     bag = in.bag[b];
 #pragma unroll
     for (int i = 0; i < kAheadWords; i++) q[i] = in.q[(size_t)i * nr + b];
-    ok = ok && itag == e * 8 + d;
+    ok = ok && itag == e * 8 + stage;
   }
   const bool draws = ok && k0 >= d0 && d0 < d1;
   const int r0 = wave_min_i(draws ? (c0 & 0xFFFF) : kAheadTwist) & ~3;
-  if (r0 < kAheadTwist) {  // the window: rows [r0, r0 + kP2Win), each lane its board's quads, all in flight
+  if (r0 < kAheadTwist) {  // the window: rows [r0, r0 + kP2Win), 16-B loads (four boards of a row per lane), all in flight
     constexpr int U = kP2Win / 4;
-    const __amdgpu_buffer_rsrc_t rs = p2_rsrc(slot, b0, nr);
-    const int qb = (int)(nr * 16), q0 = r0 >> 2;
+    const int c4 = (lane & 15) * 4;
     uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) v[u] = p2_ld4(rs, lane, (q0 + u) * qb);
+    for (int u = 0; u < U; u++) {
+      const int r = r0 + 4 * u + (lane >> 4);
+      v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      uint32_t *dd = hz_lds + base + 4 * u * kLdsStride + lane;
+      uint32_t *dd = hz_lds + base + (4 * u + (lane >> 4)) * kLdsStride + c4;
       dd[0] = v[u].x;
-      dd[kLdsStride] = v[u].y;
-      dd[2 * kLdsStride] = v[u].z;
-      dd[3 * kLdsStride] = v[u].w;
+      dd[1] = v[u].y;
+      dd[2] = v[u].z;
+      dd[3] = v[u].w;
     }
   }
-  P2_PHASE(27 + d, t0);  // window staged
+  P2_PHASE(28 + stage, t0);  // window staged
   if (!act) return;
   if (!ok) {
     out.tag[b] = -1;
     return;
   }
-  if (d == 0) cur[0] = kMTAhead;
+  if (stage == 0) cur[0] = kMTAhead;
   int k = k0, cc = c0;
   if (draws) {  // every earlier draw is done: continue in the window
     const int lim = min(r0 + kP2Win, kAheadTwist);
-    StreamDraw<WinMT> dr{WinMT(base - r0 * kLdsStride + lane, c0, lim)};
+    StreamDraw<WinMT> d{WinMT(base - r0 * kLdsStride + lane, c0, lim)};
 #pragma unroll 1
     for (int i = d0; i < d1; i++) {
-      if (dr.m.pos >= lim) break;
-      const uint32_t p9 = dr(bag);
+      if (d.m.pos >= lim) break;
+      const uint32_t p9 = d(bag);
       // a draw that consumed words past the window is discarded: the next
       // stage (or a play stage, from the stream slot) redoes it from the
       // last cursor kept
-      if (dr.m.pos > lim) break;
+      if (d.m.pos > lim) break;
       apply_pile_fast(bag, p9);
       const int bit = 9 * i, wd = bit >> 6, off = bit & 63;
       const uint64_t lo9 = (uint64_t)p9 << off, hi9 = off > 55 ? (uint64_t)p9 >> (64 - off) : 0ull;
@@ -1827,7 +1841,7 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
       q[1] |= wd == 1 ? lo9 : wd == 0 ? hi9 : 0ull;
       q[2] |= wd == 2 ? lo9 : wd == 1 ? hi9 : 0ull;
       q[3] |= wd == 3 ? lo9 : wd == 2 ? hi9 : 0ull;
-      cc = dr.m.cursor();
+      cc = d.m.cursor();
       cur[(size_t)(i + 1) * nr] = cc;
       k = i + 1;
     }
@@ -1837,18 +1851,34 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
   out.bag[b] = bag;
 #pragma unroll
   for (int i = 0; i < kAheadWords; i++) out.q[(size_t)i * nr + b] = q[i];
-  out.tag[b] = e * 8 + d + 1;
+  out.tag[b] = e * 8 + stage + 1;
 }
 
-// the rule hashes of D5's episode (read by the play stages in the next
+// the rule hashes of D4's episode (read by the play stages in the next
 // kP2Play calls)
 __device__ __forceinline__ void p2_hashes(const P2Args &a, int b) {
   const size_t nr = (size_t)a.nrow;
-  const int e = a.ep_in[b] + kP2Last - (kP2FirstPlay - 1);
+  const int e = a.ep_in[b] + kP2Last - 8;
   const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
 #pragma unroll 1
   for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
   a.ht_w[b] = e;
+}
+
+// draw-X blocks: D1 (wave 0), D2 (wave 1), P1b (wave 2), the rule hashes
+// (wave 3); draw-Y blocks: D3, D4 (waves 0, 1), P1a (wave 2).  Each draw
+// wave stages its own window and reads only it.
+__device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b0 = blk * kBlock;
+  if (w < 2) {
+    p2_draw_stage(a, b0, lane, 2 * y + w, w * kP2WinRows * kLdsStride);
+  } else if (w == 2 && b0 + lane < a.n) {
+    if (y) p2_p1a(a, b0, lane);
+    else p2_p1b(a, b0, lane);
+  } else if (w == 3 && !y && b0 + lane < a.n) {
+    p2_hashes(a, b0 + lane);
+  }
 }
 
 // a play stage's state after its plies, for the next play stage
@@ -1868,10 +1898,9 @@ __device__ __forceinline__ void p2_mid_put(const P2Mid &m, size_t nr, int b, con
   m.tag[b] = e;
 }
 // the previous play stage's state; the draw source continues its script
-// (nd entries, cursors in `cur`) or the slot stream it fell onto (sw: the
-// board's quads in the slot, quad stride s4)
+// (nd entries, cursors in `cur`) or the slot stream it fell onto
 __device__ __forceinline__ PlayDraw2 p2_mid_get(const P2Mid &m, size_t nr, int b, State &s, int &g, int nd,
-                                               uint32_t *sw, int s4, const int32_t *cur) {
+                                               uint32_t *slot, const int32_t *cur) {
 #pragma unroll
   for (int k = 0; k < 4; k++) s.pl[k] = m.st[(size_t)k * nr + b];
   s.piles = m.st[4 * nr + b];
@@ -1879,105 +1908,14 @@ __device__ __forceinline__ PlayDraw2 p2_mid_get(const P2Mid &m, size_t nr, int b
   const int d = m.i[b], fc = m.i[2 * nr + b];
   g = m.i[nr + b];
   return PlayDraw2{m.q[b], m.q[nr + b], m.q[2 * nr + b], m.q[3 * nr + b], d, nd, fc >= 0,
-                   MTQ(sw, s4, fc >= 0 ? fc : 0), cur + (size_t)nd * nr};
+                   MTR(slot, (int)nr, fc >= 0 ? fc : 0), cur + (size_t)nd * nr};
 }
 
-// play stage st (stage kP2FirstPlay + st) of the lane's board: its plies of
-// episode ep + kP2Play - 1 - st (the last stage: the rest of episode ep, or
-// all of it); returns whether the board's stream ended in LDS (the last
-// stage's unprepared fallback)
-__device__ __forceinline__ bool p2_play_stage(const P2Args &a, int b0, int lane, int st) {
-  const int b = b0 + lane;
-  if (b >= a.n) return false;
-  const size_t nr = (size_t)a.nrow;
-#ifdef HZ_DIAG
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
-  const bool last = st == kP2Play - 1;
-  const int s = kP2FirstPlay + st;
-  const int e = last ? a.episode[b] : a.ep_in[b] + kP2Last - s;
-  const P2Draw &pl = a.pl_r[st];
-  const uint32_t *hsrc = a.h_r[st];
-  const int32_t *htag = a.ht_r[st];
-  uint32_t *sw = a.s_mt[s] + 4 * (size_t)b;
-  const int s4 = (int)(4 * nr);
-  const int32_t *cur = a.s_cur[s] + b;
-  const int g_end = last ? a.max_plies : min(a.cut[st], a.max_plies);
-  const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
-  // every input's loads issued together (used only if the tags match)
-  const int ptag = pl.tag[b], nd = pl.k[b];
-  const int mtag = st > 0 ? a.m_r[st - 1].tag[b] : e;
-  const uint32_t *hs = htag[b] == e ? hsrc + b : nullptr;
-  State s0;
-  int g = 0;
-  PlayDraw2 draw = st == 0 ? PlayDraw2{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
-                                       MTQ(sw, s4, 0), cur + (size_t)nd * nr}
-                           : p2_mid_get(a.m_r[st - 1], nr, b, s0, g, nd, sw, s4, cur);
-  const bool prep = ptag == e * 8 + kP2Draw && mtag == e;
-  if (prep) {
-    if (st == 0) {
-      if (__all(nd >= 5)) draw.scripted_reset(s0);
-      else reset_state(s0, draw);
-    }
-    P2_PHASE(16 + 2 * st, t0);
-    g += p2_plies(s0, draw, g, g_end, rk, hs, nr);
-    P2_PHASE(17 + 2 * st, t0);
-  }
-  if (!last) {
-    const P2Mid &mo = a.m_w[st];
-    if (prep) p2_mid_put(mo, nr, b, s0, draw, g, e);
-    else mo.tag[b] = -1;
-    return false;
-  }
-  int cursor, src;
-  bool lds_used = false;
-  if (prep) {
-    cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
-    src = 2 + a.s_idx_last;
-  } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
-    mt_seed(hz_lds + lane, kLdsStride, sd);
-    PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
-    reset_state(s0, fb);
-    g = p2_plies(s0, fb, 0, a.max_plies, rk, nullptr, nr);
-    cursor = fb.m.cursor();
-    src = -1;
-    lds_used = true;
-  }
-  a.episode[b] = e + 1;
-  if (score_pending(s0.misc)) finish_game(s0);
-  P2_PHASE(26, t0);
-  store_state(a.st, a.n, b, s0);
-  a.pos[b] = cursor;
-  a.mt_src[b] = src;
-  a.ply[b] = g;
-  a.seed[b] = sd;
-  a.ep_out[b] = e + 1;
-  // the game this call completes, as hz_play's other pipeline counts it
-  if (a.games_done) a.games_done[b] = phase_of(s0.misc) == PH_OVER ? 1 : 0;
-  if (a.steps_done) a.steps_done[b] = g;
-  return lds_used;
-}
-
-// draw-X blocks: D1, D2, D3 (waves 0-2), the rule hashes (wave 3); draw-Y
-// blocks: D4, D5 (waves 0, 1), play0 (wave 2).  Each draw wave stages its
-// own window and reads only it.
-__device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b0 = blk * kBlock;
-  if (!y) {
-    if (w < 3) p2_draw_stage(a, b0, lane, w, w * kP2WinRows * kLdsStride);
-    else if (b0 + lane < a.n) p2_hashes(a, b0 + lane);
-  } else {
-    if (w < 2) p2_draw_stage(a, b0, lane, 3 + w, w * kP2WinRows * kLdsStride);
-    else if (w == 2) p2_play_stage(a, b0, lane, 0);
-  }
-}
-
-// play blocks: wave 3 - w runs play stage kP2Play - 1 - w (wave 0 the last:
-// the rest of episode ep, or all of it).  The stages run one code path (st
-// wave-uniform), so the block's four waves share one copy of the ply loop
-// in the instruction cache (one inlined copy per stage, ~50 KB each,
-// thrashed the cache the two CUs of a pair share).
+// play blocks: wave 3 - st runs play stage st on episode ep + kP2Play - 1 -
+// st (the last stage, wave 0: the rest of episode ep, or all of it).  The
+// stages run one code path (st wave-uniform), so the block's four waves
+// share one copy of the ply loop in the instruction cache (one inlined copy
+// per stage, ~50 KB each, thrashed the cache the two CUs of a pair share).
 __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
   __shared__ uint64_t s_lds_mask;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1985,14 +1923,76 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
   const bool act = b < a.n;
   const uint64_t actmask = __ballot(act);
   const int nb = a.n - b0 < kBlock ? a.n - b0 : kBlock;
+  const size_t nr = (size_t)a.nrow;
 #ifdef HZ_DIAG
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-  const int st = __builtin_amdgcn_readfirstlane(kP2Play - 1 - w);
-  const bool lds_used = p2_play_stage(a, b0, lane, st);
+  const int st = __builtin_amdgcn_readfirstlane(kP2Play - 1 - w);  // 0 playA .. kP2Play - 1 the last
+  const bool last = st == kP2Play - 1;
+  bool lds_used = false;
+  if (act) {
+    const int e = last ? a.episode[b] : a.ep_in[b] + kP2Play - 1 - st;
+    const P2Draw &pl = a.pl_r[st];
+    const uint32_t *hsrc = a.h_r[st];
+    const int32_t *htag = a.ht_r[st];
+    uint32_t *slot = a.s_mt[9 + st] + b;
+    const int32_t *cur = a.s_cur[9 + st] + b;
+    const int g_end = last ? a.max_plies : min(a.cut[st], a.max_plies);
+    const uint64_t sd = episode_seed(a.seed_base, b, e), rk = rule_key(sd);
+    // every input's loads issued together (used only if the tags match)
+    const int ptag = pl.tag[b], nd = pl.k[b];
+    const int mtag = st > 0 ? a.m_r[st - 1].tag[b] : e;
+    const uint32_t *hs = htag[b] == e ? hsrc + b : nullptr;
+    State s;
+    int g = 0;
+    PlayDraw2 draw = st == 0 ? PlayDraw2{pl.q[b], pl.q[nr + b], pl.q[2 * nr + b], pl.q[3 * nr + b], 0, nd, false,
+                                         MTR(slot, (int)nr, 0), cur + (size_t)nd * nr}
+                             : p2_mid_get(a.m_r[st - 1], nr, b, s, g, nd, slot, cur);
+    const bool prep = ptag == e * 8 + 4 && mtag == e;
+    if (prep) {
+      if (st == 0) {
+        if (__all(nd >= 5)) draw.scripted_reset(s);
+        else reset_state(s, draw);
+      }
+      P2_PHASE(16 + 3 * st, t0);
+      g += p2_plies(s, draw, g, g_end, rk, hs, nr);
+      P2_PHASE(17 + 3 * st, t0);
+    }
+    if (!last) {
+      const P2Mid &mo = a.m_w[st];
+      if (prep) p2_mid_put(mo, nr, b, s, draw, g, e);
+      else mo.tag[b] = -1;
+    } else {
+      int cursor, src;
+      if (prep) {
+        cursor = draw.fell ? draw.gm.cursor() : cur[(size_t)draw.d * nr];
+        src = 2 + a.s_idx_last;
+      } else {  // unprepared: the whole game, the stream seeded and drawn in LDS
+        mt_seed(hz_lds + lane, kLdsStride, sd);
+        PlayDraw fb{LdsMT(lane, kMTSeeded), false, false, 0, 0, 0, 0, 0, 0, MT(nullptr, 0), nullptr};
+        reset_state(s, fb);
+        g = p2_plies(s, fb, 0, a.max_plies, rk, nullptr, nr);
+        cursor = fb.m.cursor();
+        src = -1;
+        lds_used = true;
+      }
+      a.episode[b] = e + 1;
+      if (score_pending(s.misc)) finish_game(s);
+      P2_PHASE(27, t0);
+      store_state(a.st, a.n, b, s);
+      a.pos[b] = cursor;
+      a.mt_src[b] = src;
+      a.ply[b] = g;
+      a.seed[b] = sd;
+      a.ep_out[b] = e + 1;
+      // the game this call completes, as hz_play's other pipeline counts it
+      if (a.games_done) a.games_done[b] = phase_of(s.misc) == PH_OVER ? 1 : 0;
+      if (a.steps_done) a.steps_done[b] = g;
+    }
 #ifdef HZ_DIAG
-  if (g_stamps && act) g_stamps[(size_t)b * kP2Stamps + w] = __builtin_amdgcn_s_memtime() - t0;  // play4 .. play1
+    if (g_stamps) g_stamps[(size_t)b * kP2Stamps + w] = __builtin_amdgcn_s_memtime() - t0;  // last .. playA
 #endif
+  }
   if (w == 0) {
     const uint64_t lm = __ballot(lds_used);
     if (lane == 0) s_lds_mask = lm;
@@ -2003,7 +2003,7 @@ __device__ __forceinline__ void p2_play(const P2Args &a, int blk) {
 }
 
 // one 162 KB-LDS block per CU, so one wave per SIMD: every wave may use the
-// whole register file (the twist wave keeps 56 quads in registers)
+// whole register file (the P2b twist wave keeps 57 rows in registers)
 __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) k_play2(P2Args a, int nblk) {
   const int blk = (int)blockIdx.x;
   const int role = blk / nblk;  // 0 play, 1 draw X, 2 draw Y, 3 seed blocks
@@ -2016,9 +2016,9 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
   else if (role == 3) p2_seed(a, rb);
   else p2_draw(a, rb, role - 1);
 #ifdef HZ_DIAG
-  {  // wave durations per board, slot 4 role + wave: 0-3 play (play4 .. play1:
-     // stamped in p2_play, before its barrier), 4-7 draw X (D1, D2, D3,
-     // hashes), 8-10 draw Y (D4, D5, play0), 12-15 seed (P2x, P2y, twist, P1)
+  {  // wave durations per board, slot 4 role + wave: 0-3 play (D, C, B, A:
+     // stamped in p2_play, before its barrier), 4-7 draw X (D1, D2, P1b,
+     // hashes), 8-10 draw Y (D3, D4, P1a), 12-15 seed (P2a, P2b, P2c, twist)
     const int w = threadIdx.x >> 6, bb = rb * kBlock + (threadIdx.x & 63);
     const bool idle = role == 2 && w == 3;
     if (g_stamps && role > 0 && !idle && bb < a.n) g_stamps[(size_t)bb * kP2Stamps + 4 * role + w] = __builtin_amdgcn_s_memtime() - t0;
@@ -2027,7 +2027,7 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
 }
 
 // boards whose stream lives in a pipeline-2 slot (mt_src = 2 + slot): the
-// slot's quads of the board into the board's own stream, one wave per board
+// slot's column (word-major) into the board's own stream, one wave per board
 struct P2Slots {
   uint32_t *s[kP2Stream];
 };
@@ -2036,11 +2036,11 @@ __global__ void __launch_bounds__(64) k_mt_materialize2(uint32_t *__restrict__ m
   const int b = blockIdx.x, lane = threadIdx.x;
   const int src = mt_src[b];
   if (src < 2 || src >= 2 + kP2Stream) return;
-  const QuadPtr from{slots.s[src - 2] + 4 * (size_t)b, (int)(4 * nrow)};
+  const uint32_t *from = slots.s[src - 2] + b;
   uint32_t *to = mt + (size_t)b * kMT;
   uint32_t v[(kMT + 63) / 64];
 #pragma unroll
-  for (int k = 0; k < (kMT + 63) / 64; k++) v[k] = lane + 64 * k < kMT ? from[lane + 64 * k] : 0u;
+  for (int k = 0; k < (kMT + 63) / 64; k++) v[k] = lane + 64 * k < kMT ? from[(size_t)(lane + 64 * k) * nrow] : 0u;
 #pragma unroll
   for (int k = 0; k < (kMT + 63) / 64; k++)
     if (lane + 64 * k < kMT) to[lane + 64 * k] = v[k];
@@ -2165,12 +2165,6 @@ static int materialize(hz_env *e) {
 
 // ---------------------------------------------------------- pipeline 2 host
 static_assert(sizeof(((hz_env *)0)->p2_s) / sizeof(uint32_t *) == kP2Stream, "slot ring");
-static_assert(sizeof(((hz_env *)0)->p2_pl) / sizeof(P2Draw) == kP2Ring && sizeof(((hz_env *)0)->p2_h) / sizeof(uint32_t *) == kP2Ring,
-              "script and hash rings");
-static_assert(sizeof(((hz_env *)0)->p2_x) / sizeof(P2Draw) == 2 * (kP2Draw - 1) &&
-                  sizeof(((hz_env *)0)->p2_m) / sizeof(P2Mid) == 2 * (kP2Play - 1) &&
-                  sizeof(((hz_env *)0)->p2_cut) / sizeof(int) == kP2Play - 1,
-              "hand-off rings");
 static void free_p2(hz_env *e) {
   auto f = [](auto *&p) {
     if (p) (void)hipFree((void *)p);
@@ -2188,7 +2182,7 @@ static void free_p2(hz_env *e) {
     f(d.bag);
     f(d.c);
   };
-  for (int k = 0; k < kP2Draw - 1; k++) fd(e->p2_x[k][0]), fd(e->p2_x[k][1]);
+  for (int k = 0; k < 3; k++) fd(e->p2_x[k][0]), fd(e->p2_x[k][1]);
   for (int k = 0; k < kP2Ring; k++) fd(e->p2_pl[k]);
   for (int k = 0; k < kP2Play - 1; k++)
     for (int j = 0; j < 2; j++) {
@@ -2203,7 +2197,9 @@ static void free_p2(hz_env *e) {
     f(e->p2_h_tag[k]);
   }
   for (int k = 0; k < 2; k++) {
-    f(e->p2_ph[k]);
+    f(e->p2_p1h[k]);
+    f(e->p2_p2h[k]);
+    f(e->p2_p3h[k]);
     f(e->p2_ep[k]);
   }
 }
@@ -2216,7 +2212,7 @@ static int p2_clear_tags(hz_env *e) {
   auto c = [&](int32_t *t) { return hipMemsetAsync(t, 0xff, bytes, e->stream) != hipSuccess; };
   for (int k = 0; k < kP2Stream; k++)
     if (c(e->p2_s_tag[k])) return 1;
-  for (int k = 0; k < kP2Draw - 1; k++)
+  for (int k = 0; k < 3; k++)
     if (c(e->p2_x[k][0].tag) || c(e->p2_x[k][1].tag)) return 1;
   for (int k = 0; k < kP2Ring; k++)
     if (c(e->p2_pl[k].tag) || c(e->p2_h_tag[k])) return 1;
@@ -2239,7 +2235,7 @@ static int alloc_p2(hz_env *e) {
     return m(&d.tag, nr * 4) && m(&d.k, nr * 4) && m(&d.q, kAheadWords * nr * 8) && m(&d.bag, nr * 8) &&
            m(&d.c, nr * 4);
   };
-  for (int k = 0; ok && k < kP2Draw - 1; k++) ok = md(e->p2_x[k][0]) && md(e->p2_x[k][1]);
+  for (int k = 0; ok && k < 3; k++) ok = md(e->p2_x[k][0]) && md(e->p2_x[k][1]);
   for (int k = 0; ok && k < kP2Ring; k++)
     ok = md(e->p2_pl[k]) && m(&e->p2_h[k], kRulePlies * nr * 4) && m(&e->p2_h_tag[k], nr * 4);
   for (int k = 0; ok && k < kP2Play - 1; k++)
@@ -2248,7 +2244,7 @@ static int alloc_p2(hz_env *e) {
       ok = m(&mm.tag, nr * 4) && m(&mm.st, 6 * nr * 8) && m(&mm.q, 4 * nr * 8) && m(&mm.i, 3 * nr * 4);
     }
   for (int k = 0; ok && k < 2; k++)
-    ok = m(&e->p2_ph[k], 3 * nr * 4) &&
+    ok = m(&e->p2_p1h[k], nr * 4) && m(&e->p2_p2h[k], 3 * nr * 4) && m(&e->p2_p3h[k], 3 * nr * 4) &&
          m(&e->p2_ep[k], nr * 4);
   if (!ok || p2_clear_tags(e)) {
     free_p2(e);
@@ -2299,9 +2295,13 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
     a.s_cur[s] = e->p2_s_cur[sl(s)];
   }
   a.s_idx_last = sl(kP2Last);
-  a.ph_w = e->p2_ph[r];
-  a.ph_r = e->p2_ph[w];
-  for (int k = 0; k < kP2Draw - 1; k++) {
+  a.p1h_w = e->p2_p1h[r];
+  a.p1h_r = e->p2_p1h[w];
+  a.p2h_w = e->p2_p2h[r];
+  a.p2h_r = e->p2_p2h[w];
+  a.p3h_w = e->p2_p3h[r];
+  a.p3h_r = e->p2_p3h[w];
+  for (int k = 0; k < 3; k++) {
     a.x_w[k] = e->p2_x[k][r];
     a.x_r[k] = e->p2_x[k][w];
   }
@@ -2394,18 +2394,17 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   {  // hz_play's pipeline: 2 by default, HZ_PIPELINE=1 for the first (hz_env_set_pipeline)
     const char *pv = getenv("HZ_PIPELINE");
     e->pipeline = pv && atoi(pv) == 1 ? 1 : 2;
-    // HZ_P2_CUTS="a,b,c,d": pipeline 2's play stage boundaries (plies,
+    // HZ_P2_CUTS="a,b,c": pipeline 2's play stage boundaries (plies,
     // increasing multiples of 4: whole turns; a stage that starts at player
     // 1's turn plays single plies up to the next turn pair)
-    e->p2_cut[0] = 20;
-    e->p2_cut[1] = 32;
-    e->p2_cut[2] = 44;
-    e->p2_cut[3] = 56;
+    e->p2_cut[0] = 24;
+    e->p2_cut[1] = 40;
+    e->p2_cut[2] = 56;
     const char *cv = getenv("HZ_P2_CUTS");
-    int c[4];
-    if (cv && sscanf(cv, "%d,%d,%d,%d", &c[0], &c[1], &c[2], &c[3]) == 4 && c[0] > 0 && c[1] > c[0] && c[2] > c[1] &&
-        c[3] > c[2] && c[0] % 4 == 0 && c[1] % 4 == 0 && c[2] % 4 == 0 && c[3] % 4 == 0)
-      for (int k = 0; k < 4; k++) e->p2_cut[k] = c[k];
+    int c[3];
+    if (cv && sscanf(cv, "%d,%d,%d", &c[0], &c[1], &c[2]) == 3 && c[0] > 0 && c[1] > c[0] && c[2] > c[1] &&
+        c[0] % 4 == 0 && c[1] % 4 == 0 && c[2] % 4 == 0)
+      for (int k = 0; k < 3; k++) e->p2_cut[k] = c[k];
   }
   ok = ok && hipMalloc(&e->wait_err_own, sizeof(int32_t)) == hipSuccess &&
        hipMemset(e->wait_err_own, 0, sizeof(int32_t)) == hipSuccess;

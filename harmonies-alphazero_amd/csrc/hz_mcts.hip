@@ -1297,9 +1297,17 @@ int hz_mcts_gather_leaves(hz_mcts *m, float *board, float *glob, int32_t *rows, 
   return launch_err();
 }
 
-// boards per workgroup of the gathering expand launch (one atomic add per workgroup)
+// boards per workgroup of the gathering expand launch (one atomic add per
+// workgroup): 16 by default, HZ_GATHER_BPW=8 (A/B: two workgroups per CU)
 constexpr int kGatherBPW = 16;
 static_assert(kGatherBPW * sizeof(ExpandLds) <= 160 * 1024, "the workgroup's records fit the LDS");
+static int gather_bpw() {
+  static const int v = [] {
+    const char *e = getenv("HZ_GATHER_BPW");
+    return e && atoi(e) == 8 ? 8 : kGatherBPW;
+  }();
+  return v;
+}
 
 static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const float *value, const double *noise,
                          double eps, int32_t testing, const int32_t *slot, bool sel = false,
@@ -1327,11 +1335,13 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
                      board, glob, rows, count_out, count_prev, add_prev)
   const bool gat = sel && count_out;
   if (waves == 4) {
-    if (gat) HZ_EXPAND_LAUNCH(4, true, true, kGatherBPW);
+    if (gat && gather_bpw() == 8) HZ_EXPAND_LAUNCH(4, true, true, 8);
+    else if (gat) HZ_EXPAND_LAUNCH(4, true, true, kGatherBPW);
     else if (sel) HZ_EXPAND_LAUNCH(4, true, false, 1);
     else HZ_EXPAND_LAUNCH(4, false, false, 1);
   } else {
-    if (gat) HZ_EXPAND_LAUNCH(3, true, true, kGatherBPW);
+    if (gat && gather_bpw() == 8) HZ_EXPAND_LAUNCH(3, true, true, 8);
+    else if (gat) HZ_EXPAND_LAUNCH(3, true, true, kGatherBPW);
     else if (sel) HZ_EXPAND_LAUNCH(3, true, false, 1);
     else HZ_EXPAND_LAUNCH(3, false, false, 1);
   }

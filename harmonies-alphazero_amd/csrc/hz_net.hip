@@ -1467,14 +1467,18 @@ static bool x6_block() {
   return v == 1;
 }
 
-// the fused block's row table: 0 round 3's kX6ClassRowBlk, 1 the
-// bank-conflict-free kX6ClassRow (HZ_BLK_TABLE, hz_resblock_x6_set_table)
+// the fused block's row table: 1 (the default since round 5) the
+// bank-conflict-free kX6ClassRow, 0 round 3's kX6ClassRowBlk
+// (HZ_BLK_TABLE=0, hz_resblock_x6_set_table).  Whole forwards at 4,096 rows,
+// interleaved in one process (tools/blk_table_ab.py, 12 rounds x 20
+// forwards each): 2.2378 vs 2.2368 ms and 2.3143 vs 2.3073 ms on two boxes
+// (profiles/r05/blk_table), bit-identical
 static std::atomic<int32_t> g_x6_blk_cf{-1};
 static bool x6_blk_cf() {
   int32_t v = g_x6_blk_cf.load(std::memory_order_relaxed);
   if (v < 0) {
     const char *e = getenv("HZ_BLK_TABLE");
-    int32_t want = e && atoi(e) == 1 ? 1 : 0, expect = -1;
+    int32_t want = e && atoi(e) == 0 ? 0 : 1, expect = -1;
     g_x6_blk_cf.compare_exchange_strong(expect, want);
     v = g_x6_blk_cf.load(std::memory_order_relaxed);
   }

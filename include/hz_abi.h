@@ -148,8 +148,8 @@ int hz_play(hz_env *env, int32_t max_plies, int32_t auto_reset, uint64_t *traj_s
 int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
 /* hz_play's pipeline: 2 (the default; HZ_PIPELINE=1 in the environment at
  * hz_env_create makes 1 the default) = every board's game spread over
- * thirteen consecutive calls, one stage per call (seeding pass 1 in one
- * stage, pass 2 in two, five draw stages, five play stages), all thirteen
+ * thirteen consecutive calls, one stage per call (seeding pass 1 in two
+ * stages, pass 2 in three, four draw stages, four play stages), all thirteen
  * running in each launch on different episodes; 1 = the chance-ahead
  * pipeline above.  Same results either way; pipeline 2 applies to calls with
  * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
@@ -320,9 +320,9 @@ int32_t hz_resblock_x6_fused(int32_t batch);
  * the one-launch form where it applies; 0: the two layered convs (A/B
  * measurements); results are bit-identical. */
 int hz_resblock_x6_set_fused(int32_t on);
-/* The one-launch form's row placement: 0 (the default, unless
- * HZ_BLK_TABLE=1) round 3's row table, 1 the LDS-bank-conflict-free one the
- * layered conv uses (A/B measurements; results are bit-identical). */
+/* The one-launch form's row placement: 1 (the default, unless
+ * HZ_BLK_TABLE=0) the LDS-bank-conflict-free row table the layered conv
+ * uses, 0 round 3's (A/B measurements; results are bit-identical). */
 int hz_resblock_x6_set_table(int32_t cf);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,

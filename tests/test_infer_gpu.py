@@ -423,7 +423,7 @@ def test_resblock_x6_fused_equals_two_layered_convs(batch):
             _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6)
     finally:
         lib().hz_resblock_x6_set_fused(prev)
-        lib().hz_resblock_x6_set_table(0)
+        lib().hz_resblock_x6_set_table(1)
 
 
 def _check_resblock(batch, lib, _conv3x3_x6_act, _resblock_x6, pack_conv3x3_x6):

@@ -43,7 +43,7 @@ for r in range(rounds):
         e1.record()
         torch.cuda.synchronize()
         ts[t].append(e0.elapsed_time(e1) / 20)
-L.hz_resblock_x6_set_table(0)
+L.hz_resblock_x6_set_table(1)  # (the default)
 same = all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
 med = {t: sorted(v)[len(v) // 2] for t, v in ts.items()}
 print(json.dumps({"batch": B, "bit_identical": same, "ms_median": med, "ms_min": {t: min(v) for t, v in ts.items()},

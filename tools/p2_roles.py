@@ -18,14 +18,13 @@ out = {}
 for pipe in (1, 2):
     env = BatchedEnv(n, device="cuda")
     env.set_pipeline(pipe)
-    names = ({0: "play4", 1: "play3", 2: "play2", 3: "play1", 4: "D1", 5: "D2", 6: "D3", 7: "hashes", 8: "D4",
-              9: "D5", 10: "play0", 12: "P2x", 13: "P2y", 14: "twist", 15: "P1",
-              16: "play0_loaded", 17: "play0_plies", 18: "play1_loaded", 19: "play1_plies",
-              20: "play2_loaded", 21: "play2_plies", 22: "play3_loaded", 23: "play3_plies",
-              24: "play4_loaded", 25: "play4_plies", 26: "play4_scored",
-              27: "D1_staged", 28: "D2_staged", 29: "D3_staged", 30: "D4_staged", 31: "D5_staged",
-              32: "P2x_staged", 33: "P2y_staged",
-              35: "twist_go", 36: "twist_it1", 37: "twist_looped"} if pipe == 2 else
+    names = ({0: "playD", 1: "playC", 2: "playB", 3: "playA", 4: "D1", 5: "D2", 6: "P1b", 7: "hashes", 8: "D3",
+              9: "D4", 10: "P1a", 12: "P2a", 13: "P2b", 14: "P2c", 15: "twist",
+              16: "playA_loaded", 17: "playA_plies", 19: "playB_loaded", 20: "playB_plies",
+              22: "playC_loaded", 23: "playC_plies", 25: "playD_loaded", 26: "playD_plies", 27: "playD_scored",
+              28: "D1_staged", 29: "D2_staged", 30: "D3_staged", 31: "D4_staged",
+              32: "P2a_staged", 33: "P2b_staged", 34: "P2c_staged",
+              35: "twist_go", 36: "twist_it1", 37: "twist_looped", 38: "twist_done_seen"} if pipe == 2 else
              {5: "play", 6: "draw2", 15: "draw1", 7: "seed"})
     for only in (-1, 0, 1, 2, 3) if pipe == 2 else (-1,):
         L.hz_diag_set_role_only(-1)
