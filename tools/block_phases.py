@@ -53,6 +53,14 @@ names = ["setup", "chunk0_stage", "conv1_chunk0", "conv1_chunk1", "conv1_chunk2"
 res["fused_cycles"] = {n: med(s[:, order[i + 1]] - s[:, order[i]]) for i, n in enumerate(names)}
 res["fused_total"] = med(s[:, 7] - s[:, 0])
 res["fused_clock_mhz"] = med((s[:, 7] - s[:, 0]) / np.maximum(s[:, 9] - s[:, 8], 1) * 100.0)
+# MFMA issue cycles per wave of one fused block: 2 convs x (66 block-taps of
+# the wave's row half x 4 column blocks x 4 chunks x 6 bf16 products) x 16
+# cycles (v_mfma_f32_16x16x32_bf16, MI355X_MICROARCH.md constants) = the
+# SQ_VALU_MFMA_BUSY_CYCLES count per wave; busy = that over the workgroup's
+# in-kernel cycles (setup to epilogue end), at the clock measured alongside
+res["mfma_cycles_per_wave"] = 2 * 66 * 4 * 4 * 6 * 16
+res["fused_mfma_busy"] = res["mfma_cycles_per_wave"] / res["fused_total"]
+res["row_table"] = os.environ.get("HZ_BLK_TABLE", "1 (default)")
 for _ in range(200):
     assert lib.hz_conv3x3_x6_bias_act(x.data_ptr(), p1.data_ptr(), b1.data_ptr(), x.data_ptr(), out.data_ptr(), B,
                                       None, sp) == 0
