@@ -2010,7 +2010,7 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
   const int rb = blk - role * nblk;
 #ifdef HZ_DIAG
   if (g_role_only >= 0 && g_role_only != role) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (role == 0) p2_play(a, rb);
   else if (role == 3) p2_seed(a, rb);
@@ -2022,6 +2022,14 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
     const int w = threadIdx.x >> 6, bb = rb * kBlock + (threadIdx.x & 63);
     const bool idle = role == 2 && w == 3;
     if (g_stamps && role > 0 && !idle && bb < a.n) g_stamps[(size_t)bb * kP2Stamps + 4 * role + w] = __builtin_amdgcn_s_memtime() - t0;
+    // the wave's realtime (100 MHz) start and end and its clock cycles, per
+    // (role, wave): slot 40 of the block's boards 16 role + 4 w + k
+    // (tools/p2_span.py: the launch's span against its waves')
+    if (g_stamps && bb < a.n && (threadIdx.x & 63) < 4) {
+      const int k = threadIdx.x & 63;
+      const uint64_t v = k == 0 ? r0 : k == 1 ? __builtin_amdgcn_s_memrealtime() : k == 2 ? t0 : __builtin_amdgcn_s_memtime();
+      g_stamps[(size_t)(rb * kBlock + 16 * role + 4 * w + k) * kP2Stamps + 40] = v;
+    }
   }
 #endif
 }

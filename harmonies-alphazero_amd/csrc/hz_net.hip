@@ -1324,8 +1324,8 @@ __global__ void __launch_bounds__(256, 1)
   for (int k = 0; k < kRBT * NCB; k++) {
     const int rb = k / NCB, cb = k % NCB;
     const int row = orow(rb);
-    rv[k] = eres && row >= 0 ? *(const float4 *)(eres + gbase + (size_t)row * 128 + cow + 16 * cb)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    rv[k] = eres && row >= 0 && !(HZ_KO & 64) ? *(const float4 *)(eres + gbase + (size_t)row * 128 + cow + 16 * cb)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float4 bv[NCB];
 #pragma unroll

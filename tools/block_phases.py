@@ -42,11 +42,29 @@ def med(a):
     return float(np.median(a))
 
 
-res = {"batch": B}
-for _ in range(200):
+res = {"batch": B, "lib": os.environ.get("HZ_NET_DIAG_LIB", "libnet_diag.so")}
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for i in range(200):
+    if i == 50:
+        ev0.record()
     assert lib.hz_resblock_x6_bias_act(x.data_ptr(), p1.data_ptr(), b1.data_ptr(), p2.data_ptr(), b2.data_ptr(),
                                        out.data_ptr(), tmp.data_ptr(), B, None, sp) == 0
+ev1.record()
+torch.cuda.synchronize()
+res["fused_us_per_launch"] = ev0.elapsed_time(ev1) * 1e3 / 150
 s = stamps()
+# workgroup timeline of the last launch in us (s_memrealtime: 100 MHz)
+rt0, rt1 = s[:, 8].astype(np.float64), s[:, 9].astype(np.float64)
+base = rt0.min()
+st, en = (rt0 - base) / 100.0, (rt1 - base) / 100.0
+o = np.argsort(st)
+r1, r2 = o[:256], o[256:]
+res["timeline_us"] = {"round1_start_max": float(st[r1].max()), "round1_end_med": float(np.median(en[r1])),
+                      "round1_end_max": float(en[r1].max()),
+                      "round2_start_min": float(st[r2].min()) if len(r2) else None,
+                      "round2_start_med": float(np.median(st[r2])) if len(r2) else None,
+                      "round2_end_med": float(np.median(en[r2])) if len(r2) else None,
+                      "span": float(en.max())}
 order = [0, 1, 2, 3, 4, 5, 6, 10, 11, 12, 13, 14, 7]
 names = ["setup", "chunk0_stage", "conv1_chunk0", "conv1_chunk1", "conv1_chunk2", "conv1_chunk3", "switch",
          "conv2_chunk0", "conv2_chunk1", "conv2_chunk2", "conv2_chunk3", "epilogue"]
