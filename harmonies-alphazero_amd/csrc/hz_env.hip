@@ -2029,6 +2029,10 @@ __global__ void __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per
       const int k = threadIdx.x & 63;
       const uint64_t v = k == 0 ? r0 : k == 1 ? __builtin_amdgcn_s_memrealtime() : k == 2 ? t0 : __builtin_amdgcn_s_memtime();
       g_stamps[(size_t)(rb * kBlock + 16 * role + 4 * w + k) * kP2Stamps + 40] = v;
+      // where the wave ran: HW_ID (cu, sh, se in bits 8-14) and XCC_ID
+      if (k == 0)
+        g_stamps[(size_t)(rb * kBlock + 16 * role + 4 * w) * kP2Stamps + 41] =
+            (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
     }
   }
 #endif

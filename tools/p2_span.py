@@ -12,7 +12,7 @@ import numpy as np
 import torch
 import hzamd._native as nat
 from hzamd.env import BatchedEnv
-n = 4096
+n = int(os.environ.get("HZ_P2_BOARDS", "4096"))
 L = nat.lib()
 L.hz_diag_set_stamps.argtypes = [ctypes.c_void_p]
 stamps = torch.zeros(n, 48, dtype=torch.int64, device="cuda")
@@ -61,6 +61,29 @@ for role in range(4):
                      "dur_max": float(np.nanmax(dur[:, c])), "dur_med": float(np.nanmedian(dur[:, c])),
                      "cycles_max": float((te - ts)[:, c].max())}
 out["waves"] = waves
+# block rounds (n > 4096: more blocks than CUs): per CU, the gap between a
+# block's last wave end and the next block's first wave start there (a block
+# is (rb, role): columns 4 role .. 4 role + 3 of row rb)
+hw = stamps[:, 41].cpu().numpy().astype(np.int64).reshape(-1, 64)[:, 0::4]  # [rb][4 role + w]
+blocks = []
+for role in range(4):
+    cols = slice(4 * role, 4 * role + 4)
+    v = valid[:, cols].any(axis=1)
+    for rb in np.flatnonzero(v):
+        h = hw[rb, 4 * role]
+        blocks.append((((h >> 8) & 0x7F) | ((h >> 32) << 8), np.nanmin(start[rb, cols]), np.nanmax(end[rb, cols])))
+gaps, per_cu = [], {}
+for c, b_s, b_e in blocks:
+    per_cu.setdefault(c, []).append((b_s, b_e))
+for c, lst in per_cu.items():
+    lst.sort()
+    for (s1, e1), (s2, e2) in zip(lst[:-1], lst[1:]):
+        gaps.append(s2 - e1)
+if gaps:
+    out["block_gap_us"] = {"n": len(gaps), "median": float(np.median(gaps)), "max": float(np.max(gaps)),
+                           "min": float(np.min(gaps))}
+out["blocks_per_cu_max"] = max(len(v) for v in per_cu.values())
+out["cus_used"] = len(per_cu)
 # the last episode column's in-stage phases (cycles since the stage began;
 # tools/p2_roles.py's slot names)
 ph = stamps.cpu().numpy().astype(np.int64)
