@@ -976,12 +976,31 @@ __device__ __forceinline__ const int16_t (*x6_tab())[16] {
   if constexpr (Block && !Cf) return kX6ClassRowBlk;
   return kX6ClassRow;
 }
-template <bool Block, bool Cf = false>
-__global__ void __launch_bounds__(256, 1)
-    k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
-                   const float *__restrict__ res, float *__restrict__ out, int32_t batch,
-                   const int32_t *__restrict__ live, const bf16x8 *__restrict__ wp2,
-                   const float *__restrict__ bias2, float *__restrict__ tmp) {
+// Tower (Block only): the body runs once per residual block of a tower in
+// one launch (k_x6w4_tower): the activation it reads was written by this
+// workgroup's previous block, so its loads (staging, the skip, tmp) are
+// non-temporal (they bypass the CU's L1, which may hold the previous
+// block's lines) and the thread index is made opaque per block (nothing
+// derived from it is hoisted across blocks into registers)
+template <bool NT>
+__device__ __forceinline__ f32x4 x6_ld4(const float *p) {
+  if constexpr (NT) return __builtin_nontemporal_load((const f32x4 *)p);
+  return *(const f32x4 *)p;
+}
+template <bool NT>
+__device__ __forceinline__ float4 x6_ld4f(const float *p) {
+  if constexpr (NT) {
+    const f32x4 v = __builtin_nontemporal_load((const f32x4 *)p);
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  return *(const float4 *)p;
+}
+template <bool Block, bool Cf, bool Tower>
+__device__ __forceinline__ void x6w4_body(const float *__restrict__ x, const bf16x8 *__restrict__ wp,
+                                          const float *__restrict__ bias, const float *__restrict__ res,
+                                          float *__restrict__ out, int32_t batch, const int32_t *__restrict__ live,
+                                          const bf16x8 *__restrict__ wp2, const float *__restrict__ bias2,
+                                          float *__restrict__ tmp) {
   constexpr int NQ = 4, kRBT = 9, NCB = 4, NG = Block ? 8 : 4;
   constexpr int kZero = kCS * 35 * kX6Cell;  // 62,720 B: 256-B aligned
   constexpr int kBufT = kZero + kX6Zero;
@@ -993,7 +1012,10 @@ __global__ void __launch_bounds__(256, 1)
   static_assert(kDummyCell + kX6Cell <= 160 * 1024, "buffers, E and the dummy cell fit the LDS");
   extern __shared__ float4 lds4[];
   char *lds = (char *)lds4;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 1, chf = w & 1;
+  int t0 = threadIdx.x;
+  if constexpr (Tower) asm volatile("" : "+v"(t0));
+  __builtin_assume(t0 >= 0 && t0 < 256);
+  const int t = t0, lane = t & 63, w = t >> 6, kg = lane >> 4, rh = w >> 1, chf = w & 1;
   const int s0 = blockIdx.x * kCS;
   if (live) batch = *live < batch ? *live : batch;
   if (s0 >= batch) return;
@@ -1036,7 +1058,7 @@ __global__ void __launch_bounds__(256, 1)
       int f = it * 256 + tt;
       f = f < kRows * 8 ? f : kRows * 8 - 1;
       const int sc = s0 * 35 + srow(f);
-      stg[it] = *(const f32x4 *)(x + (size_t)(sc < last_row ? sc : last_row) * 128 + 4 * (f & 7) + 32 * q);
+      stg[it] = x6_ld4<Tower>(x + (size_t)(sc < last_row ? sc : last_row) * 128 + 4 * (f & 7) + 32 * q);
     }
   };
   // Block: conv2's chunk 2 from region E, chunks 1 and 3 from tmp (fp32 rows of 32 channels)
@@ -1057,7 +1079,7 @@ __global__ void __launch_bounds__(256, 1)
     for (int it = 0; it < kW4Stg; it++) {
       int f = it * 256 + tt;
       f = f < kRows * 8 ? f : kRows * 8 - 1;
-      stg[it] = *(const f32x4 *)(tmpg + half * kTmpRows * 32 + 32 * srow(f) + 4 * (f & 7));
+      stg[it] = x6_ld4<Tower>(tmpg + half * kTmpRows * 32 + 32 * srow(f) + 4 * (f & 7));
     }
   };
   auto stage_put = [&](int it, int buf) {
@@ -1324,9 +1346,12 @@ __global__ void __launch_bounds__(256, 1)
   for (int k = 0; k < kRBT * NCB; k++) {
     const int rb = k / NCB, cb = k % NCB;
     const int row = orow(rb);
-    rv[k] = eres && row >= 0 && !(HZ_KO & 64) ? *(const float4 *)(eres + gbase + (size_t)row * 128 + cow + 16 * cb)
+    rv[k] = eres && row >= 0 && !(HZ_KO & 64) ? x6_ld4f<Tower>(eres + gbase + (size_t)row * 128 + cow + 16 * cb)
                                               : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // (Tower: x and out are the same buffer from the second block on; every
+  // skip load is issued before any store, and the compiler keeps it so)
+  if constexpr (Tower) asm volatile("" ::: "memory");
   float4 bv[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; cb++) bv[cb] = *(const float4 *)(ebias + cow + 16 * cb);
@@ -1374,6 +1399,39 @@ __global__ void __launch_bounds__(256, 1)
   }
   HZ_STAMP(7)
   HZ_STAMP_RT(9)
+}
+template <bool Block, bool Cf = false>
+__global__ void __launch_bounds__(256, 1)
+    k_conv3x3_x6w4(const float *__restrict__ x, const bf16x8 *__restrict__ wp, const float *__restrict__ bias,
+                   const float *__restrict__ res, float *__restrict__ out, int32_t batch,
+                   const int32_t *__restrict__ live, const bf16x8 *__restrict__ wp2,
+                   const float *__restrict__ bias2, float *__restrict__ tmp) {
+  x6w4_body<Block, Cf, false>(x, wp, bias, res, out, batch, live, wp2, bias2, tmp);
+}
+// A tower of residual blocks in one launch (hz_tower_x6_blocks): each
+// workgroup carries its 8 states through every block (a block's rows depend
+// only on the same rows of the block before), writing each block's output
+// over the previous one in `out` (block 0 reads x); between blocks only the
+// workgroup's own barrier, after its stores have completed.  No launch
+// boundary per block: the workgroups drift apart, so their epilogue bursts
+// stop coinciding.  Same arithmetic per block as k_conv3x3_x6w4<true>.
+constexpr int kTowerMax = 16;
+struct X6Tower {
+  const bf16x8 *w1[kTowerMax], *w2[kTowerMax];
+  const float *b1[kTowerMax], *b2[kTowerMax];
+  int32_t nblk;
+};
+template <bool Cf>
+__global__ void __launch_bounds__(256, 1)
+    k_x6w4_tower(const float *__restrict__ x, float *out, int32_t batch, const int32_t *__restrict__ live,
+                 float *__restrict__ tmp, X6Tower tw) {
+#pragma unroll 1
+  for (int k = 0; k < tw.nblk; k++) {
+    x6w4_body<true, Cf, true>(k == 0 ? x : out, tw.w1[k], tw.b1[k], nullptr, out, batch, live, tw.w2[k], tw.b2[k],
+                              tmp);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's stores done before the barrier
+    __syncthreads();
+  }
 }
 }  // namespace
 #undef HZ_STAMP
@@ -1445,6 +1503,24 @@ static int launch_x6w4(const float *x, const void *wpack6, const float *bias, co
   }
   hipLaunchKernelGGL((k_conv3x3_x6w4<Block, Cf>), dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x,
                      (const bf16x8 *)wpack6, bias, res, out, batch, live, (const bf16x8 *)wpack6_2, bias2, tmp);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+template <bool Cf>
+static int launch_x6w4_tower(const float *x, float *out, float *tmp, const X6Tower &tw, int32_t batch,
+                             const int32_t *live, void *stream) {
+  static std::atomic<uint64_t> init_mask{0};
+  const size_t lds = 2 * (size_t)(kCS * 35 * kX6Cell + kX6Zero) + (size_t)(kRows + 1) * 128 + kX6Cell;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (!(init_mask.load(std::memory_order_acquire) >> dev & 1)) {
+    if (hipFuncSetAttribute((const void *)k_x6w4_tower<Cf>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+      return 1;
+    init_mask.fetch_or(1ull << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL((k_x6w4_tower<Cf>), dim3((batch + kCS - 1) / kCS), dim3(256), lds, (hipStream_t)stream, x, out,
+                     batch, live, tmp, tw);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -1533,6 +1609,34 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
                        : launch_x6w4<true>(x, w1, b1, nullptr, out, batch, live, stream, w2, b2, tmp);
   const int rc = launch_x6<4, false>(x, w1, b1, nullptr, tmp, batch, live, stream);
   return rc ? rc : launch_x6<4, false>(tmp, w2, b2, x, out, batch, live, stream);
+}
+
+// nblk residual blocks in one launch (k_x6w4_tower: each workgroup carries
+// its 8 states through all of them), where hz_resblock_x6_fused(batch)
+// holds; w1/b1/w2/b2 are HOST arrays of nblk device pointers (each block's
+// packed conv weights and folded biases).  out gets the last block's
+// output (and holds the intermediate ones); x is only read.  The same bits
+// as nblk hz_resblock_x6_bias_act calls.  -2: this batch takes the
+// per-block path (hz_resblock_x6_fused(batch) == 0).
+extern "C" int32_t hz_resblock_x6_fused(int32_t batch);
+extern "C" int hz_tower_x6_blocks(const float *x, const void *const *w1, const float *const *b1,
+                                  const void *const *w2, const float *const *b2, int32_t nblk, float *out,
+                                  float *tmp, int32_t batch, const int32_t *live, void *stream) {
+  if (!x || !w1 || !b1 || !w2 || !b2 || !out || !tmp || batch < 0 || nblk < 1 || nblk > kTowerMax) return -1;
+  if (((uintptr_t)x | (uintptr_t)out | (uintptr_t)tmp) & 15) return -1;
+  if (batch == 0) return 0;
+  if (!hz_resblock_x6_fused(batch)) return -2;
+  X6Tower tw{};
+  for (int k = 0; k < nblk; k++) {
+    if (!w1[k] || !b1[k] || !w2[k] || !b2[k] || (((uintptr_t)w1[k] | (uintptr_t)w2[k]) & 15)) return -1;
+    tw.w1[k] = (const bf16x8 *)w1[k];
+    tw.w2[k] = (const bf16x8 *)w2[k];
+    tw.b1[k] = b1[k];
+    tw.b2[k] = b2[k];
+  }
+  tw.nblk = nblk;
+  return x6_blk_cf() ? launch_x6w4_tower<true>(x, out, tmp, tw, batch, live, stream)
+                     : launch_x6w4_tower<false>(x, out, tmp, tw, batch, live, stream);
 }
 
 // 1: residual blocks at the 4-wave conv's batch sizes run as one launch, 0:

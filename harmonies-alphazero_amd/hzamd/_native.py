@@ -77,6 +77,7 @@ _SIGS = {
     "hz_resblock_x6_fused": ([_c.c_int32], _c.c_int32),
     "hz_resblock_x6_set_fused": ([_c.c_int32], _c.c_int),
     "hz_resblock_x6_set_table": ([_c.c_int32], _c.c_int),
+    "hz_tower_x6_blocks": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_resident": ([_vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split_max_batch": ([], _c.c_int32),

@@ -18,6 +18,7 @@ fp32; the results differ from the unfolded graph only by fp32 rounding
 (tests/test_infer_gpu.py states the tolerance).  Rebuild (or call refresh())
 after the weights change.
 """
+import ctypes
 import os
 
 import torch
@@ -225,6 +226,23 @@ def _resblock_x6(x, p1, b1, p2, b2, live=None):
     return out
 
 
+def _tower_blocks_x6(x, ptrs, nblk, live=None):
+    """Every residual block of the tower in one launch (hz_tower_x6_blocks:
+    each workgroup carries its 8 states through all blocks); None where the
+    batch takes the per-block path.  ptrs: the host pointer arrays built by
+    FoldedNet.refresh (kept alive there)."""
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    tmp = torch.empty_like(x, memory_format=torch.channels_last)
+    w1, b1, w2, b2 = ptrs
+    rc = lib().hz_tower_x6_blocks(x.data_ptr(), w1, b1, w2, b2, nblk, out.data_ptr(), tmp.data_ptr(), x.shape[0],
+                                  _live_ptr(live), torch.cuda.current_stream(x.device).cuda_stream)
+    if rc == -2:
+        return None
+    if rc != 0:
+        raise NativeError(f"hz_tower_x6_blocks failed ({rc})")
+    return out
+
+
 def pack_stem_x6(w):
     """Stem weights [128][38][3][3] in hz_stem3x3_x6_bias_act's layout: bf16
     planes [K-step][q][plane][co][32] over 64 input slots.  Slots 0-37 are
@@ -368,6 +386,13 @@ class FoldedNet(nn.Module):
     resident_max = int(os.environ.get("HZ_RESIDENT_MAX", "1024"))  # (A/B measurements)
     # ... and at most this many with 8 workgroups per state (hz_tower_x6_split)
     split_max = int(os.environ.get("HZ_SPLIT_MAX", "32"))
+    # residual blocks above the one-state forms' batch limit: 1 (the default)
+    # = all of them in one launch (hz_tower_x6_blocks), 0 = one launch per
+    # block (hz_resblock_x6_bias_act); the same bits either way.  Forward at
+    # 4,096 rows, interleaved A/B in one process (tools/tower_ab.py): 2.229 vs
+    # 2.261 ms and 2.272 vs 2.286 ms on two boxes; self-play 141.8 vs 141.0
+    # games/s (profiles/r05/tower)
+    tower_loop = int(os.environ.get("HZ_TOWER_LOOP", "1"))
 
     def __init__(self, net, epilogue=None, native_conv=True, tower="x6", fused_head=True):
         super().__init__()
@@ -404,6 +429,14 @@ class FoldedNet(nn.Module):
                 self.packed = [(allw[2 * i], allw[2 * i + 1]) for i in range(len(self.blocks))]
                 if allw.shape[0] <= 64:  # the kernel's bias table holds 64 convs
                     self.resident = (allw, torch.stack([b for blk in self.blocks for (_, b) in blk]).contiguous())
+                # hz_tower_x6_blocks' host arrays of device pointers (the
+                # biases kept contiguous here so the pointers stay valid)
+                self._tw_bias = [(b1.contiguous(), b2.contiguous()) for (_, b1), (_, b2) in self.blocks]
+                P = ctypes.c_void_p * len(self.blocks)
+                self._tw_ptrs = (P(*[p1.data_ptr() for p1, _ in self.packed]),
+                                 P(*[b1.data_ptr() for b1, _ in self._tw_bias]),
+                                 P(*[p2.data_ptr() for _, p2 in self.packed]),
+                                 P(*[b2.data_ptr() for _, b2 in self._tw_bias]))
             else:
                 self.packed = [(pk(w1), pk(w2)) for (w1, _), (w2, _) in self.blocks]
         self.pconv = _fold(n.policy_conv, n.policy_bn)
@@ -458,8 +491,14 @@ class FoldedNet(nn.Module):
         elif self.resident is not None and B <= max(self.resident_max, min(self.split_max, 32)):
             x = _tower_resident(x, *self.resident, live)
         elif self.packed is not None and self.tower == "x6":
-            for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
-                x = _resblock_x6(x, p1, b1, p2, b2, live)
+            xt = None
+            if self.tower_loop and len(self.blocks) <= 16:
+                xt = _tower_blocks_x6(x, self._tw_ptrs, len(self.blocks), live)
+            if xt is not None:
+                x = xt
+            else:
+                for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
+                    x = _resblock_x6(x, p1, b1, p2, b2, live)
         elif self.packed is not None:
             for ((_, b1), (_, b2)), (p1, p2) in zip(self.blocks, self.packed):
                 y = _conv3x3_act(x, p1, b1, None, live)

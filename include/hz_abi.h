@@ -324,6 +324,17 @@ int hz_resblock_x6_set_fused(int32_t on);
  * HZ_BLK_TABLE=0) the LDS-bank-conflict-free row table the layered conv
  * uses, 0 round 3's (A/B measurements; results are bit-identical). */
 int hz_resblock_x6_set_table(int32_t cf);
+/* nblk residual blocks (model.py:376-393, at most 16) in ONE launch where
+ * hz_resblock_x6_fused(batch) holds: each workgroup carries its 8 states
+ * through every block, block k's output written over block k-1's in out
+ * (block 0 reads x, which is only read).  w1/b1/w2/b2 are HOST arrays of
+ * nblk device pointers (each block's packed conv weights and folded
+ * biases, as hz_resblock_x6_bias_act takes them); tmp as there.  The same
+ * bits as nblk hz_resblock_x6_bias_act calls.  Returns -2 (nothing
+ * enqueued) for a batch the per-block path serves. */
+int hz_tower_x6_blocks(const float *x, const void *const *w1, const float *const *b1, const void *const *w2,
+                       const float *const *b2, int32_t nblk, float *out, float *tmp, int32_t batch,
+                       const int32_t *live, void *stream);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the

@@ -481,6 +481,59 @@ def test_folded_net_fused_blocks_same_bits():
     assert torch.equal(l0[:n - 5], l1[:n - 5]) and torch.equal(v0[:n - 5], v1[:n - 5])
 
 
+@pytest.mark.parametrize("batch", [769, 803, 4096])
+def test_tower_one_launch_equals_per_block_launches(batch):
+    """hz_tower_x6_blocks (every workgroup carries its 8 states through all
+    eight residual blocks in one launch, each block's output written over
+    the previous one) gives the bits of eight hz_resblock_x6_bias_act
+    launches, with both row tables, a partly filled last workgroup (803), a
+    live-row bound inside a workgroup and a NaN tail past the input; the
+    input is left unchanged; a batch the per-block path serves is refused
+    with -2 (nothing enqueued) and FoldedNet falls back."""
+    from hzamd._native import lib
+    from hzamd.infer import _resblock_x6, _tower_blocks_x6
+    g = torch.Generator().manual_seed(batch)
+    torch.manual_seed(batch)
+    net = HarmoniesNet().eval()
+    _randomise_bn(net, g)
+    fnet = FoldedNet(net.cuda())
+    cl = torch.channels_last
+    x = torch.randn(batch, 128, 5, 7, generator=g).relu()
+    buf = torch.full((batch + 9, 128, 5, 7), float("nan"), device="cuda").contiguous(memory_format=cl)
+    buf[:batch] = x.cuda()
+    xc = buf[:batch]
+    x0 = xc.clone()
+    live = torch.tensor([batch - 4], dtype=torch.int32, device="cuda")
+    try:
+        for table in (0, 1):
+            assert lib().hz_resblock_x6_set_table(table) == 0
+            ref = xc
+            for ((_, b1), (_, b2)), (p1, p2) in zip(fnet.blocks, fnet.packed):
+                ref = _resblock_x6(ref, p1, b1, p2, b2)
+            tw = _tower_blocks_x6(xc, fnet._tw_ptrs, len(fnet.blocks))
+            assert tw is not None and torch.equal(tw, ref), table
+            part = _tower_blocks_x6(xc, fnet._tw_ptrs, len(fnet.blocks), live)
+            assert torch.equal(part[:batch - 4], ref[:batch - 4]), table
+            assert torch.equal(xc, x0)
+    finally:
+        lib().hz_resblock_x6_set_table(1)
+    small = torch.zeros(64, 128, 5, 7, device="cuda").contiguous(memory_format=cl)
+    assert _tower_blocks_x6(small, fnet._tw_ptrs, len(fnet.blocks)) is None
+    # the whole forward with the tower loop on and off: the same bits
+    board = (torch.rand(batch, 38, 5, 7, generator=g) > 0.8).float().cuda()
+    board[:, 37] = 2.0 / 3.0
+    glob = torch.rand(batch, 42, generator=g).cuda()
+    prev = fnet.tower_loop
+    try:
+        fnet.tower_loop = 0
+        l0, v0 = fnet(board, glob)
+        fnet.tower_loop = 1
+        l1, v1 = fnet(board, glob)
+    finally:
+        fnet.tower_loop = prev
+    assert torch.equal(l0, l1) and torch.equal(v0, v1)
+
+
 _CS4_SCRIPT = """
 import sys, torch
 sys.path[:0] = [sys.argv[2]]
