@@ -324,7 +324,8 @@ int hz_resblock_x6_set_fused(int32_t on);
  * HZ_BLK_TABLE=0) the LDS-bank-conflict-free row table the layered conv
  * uses, 0 round 3's (A/B measurements; results are bit-identical). */
 int hz_resblock_x6_set_table(int32_t cf);
-/* nblk residual blocks (model.py:376-393, at most 16) in ONE launch where
+/* The residual tower (model.py:332-334: nblk <= 16 ResidualBlock.forward,
+ * :376-393) in ONE launch where
  * hz_resblock_x6_fused(batch) holds: each workgroup carries its 8 states
  * through every block, block k's output written over block k-1's in out
  * (block 0 reads x, which is only read).  w1/b1/w2/b2 are HOST arrays of
