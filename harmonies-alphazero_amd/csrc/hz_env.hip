@@ -1030,90 +1030,187 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 #endif
     bool lds_used = !seeded;  // the LDS copy of the stream is live
     bool pre = seeded && ahead_rule != nullptr;  // the episode's rule hashes are in LDS
-    for (int i = 0; i < max_plies; i++) {
-      if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
-        if constexpr (!AutoReset) {
-          if (Record && traj_action) {
-            for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
+    if constexpr (AutoReset) {
+      // A board whose game ends starts its next episode: seeding its stream
+      // is a 1,246-step chain (~60 k cycles) that the whole wave waits for.
+      // Each lane counts its own plies (used), and a lane whose game ended
+      // waits until no lane of the wave can play on; then every waiting lane
+      // seeds together, in one pass, and play resumes.  Every board plays the
+      // same plies in the same order as with a reset at its own ply (lanes
+      // share nothing), so results are the same; the wave seeds once or
+      // twice per launch instead of once per distinct game end.
+      int used = 0;
+      bool stuck = false;
+      while (true) {
+        const bool over = phase_of(s.misc) == PH_OVER;
+        const bool can = !over && !stuck && used < max_plies;
+        if (!__any(can)) {
+          const bool want = over && !stuck && used < max_plies;
+          if (!__any(want)) break;
+          if (want) {  // the next episode of every waiting board, seeded together
+            if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
+            int e = episode[b];
+            sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+            rkey = rule_key(sd);
+            episode[b] = e + 1;
+            mt_seed(hz_lds + lane, kLdsStride, sd);
+            draw.m = LdsMT(lane, kMTSeeded);
+            draw.scripted = false;
+            lds_used = true;
+            pre = false;
+            reset_state(s, draw);
+            g_ply = 0;
           }
-          break;
-        }
-        if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
-        int e = episode[b];
-        sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
-        rkey = rule_key(sd);
-        episode[b] = e + 1;
-        mt_seed(hz_lds + lane, kLdsStride, sd);
-        draw.m = LdsMT(lane, kMTSeeded);
-        draw.scripted = false;
-        lds_used = true;
-        pre = false;
-        reset_state(s, draw);
-        g_ply = 0;
-      }
-      if constexpr (!Record) {
-        // a pair of whole turns at once while every board of the wave still
-        // playing is at a pair boundary (always, for boards reset together)
-        if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
-          uint32_t h[8];
-          if (__all(pre && g_ply + 8 <= kRulePlies)) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) h[j] = hz_lds[(g_ply + j) * kLdsStride + lane];
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) h[j] = rule_h32(rkey, g_ply + j);
-          }
-          int done = 4;
-          if (__all(draw.pair_pops())) {  // the refills are plain pops
-            play_turn_h<0, PlayDraw, true>(s, draw, h[0], h[1], h[2], h[3]);
-            if (phase_of(s.misc) != PH_OVER) {
-              play_turn_h<1, PlayDraw, true>(s, draw, h[4], h[5], h[6], h[7]);
-              done = 8;
-            }
-          } else {
-            play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
-            if (phase_of(s.misc) != PH_OVER) {
-              play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
-              done = 8;
-            }
-          }
-          g_ply += done;
-          steps += done;
-          i += done - 1;
-          if (phase_of(s.misc) == PH_OVER) games++;
           continue;
         }
-      }
-      int a;
-      HZ_ACC(8, t0);
-      if constexpr (Record) {
-        uint64_t mk[3];
-        int L = legal_mask(s, mk);
-        HZ_ACC(9, t0);
-        if (traj_state) {
-          uint64_t *o = traj_state + (size_t)i * 6 * n + b;
-          o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
-          o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+        if (!can) continue;
+        if constexpr (!Record) {
+          // a pair of whole turns at once while every playing board of the
+          // wave is at a pair boundary with 8 plies of budget
+          if (__all(used + 8 <= max_plies && turn_pair_safe(s))) {
+            uint32_t h[8];
+            if (__all(pre && g_ply + 8 <= kRulePlies)) {
+#pragma unroll
+              for (int j = 0; j < 8; j++) h[j] = hz_lds[(g_ply + j) * kLdsStride + lane];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; j++) h[j] = rule_h32(rkey, g_ply + j);
+            }
+            int done = 4;
+            if (__all(draw.pair_pops())) {  // the refills are plain pops
+              play_turn_h<0, PlayDraw, true>(s, draw, h[0], h[1], h[2], h[3]);
+              if (phase_of(s.misc) != PH_OVER) {
+                play_turn_h<1, PlayDraw, true>(s, draw, h[4], h[5], h[6], h[7]);
+                done = 8;
+              }
+            } else {
+              play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
+              if (phase_of(s.misc) != PH_OVER) {
+                play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
+                done = 8;
+              }
+            }
+            g_ply += done;
+            steps += done;
+            used += done;
+            if (phase_of(s.misc) == PH_OVER) games++;
+            continue;
+          }
         }
-        if (traj_mask) {
-          uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
-          o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+        int a;
+        if constexpr (Record) {
+          uint64_t mk[3];
+          int L = legal_mask(s, mk);
+          if (traj_state) {
+            uint64_t *o = traj_state + (size_t)used * 6 * n + b;
+            o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
+            o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+          }
+          if (traj_mask) {
+            uint64_t *o = traj_mask + ((size_t)used * n + b) * 3;
+            o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+          }
+          a = L ? kth_action(mk, rule_pick_k(rkey, g_ply, L)) : -1;
+          if (traj_action) traj_action[(size_t)used * n + b] = (int16_t)a;
+        } else {
+          a = rule_action(s, rule_h32(rkey, g_ply));  // legal mask + rule pick, fused
         }
-        a = L ? kth_action(mk, rule_pick_k(rkey, g_ply, L)) : -1;
-        if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
-      } else {
-        a = rule_action(s, rule_h32(rkey, g_ply));  // legal mask + rule pick, fused
-        HZ_ACC(9, t0);
+        if (a < 0) {  // stuck board (unreachable from HarmoniesGameState())
+          stuck = true;
+          continue;
+        }
+        step_trusted<true>(s, a, draw);
+        g_ply++;
+        steps++;
+        used++;
+        if (phase_of(s.misc) == PH_OVER) games++;
       }
-      if (a < 0) break;  // stuck board (unreachable from HarmoniesGameState())
-      HZ_ACC(10, t0);
-      bool te = phase_of(s.misc) == PH_P3;
-      step_trusted<true>(s, a, draw);
-      if (te) HZ_ACC(12, t0);
-      else HZ_ACC(11, t0);
-      g_ply++;
-      steps++;
-      if (phase_of(s.misc) == PH_OVER) games++;
+    } else {
+      for (int i = 0; i < max_plies; i++) {
+        if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
+          if constexpr (!AutoReset) {
+            if (Record && traj_action) {
+              for (int j = i; j < max_plies; j++) traj_action[(size_t)j * n + b] = -1;
+            }
+            break;
+          }
+          if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
+          int e = episode[b];
+          sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+          rkey = rule_key(sd);
+          episode[b] = e + 1;
+          mt_seed(hz_lds + lane, kLdsStride, sd);
+          draw.m = LdsMT(lane, kMTSeeded);
+          draw.scripted = false;
+          lds_used = true;
+          pre = false;
+          reset_state(s, draw);
+          g_ply = 0;
+        }
+        if constexpr (!Record) {
+          // a pair of whole turns at once while every board of the wave still
+          // playing is at a pair boundary (always, for boards reset together)
+          if (__all(i + 8 <= max_plies && turn_pair_safe(s))) {
+            uint32_t h[8];
+            if (__all(pre && g_ply + 8 <= kRulePlies)) {
+  #pragma unroll
+              for (int j = 0; j < 8; j++) h[j] = hz_lds[(g_ply + j) * kLdsStride + lane];
+            } else {
+  #pragma unroll
+              for (int j = 0; j < 8; j++) h[j] = rule_h32(rkey, g_ply + j);
+            }
+            int done = 4;
+            if (__all(draw.pair_pops())) {  // the refills are plain pops
+              play_turn_h<0, PlayDraw, true>(s, draw, h[0], h[1], h[2], h[3]);
+              if (phase_of(s.misc) != PH_OVER) {
+                play_turn_h<1, PlayDraw, true>(s, draw, h[4], h[5], h[6], h[7]);
+                done = 8;
+              }
+            } else {
+              play_turn_h<0>(s, draw, h[0], h[1], h[2], h[3]);
+              if (phase_of(s.misc) != PH_OVER) {
+                play_turn_h<1>(s, draw, h[4], h[5], h[6], h[7]);
+                done = 8;
+              }
+            }
+            g_ply += done;
+            steps += done;
+            i += done - 1;
+            if (phase_of(s.misc) == PH_OVER) games++;
+            continue;
+          }
+        }
+        int a;
+        HZ_ACC(8, t0);
+        if constexpr (Record) {
+          uint64_t mk[3];
+          int L = legal_mask(s, mk);
+          HZ_ACC(9, t0);
+          if (traj_state) {
+            uint64_t *o = traj_state + (size_t)i * 6 * n + b;
+            o[0] = s.pl[0]; o[(size_t)n] = s.pl[1]; o[(size_t)2 * n] = s.pl[2]; o[(size_t)3 * n] = s.pl[3];
+            o[(size_t)4 * n] = s.piles; o[(size_t)5 * n] = s.misc;
+          }
+          if (traj_mask) {
+            uint64_t *o = traj_mask + ((size_t)i * n + b) * 3;
+            o[0] = mk[0]; o[1] = mk[1]; o[2] = mk[2];
+          }
+          a = L ? kth_action(mk, rule_pick_k(rkey, g_ply, L)) : -1;
+          if (traj_action) traj_action[(size_t)i * n + b] = (int16_t)a;
+        } else {
+          a = rule_action(s, rule_h32(rkey, g_ply));  // legal mask + rule pick, fused
+          HZ_ACC(9, t0);
+        }
+        if (a < 0) break;  // stuck board (unreachable from HarmoniesGameState())
+        HZ_ACC(10, t0);
+        bool te = phase_of(s.misc) == PH_P3;
+        step_trusted<true>(s, a, draw);
+        if (te) HZ_ACC(12, t0);
+        else HZ_ACC(11, t0);
+        g_ply++;
+        steps++;
+        if (phase_of(s.misc) == PH_OVER) games++;
+      }
     }
 #ifdef HZ_DIAG_ROLES_ONLY
     HZ_PHASE(9, role_t0, b);
