@@ -85,7 +85,7 @@ def parse():
                     help="config 2: skip the per-ply API path leg (reset / legal+rule+step per ply / score graphs)")
     ap.add_argument("--no-auto-reset", action="store_true",
                     help="config 2: skip the steady-state auto-reset leg (hz_rollout auto_reset launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"))
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="1: one game at a time through the drop-in modules (profile_self_play.py); "
                          "2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "

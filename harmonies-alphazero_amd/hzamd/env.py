@@ -38,6 +38,7 @@ class BatchedEnv:
         nat.check(L.hz_env_set_error_word(self._h, nat.ptr(self.wait_err)), "hz_env_set_error_word")
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self._err_ev = None
+        self._err_calls = 0
 
     # -- plumbing ----------------------------------------------------------
     def _sync_stream(self):
@@ -191,14 +192,21 @@ class BatchedEnv:
         self._poll_errors()
         return games_done, steps_done, traj
 
+    POLL_EVERY = 32  # rollout calls between two queued error-word copies
+
     def _poll_errors(self):
-        """After a rollout launch: if the previous launch's error-word copy has
-        landed, raise on it; then queue this launch's copy (no host wait)."""
+        """After a rollout launch: if the last queued error-word copy has
+        landed, raise on it; every POLL_EVERY calls queue a new copy (no host
+        wait).  check_errors() waits and checks everything queued so far."""
         ev = self._err_ev
         if ev is not None and ev.query():
             self._err_ev = None
             self._raise_wait_error(int(self._err_host[0]))
-        if self._err_ev is None:
+        self._err_calls += 1
+        # (a copy and an event on the stream every POLL_EVERY calls, not
+        # every call: back-to-back launches stay back to back)
+        if self._err_ev is None and self._err_calls >= self.POLL_EVERY:
+            self._err_calls = 0
             self._err_host.copy_(self.wait_err, non_blocking=True)
             self._err_ev = torch.cuda.Event()
             self._err_ev.record()

@@ -2,7 +2,11 @@
 command (the roofline must be reproducible from
 profiles/).
 
-usage: driver_prof.py <run_kernel_trace.csv> <run_kernel_stats.csv> <bench.json> <out.json>
+usage: driver_prof.py <run_kernel_trace.csv> <run_kernel_stats.csv> <bench.json> <out.json> [untraced_bench.json]
+
+(bench.json: the line the traced run printed; untraced_bench.json: the same
+command's line without the profiler, whose event-timed kernel_ms carries no
+tracer overhead: the profile's median is checked against both)
 
 For every kernel of interest: dispatch count, mean, median, 10 % trimmed mean
 (the middle 80 % of dispatches), p90, p99 and max in us, next to rocprofv3's
@@ -17,7 +21,9 @@ import sys
 import numpy as np
 
 KEEP = ("k_play2", "k_rollout", "k_conv3x3_x6w4", "k_conv3x3_x6<", "k_stem", "k_heads_fc", "k_expand_backup",
-        "k_select", "k_gather_encode", "k_ply", "k_legal", "k_step", "k_rule", "k_score", "k_tower_x6")
+        "k_select", "k_gather_encode", "k_ply", "k_legal", "k_step", "k_rule", "k_score", "k_tower_x6", "k_x6w4_tower")
+# the full-batch leaf-eval forward: the residual tower in one launch, the stem, the fused head
+NN_KERNELS = ("k_x6w4_tower<true>", "k_conv3x3_x6<2, true, 8, 2>", "k_heads_fc")
 
 
 def short(name):
@@ -73,7 +79,36 @@ def main():
         if sp:
             out["selfplay_line"] = {k2: sp.get(k2) for k2 in ("games_per_s", "ms_per_move", "nn_ms_per_move",
                                                               "tree_ms_per_move")}
-            out["selfplay_line"]["nn_roofline_frac"] = (sp.get("nn_roofline") or {}).get("frac")
+            nr = sp.get("nn_roofline") or {}
+            out["selfplay_line"]["nn_roofline_frac"] = nr.get("frac")
+            # the same roofline from the profile: the forward's kernels'
+            # median dispatches (most dispatches are full 4,096-row batches)
+            if nr.get("flop_per_eval") and all(kn2 in kernels for kn2 in NN_KERNELS):
+                fwd_us = sum(kernels[kn2]["median_us"] for kn2 in NN_KERNELS)
+                rows = sp.get("boards") or 4096
+                out["selfplay_line"]["nn_forward_us_from_median"] = fwd_us
+                out["selfplay_line"]["nn_roofline_frac_from_median"] = (
+                    nr["flop_per_eval"] * rows / (fwd_us * 1e-6) / (nr["peak"] * 1e12))
+    if len(sys.argv) > 5 and "driver_line_check" in out:
+        try:
+            ul = json.loads(open(sys.argv[5]).read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            ul = None
+        k = kernels.get(out["driver_line_check"]["kernel"])
+        if ul and k:
+            rf = ul["roofline"]
+            lpstep = ul["config"].get("launches_per_step", 256)
+            fm = rf["alg_bytes_per_launch"] / (k["median_us"] * 1e-6) / (rf["peak"] * 1e9)
+            out["untraced_line_check"] = {
+                "ms_per_step": ul["ms_per_step"], "line_kernel_ms": rf.get("kernel_ms"), "line_frac": rf["frac"],
+                "launches_x_median_us_ms": lpstep * k["median_us"] / 1e3,
+                "fits_ms_per_step_median": lpstep * k["median_us"] / 1e3 <= ul["ms_per_step"],
+                "frac_from_median_us": fm, "frac_rel_diff_median": abs(fm / rf["frac"] - 1)}
+            nr = (ul.get("selfplay") or {}).get("nn_roofline") or {}
+            if "nn_roofline_frac_from_median" in out.get("selfplay_line", {}) and nr.get("frac"):
+                out["untraced_line_check"]["nn_roofline_frac"] = nr["frac"]
+                out["untraced_line_check"]["nn_frac_rel_diff"] = abs(
+                    out["selfplay_line"]["nn_roofline_frac_from_median"] / nr["frac"] - 1)
     json.dump(out, open(out_p, "w"), indent=1)
     for n, k in sorted(kernels.items(), key=lambda t: -t[1]["n"] * t[1]["mean_us"]):
         print(f"{n[:44]:44s} n={k['n']:7d} mean={k['mean_us']:8.2f} med={k['median_us']:8.2f} "
