@@ -1041,12 +1041,21 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       // twice per launch instead of once per distinct game end.
       int used = 0;
       bool stuck = false;
+#ifdef HZ_DIAG_ROLES_ONLY
+      int n_pass = 0, n_iter = 0;
+#endif
       while (true) {
         const bool over = phase_of(s.misc) == PH_OVER;
         const bool can = !over && !stuck && used < max_plies;
+#ifdef HZ_DIAG_ROLES_ONLY
+        n_iter++;
+#endif
         if (!__any(can)) {
           const bool want = over && !stuck && used < max_plies;
           if (!__any(want)) break;
+#ifdef HZ_DIAG_ROLES_ONLY
+          n_pass++;
+#endif
           if (want) {  // the next episode of every waiting board, seeded together
             if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
             int e = episode[b];
@@ -1125,6 +1134,12 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
         used++;
         if (phase_of(s.misc) == PH_OVER) games++;
       }
+#ifdef HZ_DIAG_ROLES_ONLY
+      if (g_stamps && lane == 0) {  // the wave's reseeding passes and loop iterations (tools/ar_passes.py)
+        g_stamps[(size_t)b * 16 + 11] = n_pass;
+        g_stamps[(size_t)b * 16 + 12] = n_iter;
+      }
+#endif
     } else {
       for (int i = 0; i < max_plies; i++) {
         if (phase_of(s.misc) == PH_OVER) {  // finished (scored, or scoring deferred)
@@ -1285,6 +1300,21 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
 // games_done / steps_done count that game (its first plies ran in the three
 // calls before, in playA, playB and playC).  In steady state a call does
 // every stage once per board: one game's worth of work per board per call.
+#ifndef HZ_P2_ST_WT
+// 1: the hand-off stores (hashes, cursors, scripts, mid-game states) write-
+// through too (global_store ... sc1): 17.0 G against 18.3 G with them plain
+// (profiles/r05/p2_writethrough), so plain by default
+#define HZ_P2_ST_WT 0
+#endif
+#ifndef HZ_P2_AUX
+// cache policy of the seeding stages' and the twist's stream-slot stores
+// (~24 MB per 4096-board launch): 16 = sc1, write-through, the line dropped
+// from the XCD's L2 (the next call's stages read them, from the MALL), so
+// the kernel's end finds no dirty slot lines to write back: 14.1 vs 15.8 us
+// per launch against plain stores (0), 15.5 with nt (2)
+// (profiles/r05/p2_writethrough; A/B builds -DHZ_P2_AUX=0 / 2)
+#define HZ_P2_AUX 16
+#endif
 constexpr int kP2Win = 96;        // rows a draw stage stages, from its wave's lowest cursor
 constexpr int kP2WinRows = kP2Win + 24;  // LDS rows per window (a scan reads up to 23 rows past its cursor)
 constexpr int kP2Play = 4;        // play stages
@@ -1488,8 +1518,28 @@ __device__ __forceinline__ void p2_publish(int *flag, int v) {
 // (wb = the slot's column of the wave's first board, wave-uniform, so a
 // row's address is a scalar base plus the lane: no 64-bit address
 // arithmetic per step in the chain)
-__device__ __forceinline__ void mt_pass1_span(uint32_t *__restrict__ wb, int lane, size_t ns, uint32_t kA, uint32_t kB,
-                                              int i0, int i1, uint32_t &prev) {
+// the slot's columns of boards [b0, b0 + 64) as a buffer (rows of nr words)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, int b0, size_t nr) {
+  const uint64_t base = (uint64_t)(slot + b0);
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+// a store read by another stage in a later call only: write-through (sc1)
+// like the slot stores (HZ_P2_AUX), so the kernel's end has no dirty lines
+// of it to write back
+template <class T>
+__device__ __forceinline__ void p2_st(T *p, T v) {
+  if constexpr (HZ_P2_AUX == 16 && HZ_P2_ST_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+// (the stream slots' stores: written by one stage, read by another in the
+// next call, never by this one: HZ_P2_AUX write-through (sc1) leaves no
+// dirty lines in the XCD's L2 for the end of the kernel to write back)
+__device__ __forceinline__ void mt_pass1_span(uint32_t *__restrict__ slot, int b0, int lane, size_t ns, uint32_t kA,
+                                              uint32_t kB, int i0, int i1, uint32_t &prev) {
+  const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, ns);
+  const int row_bytes = __builtin_amdgcn_readfirstlane((int)(ns * 4));
   // init_genrand's table words a group ahead (scalar loads: their wait
   // would otherwise sit in the chain once per group)
   uint32_t iv[8];
@@ -1500,10 +1550,11 @@ __device__ __forceinline__ void mt_pass1_span(uint32_t *__restrict__ wb, int lan
     uint32_t nx[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) nx[u] = kInitGen.v[g + 8 + u < kMT ? g + 8 + u : kMT - 1];
+    const int soff = __builtin_amdgcn_readfirstlane(g * row_bytes);
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const uint32_t v = (iv[u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
-      wb[(size_t)(g + u) * ns + lane] = v;
+      __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, soff + u * row_bytes, HZ_P2_AUX);
       prev = v;
     }
 #pragma unroll
@@ -1524,7 +1575,7 @@ __device__ __forceinline__ void p2_p1a(const P2Args &a, int b0, int lane) {
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
   uint32_t prev = 19650218u;
-  mt_pass1_span(a.s_mt[0] + b0, lane, nr, kA, kB, 1, kP1Split, prev);
+  mt_pass1_span(a.s_mt[0], b0, lane, nr, kA, kB, 1, kP1Split, prev);
   a.p1h_w[b] = prev;
   a.s_tag[0][b] = e * 8 + 1;
 }
@@ -1536,16 +1587,20 @@ __device__ __forceinline__ void p2_p1b(const P2Args &a, int b0, int lane) {
   uint32_t kA, kB;
   p2_keys(episode_seed(a.seed_base, b, e), kA, kB);
   uint32_t prev = a.p1h_r[b];
-  uint32_t *w = a.s_mt[1] + b;
-  mt_pass1_span(a.s_mt[1] + b0, lane, nr, kA, kB, kP1Split, 617, prev);
+  const uint32_t *w = a.s_mt[1] + b;
+  const uint32_t row1 = w[nr];  // (P1a's step-1 word, read before any store of this wave)
+  mt_pass1_span(a.s_mt[1], b0, lane, nr, kA, kB, kP1Split, 617, prev);
+  const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(a.s_mt[1], b0, nr);
+  const int row_bytes = __builtin_amdgcn_readfirstlane((int)(nr * 4));
 #pragma unroll
   for (int u = 0; u < 7; u++) {  // steps 617..623
     const uint32_t v = (kInitGen.v[617 + u] ^ ((prev ^ (prev >> 30)) * 1664525U)) + ((u & 1) ? kB : kA);
-    w[(size_t)(617 + u) * nr] = v;
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, (617 + u) * row_bytes, HZ_P2_AUX);
     prev = v;
   }
   // mt[0] = mt[623]; the 624th step at i = 1 (key j = 623 % keylen -> kB)
-  w[nr] = (w[nr] ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB;
+  __builtin_amdgcn_raw_buffer_store_b32((row1 ^ ((prev ^ (prev >> 30)) * 1664525U)) + kB, rs, lane * 4, row_bytes,
+                                        HZ_P2_AUX);
   a.s_tag[1][b] = e * 8 + 2;
 }
 
@@ -1603,13 +1658,6 @@ __device__ __forceinline__ void p2_put(const P2Piece<R0, R1> &pc, int lane) {
   }
   // (a wave's LDS operations execute in order: its later reads see these)
 }
-// the slot's columns of boards [b0, b0 + 64) as a buffer (rows of nr words)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, int b0, size_t nr) {
-  const uint64_t base = (uint64_t)(slot + b0);
-  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
-  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
-}
 // twist_word(cur, next, far) = far ^ twist_part(cur, next): the part of row
 // r's next-generation word that rows r and r + 1 decide
 __device__ __forceinline__ uint32_t twist_part(uint32_t cur, uint32_t next) {
@@ -1649,7 +1697,7 @@ __device__ __forceinline__ void p2_span(int lane, __amdgpu_buffer_rsrc_t rs, int
       uint32_t v;
       asm("v_xad_u32 %0, %1, %2, %3" : "=v"(v) : "v"(p), "v"(cur[u]), "s"(kneg - (uint32_t)u));
       __builtin_amdgcn_raw_buffer_store_b32(Mode == kP2Part ? twist_part(prev, v) : v, rs, lane * 4,
-                                            soff + u * row_bytes, 0);
+                                            soff + u * row_bytes, HZ_P2_AUX);
       if (KeepLds) l[(g + u) * S] = v;
       prev = v;
     }
@@ -1664,8 +1712,8 @@ __device__ __forceinline__ void p2_tail(int lane, __amdgpu_buffer_rsrc_t rs, int
 #pragma unroll
   for (int i = G; i < G1; i++) {
     const uint32_t v = (hz_lds[i * kLdsStride + lane] ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
-    if (Mode == kP2Part) __builtin_amdgcn_raw_buffer_store_b32(twist_part(prev, v), rs, lane * 4, (i - 1) * row_bytes, 0);
-    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, 0);
+    if (Mode == kP2Part) __builtin_amdgcn_raw_buffer_store_b32(twist_part(prev, v), rs, lane * 4, (i - 1) * row_bytes, HZ_P2_AUX);
+    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, lane * 4, i * row_bytes, HZ_P2_AUX);
     if (Mode == kP2Keep) hz_lds[i * kLdsStride + lane] = v;
     prev = v;
   }
@@ -1737,7 +1785,7 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
   } else if constexpr (K == 1) {
     static_assert(kAheadTwist + 1 - kP2aEnd == 16, "P2b's part steps: two groups");
     p2_span<kP2aEnd, kAheadTwist + 1, kP2Part>(lane, rs, row_bytes, prev, s_prog);  // parts of rows 208-223
-    __builtin_amdgcn_raw_buffer_store_b32(prev, rs, lane * 4, kAheadTwist * row_bytes, 0);  // row 224's final word
+    __builtin_amdgcn_raw_buffer_store_b32(prev, rs, lane * 4, kAheadTwist * row_bytes, HZ_P2_AUX);  // row 224's final word
     p2_span<kAheadTwist + 1, P1, kP2Final>(lane, rs, row_bytes, prev, s_prog);
     p2_put(pc1, lane);
     p2_load(pc2, slot, nr, b0, lane);
@@ -1759,8 +1807,8 @@ __device__ __forceinline__ void p2_third(const P2Args &a, int b0, int lane, int 
     p2_publish(s_prog, kMT);
     const uint32_t row1 = (first1 ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;  // the last step, at i = 1
     // mt[0] = 0x80000000 after init_by_array; row 1's next row is row 2
-    __builtin_amdgcn_raw_buffer_store_b32(f0 ^ twist_part(0x80000000u, row1), rs, lane * 4, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(f1 ^ twist_part(row1, row2), rs, lane * 4, row_bytes, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(f0 ^ twist_part(0x80000000u, row1), rs, lane * 4, 0, HZ_P2_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(f1 ^ twist_part(row1, row2), rs, lane * 4, row_bytes, HZ_P2_AUX);
   }
   if (K < 2) {
     if (ok) {
@@ -1798,7 +1846,13 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
   const int grp = lane >> 4, c4 = (lane & 15) * 4;
   uint32_t *col = slot + b0 + c4;
   auto row = [&](int r) { return *reinterpret_cast<const uint4 *>(col + (size_t)r * nr); };
-  auto store = [&](int r, const uint4 &v) { *reinterpret_cast<uint4 *>(col + (size_t)r * nr) = v; };
+  const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
+  const int row_bytes = __builtin_amdgcn_readfirstlane((int)(nr * 4));
+  auto store = [&](int r, const uint4 &v) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    // (r = grp + 4 i differs across the lane groups: per-lane voffset, no soffset)
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rs, c4 * 4 + r * row_bytes, 0, HZ_P2_AUX);
+  };
 #ifdef HZ_DIAG
   const int b = b0 + lane;
   const uint64_t tz = __builtin_amdgcn_s_memtime();
@@ -1939,16 +1993,16 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
       q[2] |= wd == 2 ? lo9 : wd == 1 ? hi9 : 0ull;
       q[3] |= wd == 3 ? lo9 : wd == 2 ? hi9 : 0ull;
       cc = d.m.cursor();
-      cur[(size_t)(i + 1) * nr] = cc;
+      p2_st(&cur[(size_t)(i + 1) * nr], cc);
       k = i + 1;
     }
   }
-  out.k[b] = k;
-  out.c[b] = cc;
-  out.bag[b] = bag;
+  p2_st(&out.k[b], k);
+  p2_st(&out.c[b], cc);
+  p2_st(&out.bag[b], bag);
 #pragma unroll
-  for (int i = 0; i < kAheadWords; i++) out.q[(size_t)i * nr + b] = q[i];
-  out.tag[b] = e * 8 + stage + 1;
+  for (int i = 0; i < kAheadWords; i++) p2_st(&out.q[(size_t)i * nr + b], q[i]);
+  p2_st(&out.tag[b], e * 8 + stage + 1);
 }
 
 // the rule hashes of D4's episode (read by the play stages in the next
@@ -1958,7 +2012,7 @@ __device__ __forceinline__ void p2_hashes(const P2Args &a, int b) {
   const int e = a.ep_in[b] + kP2Last - 8;
   const uint64_t rk = rule_key(episode_seed(a.seed_base, b, e));
 #pragma unroll 1
-  for (int j = 0; j < kRulePlies; j++) a.h_w[(size_t)j * nr + b] = rule_h32(rk, j);
+  for (int j = 0; j < kRulePlies; j++) p2_st(&a.h_w[(size_t)j * nr + b], rule_h32(rk, j));
   a.ht_w[b] = e;
 }
 
@@ -1982,17 +2036,17 @@ __device__ __forceinline__ void p2_draw(const P2Args &a, int blk, int y) {
 __device__ __forceinline__ void p2_mid_put(const P2Mid &m, size_t nr, int b, const State &s, const PlayDraw2 &d, int g,
                                            int e) {
 #pragma unroll
-  for (int k = 0; k < 4; k++) m.st[(size_t)k * nr + b] = s.pl[k];
-  m.st[4 * nr + b] = s.piles;
-  m.st[5 * nr + b] = s.misc;
-  m.q[b] = d.q0;
-  m.q[nr + b] = d.q1;
-  m.q[2 * nr + b] = d.q2;
-  m.q[3 * nr + b] = d.q3;
-  m.i[b] = d.d;
-  m.i[nr + b] = g;
-  m.i[2 * nr + b] = d.fell ? d.gm.cursor() : -1;
-  m.tag[b] = e;
+  for (int k = 0; k < 4; k++) p2_st(&m.st[(size_t)k * nr + b], s.pl[k]);
+  p2_st(&m.st[4 * nr + b], s.piles);
+  p2_st(&m.st[5 * nr + b], s.misc);
+  p2_st(&m.q[b], d.q0);
+  p2_st(&m.q[nr + b], d.q1);
+  p2_st(&m.q[2 * nr + b], d.q2);
+  p2_st(&m.q[3 * nr + b], d.q3);
+  p2_st(&m.i[b], d.d);
+  p2_st(&m.i[nr + b], g);
+  p2_st(&m.i[2 * nr + b], d.fell ? d.gm.cursor() : -1);
+  p2_st(&m.tag[b], e);
 }
 // the previous play stage's state; the draw source continues its script
 // (nd entries, cursors in `cur`) or the slot stream it fell onto
