@@ -1323,6 +1323,10 @@ constexpr int kP2Last = kP2Stages - 1;  // stage s works on episode ep + kP2Last
 constexpr int kP2Ring = kP2Play + 1;    // D4's scripts and the rule hashes: read by the play stages 1..kP2Play calls later
 constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: the last play stage's slot stays the board's stream)
 constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
+#ifndef HZ_P2_DCUT
+#define HZ_P2_DCUT 0, 6, 12, 18  // the draw stages' first draws (A/B builds)
+#endif
+constexpr int kP2DCut[4] = {HZ_P2_DCUT};
 constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
 constexpr int kP1Split = 313;
 #ifdef HZ_DIAG
@@ -1525,6 +1529,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t p2_slot_rsrc(uint32_t *slot, i
   const int bytes = __builtin_amdgcn_readfirstlane((int)((size_t)kMT * nr * 4 - (size_t)b0 * 4));
   return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
 }
+#ifndef HZ_P2_LDNT
+#define HZ_P2_LDNT 0  // 1: the stages' 16-B slot reads (staging, windows, the twist's rows) non-temporal (A/B builds)
+#endif
+__device__ __forceinline__ uint4 p2_ld4(const uint32_t *p) {
+  if constexpr (HZ_P2_LDNT) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_nontemporal_load((const v4u *)p);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  return *reinterpret_cast<const uint4 *>(p);
+}
 // a store read by another stage in a later call only: write-through (sc1)
 // like the slot stores (HZ_P2_AUX), so the kernel's end has no dirty lines
 // of it to write back
@@ -1638,7 +1653,7 @@ __device__ __forceinline__ void p2_load(P2Piece<R0, R1> &pc, const uint32_t *__r
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int r = R0 + 4 * u + (lane >> 4);
-    if (r < R1) pc.v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+    if (r < R1) pc.v[u] = p2_ld4(slot + (size_t)r * nr + b0 + c4);
   }
 }
 template <int R0, int R1>
@@ -1845,7 +1860,7 @@ __device__ __forceinline__ void p2_twist(const P2Args &a, int b0, int lane, bool
   uint32_t *slot = a.s_mt[4];
   const int grp = lane >> 4, c4 = (lane & 15) * 4;
   uint32_t *col = slot + b0 + c4;
-  auto row = [&](int r) { return *reinterpret_cast<const uint4 *>(col + (size_t)r * nr); };
+  auto row = [&](int r) { return p2_ld4(col + (size_t)r * nr); };
   const __amdgpu_buffer_rsrc_t rs = p2_slot_rsrc(slot, b0, nr);
   const int row_bytes = __builtin_amdgcn_readfirstlane((int)(nr * 4));
   auto store = [&](int r, const uint4 &v) {
@@ -1928,7 +1943,7 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
 #endif
   const bool act = b < a.n;
   const size_t nr = (size_t)a.nrow;
-  const int d0 = kP2DrawsPer * stage, d1 = stage == 3 ? a.draws : min(a.draws, d0 + kP2DrawsPer);
+  const int d0 = kP2DCut[stage], d1 = stage == 3 ? a.draws : min(a.draws, kP2DCut[stage + 1]);
   const int e = act ? a.ep_in[b] + kP2Last - 5 - stage : 0;
   const uint32_t *slot = a.s_mt[5 + stage];
   int32_t *cur = a.s_cur[5 + stage] + b;
@@ -1955,7 +1970,7 @@ __device__ __forceinline__ void p2_draw_stage(const P2Args &a, int b0, int lane,
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int r = r0 + 4 * u + (lane >> 4);
-      v[u] = *reinterpret_cast<const uint4 *>(slot + (size_t)r * nr + b0 + c4);
+      v[u] = p2_ld4(slot + (size_t)r * nr + b0 + c4);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
