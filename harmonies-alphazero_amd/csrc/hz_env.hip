@@ -1324,7 +1324,11 @@ constexpr int kP2Ring = kP2Play + 1;    // D4's scripts and the rule hashes: rea
 constexpr int kP2Stream = 14;     // stream slots (>= kP2Stages + 1: the last play stage's slot stays the board's stream)
 constexpr int kP2DrawsPer = 6;    // pile draws per draw stage (4 x 6 = kAheadDraws)
 #ifndef HZ_P2_DCUT
-#define HZ_P2_DCUT 0, 6, 12, 18  // the draw stages' first draws (A/B builds)
+// the draw stages' first draws: D1 0-6, D2 7-12, D3 13-17, D4 18-23.  With
+// six each, D3 was the longest stage (13.8 us against 10.5 for D1) once the
+// slot stores were written through: 19.37 vs 18.24 G env-steps/s, 13.2 vs
+// 14.1 us per launch (profiles/r05/p2_dcut; A/B builds -DHZ_P2_DCUT=...)
+#define HZ_P2_DCUT 0, 7, 13, 18
 #endif
 constexpr int kP2DCut[4] = {HZ_P2_DCUT};
 constexpr int kP2MinPlies = 96;   // hz_play max_plies from which pipeline 2 applies (rule games end by ply 80)
