@@ -382,8 +382,10 @@ class FoldedNet(nn.Module):
     # launch (hz_tower_x6_resident; 0 = always layered).  Measured per
     # predict (tools/resident_bench.py): 262 vs 402 us at 1 board, 986 vs
     # 1047 us at 1024; from 1536 the layered eight-state convs win (1066 vs
-    # 1488 us: weights shared by 8 states, off-board taps skipped)
-    resident_max = int(os.environ.get("HZ_RESIDENT_MAX", "1024"))  # (A/B measurements)
+    # 1488 us: weights shared by 8 states, off-board taps skipped).  Round 5
+    # (tools/rows_dist.py, profiles/r05/rows: the eight-state tower in one
+    # launch): 957 vs 979 us at 896, 1080 vs 990 us at 1024
+    resident_max = int(os.environ.get("HZ_RESIDENT_MAX", "896"))  # (A/B measurements)
     # ... and at most this many with 8 workgroups per state (hz_tower_x6_split)
     split_max = int(os.environ.get("HZ_SPLIT_MAX", "32"))
     # residual blocks above the one-state forms' batch limit: 1 (the default)
