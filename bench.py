@@ -83,6 +83,8 @@ def parse():
                     help="skip the chance-ahead-off comparison run (profiling)")
     ap.add_argument("--no-api-path", action="store_true",
                     help="config 2: skip the per-ply API path leg (reset / legal+rule+step per ply / score graphs)")
+    ap.add_argument("--no-api-caller", action="store_true",
+                    help="config 2: skip the api_caller leg (a Python caller's own moves through legal_actions/step)")
     ap.add_argument("--no-auto-reset", action="store_true",
                     help="config 2: skip the steady-state auto-reset leg (hz_rollout auto_reset launches)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"))
@@ -338,6 +340,9 @@ class TimedEvaluator:
 
     def __init__(self, pred, dev):
         self.pred = pred
+        # the fused (arrival-order) leaf gather exactly when the wrapped
+        # evaluator allows it (hzamd.mcts.BatchedMCTS.search)
+        self.row_independent = bool(getattr(pred, "row_independent", False))
         self.events = []
         self.mcts = None  # attach(): the BatchedMCTS whose searches call this evaluator
         self._base = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -1226,6 +1231,7 @@ def main():
         off_steps, off_elapsed = off_compare(env, one_launch, games, args, dev, world)
 
     api = None if args.no_api_path else api_path_leg(args, dev, rank, world)
+    caller = None if args.no_api_caller else api_caller_leg(args, dev, rank, world)
     auto = None if args.no_auto_reset else auto_reset_leg(args, dev, rank, world)
     enc = encoder_roofline(dev, n, args.seed_base) if rank == 0 else None
 
@@ -1312,6 +1318,7 @@ def main():
             "selfplay": sp,
         }
         out["api_path"] = api
+        out["api_caller"] = caller
         out["auto_reset"] = auto
         print(json.dumps(out))
     if args.no_selfplay:
@@ -1491,6 +1498,89 @@ def api_path_leg(args, dev, rank, world, plies=MAX_PLIES, reps=10):
                       "step counts of the timed episodes",
             "note": "one HIP graph per batch: hz_reset, then per ply hz_rule_ply (get_legal_moves -> rule pick -> "
                     "apply_move in one launch), then hz_score"}
+
+
+def api_caller_leg(args, dev, rank, world, plies=MAX_PLIES, reps=5):
+    """The caller-facing batched loop (harmonies_engine.py:145-298 through
+    process_game_state.py:156-179's action index), as a Python caller drives
+    it: reset every board with its episode's seed, then per ply
+    BatchedEnv.legal_actions() (the 143-bit masks, unpacked on the device)
+    -> the caller's own move, chosen OUTSIDE the env kernels with PyTorch ops
+    on a device tensor (uniform over the legal moves: a seeded device
+    generator's scores, masked, arg-max) -> BatchedEnv.step().  Eager launches
+    from a plain Python loop, no host read per ply; `plies` plies per batch
+    (finished boards get an empty mask and a no-op).  Every timed batch's
+    actions are kept and replayed by the C oracle from the same seeds: final
+    states bit-exact, no move rejected, every game over; env steps are the
+    moves applied."""
+    import numpy as np
+    import oracle
+    from hzamd.env import BatchedEnv
+    from hzamd.state import unpack_ref
+    n = args.boards
+    base = args.seed_base + rank * n
+    env = BatchedEnv(n, seed_base=base, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(20_251 + rank)
+    bidx = torch.arange(n, device=dev, dtype=torch.int64)
+    acts = torch.full((reps + 1, plies, n), -1, dtype=torch.int16, device=dev)
+    finals = torch.zeros(reps + 1, 6, n, dtype=torch.int64, device=dev)
+    none = torch.full((n,), -1, dtype=torch.int64, device=dev)
+
+    def batch(r):
+        env.reset(seeds=base + bidx + (r << 32))  # episode r of every board
+        for p in range(plies):
+            legal = env.legal_actions()                        # bool [n, 143] on the device
+            score = torch.rand(n, 143, device=dev, generator=gen)
+            score.masked_fill_(~legal, -1.0)
+            a = torch.where(legal.any(1), score.argmax(1), none)  # the caller's pick
+            acts[r, p] = a.to(torch.int16)
+            env.step(acts[r, p])
+        finals[r] = env.export_state()
+
+    batch(0)  # warm-up (allocator, first launches)
+    torch.cuda.synchronize(dev)
+    if dd():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for r in range(1, reps + 1):
+        batch(r)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    a_np = acts.cpu().numpy()
+    f_np = finals.cpu().numpy()
+    steps, bad, over = 0, 0, 0
+    for r in range(1, reps + 1):
+        seeds = (base + np.arange(n, dtype=np.uint64) + (np.uint64(r) << np.uint64(32))).astype(np.uint64)
+        total, ref, rej = oracle.replay_actions(seeds, a_np[r], nthreads=8)
+        got = f_np[r]
+        bad += int((rej != 0).sum()) + sum(1 for b in range(n) if not (unpack_ref(got[:, b]) == ref[b]).all())
+        over += sum(1 for b in range(n) if oracle.is_game_over(ref[b]))
+        steps += int(total)
+        assert total == int((a_np[r] >= 0).sum())
+    env.close()
+    resets = n * reps
+    if dd():
+        dt = all_reduce([dt], dist.ReduceOp.MAX)[0]
+        steps, resets, bad, over = (int(x) for x in all_reduce([steps, resets, bad, over], dist.ReduceOp.SUM))
+    assert bad == 0, f"api caller: {bad} boards differ from the C oracle's replay of the same actions"
+    assert over == resets, f"api caller: {resets - over} games not over after {plies} plies"
+    alg = steps * BYTES_PER_ENV_STEP + resets * BYTES_PER_RESET
+    gbs = alg / dt / 1e9
+    return {"env_steps_per_s": steps / dt, "games_per_s": resets / dt, "ms_per_batch": dt / reps * 1e3,
+            "boards": n, "plies_per_batch": plies, "batches_timed": reps,
+            "launches_per_ply": "hz_legal_mask + unpack (3) + rand + masked_fill + any + argmax + where + copy "
+                                "+ hz_step (~10 eager launches)",
+            "roofline": {"bound": "launch (a Python loop of ~10 eager launches per ply)",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "alg_bytes_per_batch": alg / reps / world,
+                         "basis": f"{BYTES_PER_ENV_STEP} B per env step + {BYTES_PER_RESET} B per reset over the "
+                                  "loop's wall time"},
+            "parity": f"every timed batch ({reps} x {world * n} games): the caller's recorded actions replayed by the "
+                      "C oracle (or_replay_actions) from the same seeds: final states bit-exact, 0 moves rejected, "
+                      "every game over",
+            "note": "legal_actions() -> the caller's own choice (PyTorch ops on a device tensor, seeded device "
+                    "generator) -> step(), one eager Python loop per batch; the fused rule path is api_path"}
 
 
 def auto_reset_leg(args, dev, rank, world, plies=MAX_PLIES, warmup=4, launches=40):

@@ -107,6 +107,7 @@ class _FoldedRows:
 
     device_rows = True
     capturable = True  # HIP kernels + PyTorch ops only: one simulation is replayed as a HIP graph
+    row_independent = True  # each row computed on its own (arrival-order leaf batches are fine)
 
     def __init__(self, folded):
         self.f = folded

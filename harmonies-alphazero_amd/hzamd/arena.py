@@ -74,6 +74,8 @@ class _Routed:
         self.eval_a, self.eval_b, self.a_rows = eval_a, eval_b, a_rows
         self.both_device = bool(getattr(eval_a, "device_rows", False) and getattr(eval_b, "device_rows", False))
         self.capturable = self.both_device and all(getattr(e, "capturable", False) for e in (eval_a, eval_b))
+        # agents are picked by rows[j], never by position
+        self.row_independent = all(getattr(e, "row_independent", False) for e in (eval_a, eval_b))
 
     def __call__(self, board, glob, rows=None, count=None):
         if rows is not None and self.both_device:

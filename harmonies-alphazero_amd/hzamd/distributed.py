@@ -81,16 +81,22 @@ def all_gather_records(rec, group=None):
 
 
 def broadcast_weights(model, src=0, group=None):
-    """Rank src's parameters and buffers to every rank (one flat tensor)."""
+    """Rank src's parameters and buffers to every rank: one flat tensor per
+    dtype, each in its own dtype (float32 weights travel as 4 B, not
+    upcast), so a broadcast moves exactly the state_dict's bytes."""
     tensors = [t for t in model.state_dict().values() if torch.is_tensor(t)]
-    flat = torch.cat([t.detach().reshape(-1).to(torch.float64) for t in tensors])
-    dist.broadcast(flat, src=src, group=group)
-    off = 0
-    with torch.no_grad():
-        for t in tensors:
-            k = t.numel()
-            t.copy_(flat[off:off + k].reshape(t.shape).to(t.dtype))
-            off += k
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                k = t.numel()
+                t.copy_(flat[off:off + k].reshape(t.shape))
+                off += k
 
 
 class ReplayBuffer:

@@ -7,7 +7,11 @@ batch (the reference evaluates one leaf at a time: MCTS.py:291-352).
 
 Like the reference, which calls predict only for non-terminal leaves
 (MCTS.py:297-341), each simulation's batch holds only the active boards
-whose selected leaf is not terminal, gathered in board order on the device.
+whose selected leaf is not terminal, gathered on the device: in board order
+(hz_mcts_gather_leaves), or, for an evaluator that declares
+`row_independent = True` (each output row a function of its input row
+alone, whatever its position or the batch size: the folded network, the
+stub), in arrival order by the fused expand/backup/select/gather launch.
 
 The evaluator is any callable (board f32[k,38,5,7], glob f32[k,42]) ->
 (policy f32[k,143] probabilities, value f32[k]) on the same device, e.g.
@@ -259,7 +263,10 @@ class BatchedMCTS:
             # (and, fuse_gather, the gather + encode of its leaf batch: the
             # two count buffers alternate, each zeroed by the launch after the
             # one that filled it, so both are zero between searches)
-            fuse_gather = self.fuse_gather
+            # rows in arrival order only for an evaluator that opts in: one
+            # that maps rows to boards by position, or whose results depend on
+            # a row's place in the batch, keeps the board-order gather
+            fuse_gather = self.fuse_gather and bool(getattr(evaluator, "row_independent", False))
             if fuse_gather:
                 self.count_b.zero_()  # (defensive: a search cut short may have left it set)
             board, glob, rows, count = self.select_gather(cpuct, active)
@@ -361,6 +368,10 @@ class BatchedPredictor:
         # the folded fp32 path is HIP kernels + PyTorch ops only: it can be
         # captured in a HIP graph (BatchedMCTS.search(graph=True))
         self.capturable = self.fast is not None and (dtype is None or dtype == torch.float32)
+        # the folded kernels compute every row on its own, in one summation
+        # order whatever the batch (test_predict_rows_do_not_depend_on_batch_size);
+        # the PyTorch/MIOpen path makes no such promise
+        self.row_independent = self.capturable
 
     def refresh(self):
         """Re-fold after the model's weights changed."""
@@ -399,3 +410,6 @@ def stub_evaluator(board, glob):
     pol = ((h >> 22) + 1).to(torch.float32) / 1024.0
     val = ((K % 255) - 127).to(torch.float64) / 128.0
     return pol, val.to(torch.float32)
+
+
+stub_evaluator.row_independent = True  # a function of each row alone

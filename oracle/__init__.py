@@ -69,6 +69,9 @@ def lib():
         L.or_play_rule_auto.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.or_play_rule_auto.restype = ctypes.c_int64
+        L.or_replay_actions.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.or_replay_actions.restype = ctypes.c_int64
         L.or_mcts_search.argtypes = [ctypes.c_void_p, P(MT), P(MctsCfg), ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.or_mcts_search.restype = ctypes.c_int
@@ -183,6 +186,21 @@ def play_rule_auto(n, seed_base, plies, ep0=0, nthreads=0):
     total = lib().or_play_rule_auto(n, ctypes.c_uint64(seed_base), int(ep0), int(plies), _p(finals), _p(games),
                                     _p(ep), nthreads)
     return total, finals, games, ep
+
+
+def replay_actions(seeds, actions, nthreads=0):
+    """Every board b reset after random.seed(seeds[b]) and then given
+    actions[p, b] for each ply p (negative = no-op; a rejected move leaves
+    the state unchanged).  Returns (moves applied, finals [n, 78], rejected
+    moves per board [n])."""
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    actions = np.ascontiguousarray(actions, np.int16)
+    plies, n = actions.shape
+    assert seeds.shape == (n,)
+    finals = np.zeros((n, REFSTATE), np.int16)
+    rejected = np.zeros(n, np.int32)
+    total = lib().or_replay_actions(n, _p(seeds), plies, _p(actions), _p(finals), _p(rejected), nthreads)
+    return total, finals, rejected
 
 
 def mcts_search(st, m, sims, cpuct, eps=0.25, testing=True, tau0=15, ply=0, u=0.0, noise=None,

@@ -654,7 +654,12 @@ int64_t or_play_rule_auto(int n, uint64_t seed_base, int ep0, int64_t plies, int
       uint8_t mask[143];
       while (left > 0 && !(s.game_over && s.winner != -2)) {
         int L = legal_of(&s, mask);
-        if (!L) break;
+        if (!L) {
+          /* stuck (no legal move, game not over): the kernel's auto-reset
+           * path stops such a board for the rest of the call, so does this */
+          left = 0;
+          break;
+        }
         uint64_t z = or_rule(seed, (uint64_t)ply);
         int k = (int)(((z >> 32) * (uint64_t)L) >> 32);
         step_state(&s, kth_legal(mask, k), &m);
@@ -669,6 +674,46 @@ int64_t or_play_rule_auto(int n, uint64_t seed_base, int ep0, int64_t plies, int
     if (finals) to_ref(&s, finals + (size_t)b * 78);
     if (games) games[b] = done;
     if (episode_out) episode_out[b] = e;
+  }
+  return total;
+}
+
+/* A caller's own moves replayed: board b starts HarmoniesGameState() after
+ * random.seed(seeds[b]) (harmonies_engine.py:66-79) and applies
+ * actions[p * n + b] for p < plies with apply_move (:210-298; a negative
+ * action is the batched step's no-op), the state kept unchanged on a
+ * rejected move like the reference's clone-then-commit.  finals: the last
+ * state; rejected[b]: the moves that were rejected.  Returns the moves
+ * applied. */
+int64_t or_replay_actions(int n, const uint64_t *seeds, int plies, const int16_t *actions, int16_t *finals,
+                          int32_t *rejected, int nthreads) {
+  geom_init();
+  int64_t total = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : total)
+#endif
+  for (int b = 0; b < n; b++) {
+    or_mt m;
+    or_mt_seed(&m, seeds[b]);
+    int16_t st[78];
+    or_reset(&m, st);
+    ostate s;
+    from_ref(st, &s);
+    int bad = 0;
+    for (int p = 0; p < plies; p++) {
+      int a = actions[(size_t)p * n + b];
+      if (a < 0) continue;
+      ostate t = s;
+      if (step_state(&t, a, &m) == 0) {
+        s = t;
+        total++;
+      } else {
+        bad++;
+      }
+    }
+    if (finals) to_ref(&s, finals + (size_t)b * 78);
+    if (rejected) rejected[b] = bad;
   }
   return total;
 }

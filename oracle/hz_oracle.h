@@ -58,6 +58,9 @@ int64_t or_play_rule_games_ep(int n, uint64_t seed_base, int episode, int16_t *f
  * ep0's reset, each ended game followed by the board's next episode. */
 int64_t or_play_rule_auto(int n, uint64_t seed_base, int ep0, int64_t plies, int16_t *finals, int32_t *games,
                           int32_t *episode_out, int nthreads);
+/* a caller's own moves replayed from random.seed(seeds[b]) resets (the api_caller leg's check) */
+int64_t or_replay_actions(int n, const uint64_t *seeds, int plies, const int16_t *actions, int16_t *finals,
+                          int32_t *rejected, int nthreads);
 
 /* MCTS (reference MCTS.py get_best_action_and_pi) with the deterministic stub
  * evaluator of tests/golden/make_golden.py, canonical (ascending action index)

@@ -28,7 +28,7 @@ def main(out, folder):
         # two runs of the loop over different backends end with the same
         # weights and the broadcast can be compared bit for bit
         torch.backends.cudnn.enabled = False
-        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.use_deterministic_algorithms(True)  # an op without a deterministic form raises here
     backend = os.environ.get("HZ_DIST_BACKEND", "gloo")  # "nccl" (RCCL): one rank only on a one-GPU box
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", 0))

@@ -175,6 +175,7 @@ def test_mcts_gathered_leaf_batch_matches_full_batch():
 
     class DeviceRows:
         device_rows = True
+        row_independent = True
 
         def __init__(self):
             self.calls = []
@@ -259,6 +260,7 @@ def test_fused_select_equals_separate_launches():
 
         class DeviceRows:
             device_rows = True
+            row_independent = True
 
             def __call__(self, board, glob, r, count):
                 rows.append(count.clone())
@@ -283,6 +285,43 @@ def test_fused_select_equals_separate_launches():
     assert int(out[0][5]) == int(out[0][2].sum())  # the eval counter holds every batch's rows
 
 
+def test_fused_gather_only_for_row_independent_evaluators():
+    """The fused gather hands rows over in arrival order, so search() takes it
+    only for an evaluator that declares row_independent; any other evaluator
+    (device rows or host rows) gets every batch in ascending board order, and
+    both searches give the same visits."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, sims = 300, 12
+    out = []
+    for indep in (False, True):
+        env = BatchedEnv(n, seed_base=515, device=DEV)
+        env.reset()
+        for p in range(18):
+            mask, count = env.legal_mask()
+            env.step(env.rule_actions(mask, count))
+        mcts = BatchedMCTS(env, sims)
+        assert mcts.fuse_select and mcts.fuse_gather
+        ordered = []
+
+        class DeviceRows:
+            device_rows = True
+            row_independent = indep
+
+            def __call__(self, board, glob, r, count):
+                k = int(count.item())
+                ordered.append(bool((r[1:k] > r[:k - 1]).all()) if k > 1 else True)
+                return stub_evaluator(board, glob)
+        v = mcts.search(DeviceRows(), 2.0, testing=True).clone()
+        out.append((v.cpu(), ordered))
+        mcts.close()
+        env.close()
+    (v0, ord0), (v1, ord1) = out
+    assert torch.equal(v0, v1)
+    assert all(ord0) and len(ord0) == sims
+    assert not all(ord1)  # arrival order somewhere (the fused gather ran)
+
+
 def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
     """BASELINE config 3's search at full size: 4096 boards at assorted game
     positions, 200 simulations, self-play settings (testing=False: the root
@@ -295,6 +334,7 @@ def test_mcts_4096_boards_200_sims_selfplay_config_vs_oracle():
 
     class DeviceRows:  # the stub on the device-row protocol (no host read per simulation)
         device_rows = True
+        row_independent = True
 
         def __call__(self, board, glob, rows, count):
             return stub_evaluator(board, glob)

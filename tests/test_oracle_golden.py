@@ -159,3 +159,29 @@ def test_play_rule_auto_matches_stepwise_loop():
                 break
             e += 1
         assert (finals[b] == s).all() and games[b] == done and ep[b] == e, b
+
+
+def test_replay_actions_matches_reference_traces():
+    """or_replay_actions (the api_caller leg's check: a caller's own moves
+    replayed from the same seeds) reproduces the reference's recorded games
+    from their action lists, with no-ops and rejected moves mixed in (a
+    rejected move leaves the state as it was, like the reference's
+    clone-then-commit)."""
+    f = load("env_traces.npz")
+    acts, off, seeds = f["actions"], f["offsets"], f["seeds"]
+    n = len(seeds)
+    lens = off[1:] - off[:-1]
+    T = int(lens.max())
+    clean = np.full((T, n), -1, np.int16)
+    for g in range(n):
+        clean[:lens[g], g] = acts[off[g]:off[g + 1]]
+    total, finals, rej = oracle.replay_actions(seeds.astype(np.uint64), clean)
+    assert total == int(lens.sum()) and (rej == 0).all()
+    assert (finals == f["finals"]).all()
+    # interleave no-op plies and an illegal action (142 never fits the
+    # opening's pile phase, and a pile index past the piles never fits later)
+    noisy = np.full((3 * T, n), -1, np.int16)
+    noisy[1::3] = clean
+    noisy[0, :] = 142
+    total2, finals2, rej2 = oracle.replay_actions(seeds.astype(np.uint64), noisy)
+    assert total2 == total and (rej2 == 1).all() and (finals2 == finals).all()
