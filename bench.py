@@ -47,6 +47,7 @@ BYTES_PER_RESET = 2564     # 624x4 B MT init + idx + 64 B state
 BYTES_PER_ENCODE = 5488    # f32 [38,5,7] + [42] written per state
 TREE_BYTES_POLICY = 576    # f32 [143] policy + value row read per evaluated leaf
 TREE_BYTES_CHILD = 88      # per expansion child: 64 B state + 16 B edge + 8 B hash slot
+TREE_BYTES_PATH = 16       # per edge level walked by a simulation (~16 B / path edge)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MAX_PLIES = 96             # rule games end after 56-72 plies
 # hz_play launches until every board replays a fully prepared episode, by
@@ -87,7 +88,8 @@ def parse():
                     help="config 2: skip the api_caller leg (a Python caller's own moves through legal_actions/step)")
     ap.add_argument("--no-auto-reset", action="store_true",
                     help="config 2: skip the steady-state auto-reset leg (hz_rollout auto_reset launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
+                    help="HBM bytes per launch from the counter passes (tools/traffic_r06.sh)")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="1: one game at a time through the drop-in modules (profile_self_play.py); "
                          "2: env kernels (default, the headline) + the selfplay sub-object; 3: MCTS self-play "
@@ -102,6 +104,8 @@ def parse():
     ap.add_argument("--sp-moves", type=int, default=3, help="selfplay sub-object: timed moves")
     ap.add_argument("--sp-cpu-seconds", type=float, default=8.0,
                     help="selfplay sub-object: bound of the one-thread C-twin sample (seconds x 4)")
+    ap.add_argument("--sp-steady-moves", type=int, default=80,
+                    help="selfplay sub-object: moves of the continuous (steady-state) leg, 0 = off")
     ap.add_argument("--sp-games", type=int, default=1,
                     help="selfplay sub-object: complete games timed on every board (0: estimate games/s from "
                          "the per-move leg)")
@@ -130,6 +134,35 @@ def parse():
 
 
 _RED_DEV = None  # device of reduction tensors: the GPU under RCCL, the CPU under gloo
+
+
+def traffic_entry(args, kernel):
+    """The counter passes' figures for one kernel (tools/traffic_r06.py:
+    bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE, and the kernel's mean
+    rocprof duration in the same command), or None."""
+    try:
+        with open(args.traffic_json) as f:
+            return json.load(f).get("kernels", {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def traffic_rate(entry, seconds_per_launch=None):
+    """Counter bytes per launch as a rate: over `seconds_per_launch` (a live
+    measurement of this run) when given, else over the counter run's own
+    rocprof mean duration."""
+    if not entry:
+        return None
+    b = entry["bytes_per_launch"]
+    t = seconds_per_launch if seconds_per_launch else entry.get("mean_ns", 0) * 1e-9
+    if not t:
+        return None
+    gbs = b / t / 1e9
+    return {"bytes_per_launch": b, "traffic_gbs": gbs, "traffic_frac": gbs / HBM_PEAK_GBS,
+            "over": "this run's live launch time" if seconds_per_launch else
+                    f"the counter run's rocprof mean ({entry.get('mean_ns', 0) / 1e3:.1f} us)",
+            "source": "profiles/r06/traffic.json (tools/traffic_r06.sh: FETCH_SIZE x2 + WRITE_SIZE, separate "
+                      "--pmc passes of one command)"}
 
 
 def all_reduce(vals, op):
@@ -347,6 +380,7 @@ class TimedEvaluator:
         self.mcts = None  # attach(): the BatchedMCTS whose searches call this evaluator
         self._base = torch.zeros(1, dtype=torch.int64, device=dev)
         self._ebase = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._pbase = torch.zeros(1, dtype=torch.int64, device=dev)
         self.calls = 0
         self.snap_at = None  # call index whose leaf batch + outputs are kept (device copies) for nn_guard
         self.snap = None
@@ -359,6 +393,7 @@ class TimedEvaluator:
     def attach(self, mcts):
         self.mcts = mcts
         mcts.count_edges = True  # expansion env steps counted on the device (edges_total)
+        mcts.count_path = True  # edge levels walked by the simulations (path_total)
 
     def __call__(self, board, glob, rows=None, count=None):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -385,12 +420,18 @@ class TimedEvaluator:
         """Expansion env steps (apply_move per legal child) since reset()."""
         return self.mcts.edges_total - self._ebase
 
+    @property
+    def path_edges(self):
+        """Edge levels walked by the simulations (select + backup) since reset()."""
+        return self.mcts.path_total - self._pbase
+
     def reset(self):
         torch.cuda.synchronize()
         self.events.clear()
         self.rowlog.clear()
         self._base = self.mcts.eval_rows_total.clone()
         self._ebase = self.mcts.edges_total.clone()
+        self._pbase = self.mcts.path_total.clone()
 
     def ms(self):
         return sum(a.elapsed_time(b) for a, b in self.events)
@@ -657,8 +698,9 @@ def selfplay_probe(args, dev, rank, world):
     # child its state, edge and hash slot), over the move time the network
     # does not take (select, expand, backup, gather + encode, noise, choice)
     edges = int(ev.edges.item())
+    path = int(ev.path_edges.item())
     tree_s = elapsed - nn_ms * 1e-3
-    tree_bytes = rows * (BYTES_PER_ENCODE + TREE_BYTES_POLICY) + edges * TREE_BYTES_CHILD
+    tree_bytes = rows * (BYTES_PER_ENCODE + TREE_BYTES_POLICY) + edges * TREE_BYTES_CHILD + path * TREE_BYTES_PATH
     tree_gbs = tree_bytes / tree_s / 1e9 if tree_s > 0 else None
     tree_roofline = {"bound": "latency (a wave per board walks, expands and backs up one path per simulation)",
                      "achieved": tree_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -666,13 +708,18 @@ def selfplay_probe(args, dev, rank, world):
                      "alg_bytes_per_move": tree_bytes / args.sp_moves,
                      "basis": f"{BYTES_PER_ENCODE} B encoded + {TREE_BYTES_POLICY} B policy/value read per "
                               f"evaluated leaf ({rows} rows), {TREE_BYTES_CHILD} B per expansion child (state, key "
-                              f"digest, edge, hash slot; {edges} children), over the timed moves' time minus the "
-                              "network's (the path walks' ~16 B per edge level are left out)"}
+                              f"digest, edge, hash slot; {edges} children), {TREE_BYTES_PATH} B per edge level "
+                              f"walked (select's read + backup's N/W update; {path} levels = the sum of the trees' "
+                              "edge visit counts, hz_mcts_path_edges), over the timed moves' time minus the "
+                              "network's",
+                     "path_edge_levels": path, "mean_path_depth": path / max(1, board_moves * sims),
+                     "traffic": traffic_rate(traffic_entry(args, "k_expand_backup<4, true, true, 16>"))}
     # the network's numerics in the measured run: rows of a timed leaf batch
     # against the checkpoint's network in float64 on the CPU
     nn_parity = nn_guard(ev, dev)
     # -- leg 2: complete games (+ config 4's exchange at N > 1)
     game = selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl) if args.sp_games > 0 else None
+    steady = selfplay_steady_leg(args, sp, ev, dev, rank, world, sims, fl) if args.sp_steady_moves > 0 else None
     # -- leg 3: the parity guard (every rank), with the CPU twin's timing
     guard = selfplay_guard(roots, active0, noise0, sims, dev, rank, world,
                            cpu_sample=rank == 0 and world == 1 and args.sp_cpu_seconds > 0,
@@ -703,7 +750,8 @@ def selfplay_probe(args, dev, rank, world):
                                         "product block, so their ceiling is the bf16 dense peak / 6 = "
                                         f"{emu_peak:.1f} TFLOP/s; fp32_mfma_frac is the same figure against the "
                                         f"f32 MFMA's dense peak ({FP32_MFMA_PEAK_TFLOPS} TFLOP/s), which this path "
-                                        "does not use"},
+                                        "does not use",
+                               "traffic": traffic_rate(traffic_entry(args, "k_x6w4_tower<true>"))},
                "tree_roofline": tree_roofline,
                "dtype": "fp32", "n_gpus": world, "network": ev.network, "parity": guard["parity"],
                "nn_parity": nn_parity}
@@ -715,6 +763,9 @@ def selfplay_probe(args, dev, rank, world):
                                            "ranks, over the slowest rank's time",
                         "game": game})
             out["exchange"] = game.get("exchange")
+        out["steady"] = steady
+        if steady is not None:
+            out["steady_games_per_s"] = steady["games_per_s"]
         else:
             out.update({"env_steps_per_s": env_all / elapsed,
                         "env_steps_basis": "per-move leg: expansion children + real moves",
@@ -801,6 +852,56 @@ def selfplay_games_leg(args, sp, ev, dev, rank, world, sims, fl):
             "nn_rows_skipped": moves_all * sims - rows_all, "nn_s_rank0": nn_ms * 1e-3,
             "nn_tflops_rank0": fl * rows / (nn_ms * 1e-3) / 1e12 if nn_ms else None,
             "nn_call_ms_rank0": nn_calls, "exchange": exchange}
+
+
+def selfplay_steady_leg(args, sp, ev, dev, rank, world, sims, fl):
+    """Leg 2b of the selfplay sub-object: continuous self-play
+    (SelfPlay.play_steady: the reference's self_play_worker run game after
+    game on every board, trainer.py:434-541; a board whose game ended starts
+    its next game, seeded by global id and game index, before the next move),
+    `sp_steady_moves` moves from a fresh reset, timed end to end.  Every
+    move searches all boards, so no leaf batch shrinks as games end.
+    games_per_s = board-moves per second / the mean length of the games that
+    ended in the run (the long-run rate of a renewal process: both factors
+    measured here); games_ended_per_s, the raw count over the same time, is
+    beside it (games still running when the window closes are not counted
+    there)."""
+    n, M = sp.n, args.sp_steady_moves
+    ev.reset()
+
+    def progress(m):  # a long run must not look hung
+        if m % 16 == 0:
+            print(f"[selfplay steady] rank {rank} move {m}", file=sys.stderr, flush=True)
+    if dd():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    rec = sp.play_steady(M, progress=progress)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ended = rec["ended"]
+    games = int(ended.sum().item())
+    plies = int(rec["plies"][ended].to(torch.int64).sum().item())
+    nn_ms, rows = ev.ms(), int(ev.rows.item())
+    edges = int(ev.edges.item())
+    moves = n * M
+    del rec
+    if dd():
+        dt = all_reduce([dt], dist.ReduceOp.MAX)[0]
+        games, plies, moves, rows, edges = (int(x) for x in all_reduce([games, plies, moves, rows, edges],
+                                                                          dist.ReduceOp.SUM))
+    if rank != 0:
+        return None
+    mean_len = plies / max(1, games)
+    return {"games_per_s": moves / dt / mean_len,
+            "basis": f"continuous self-play, {M} moves of every board from a fresh reset (finished boards start "
+                     "their next game before the next move): board-moves/s over the mean length of the games that "
+                     "ended in the run",
+            "seconds": dt, "moves_per_board": M, "board_moves_per_s": moves / dt, "games_ended": games,
+            "mean_game_plies": mean_len, "games_ended_per_s": games / dt, "sims_per_s": moves * sims / dt,
+            "env_steps_per_s": (edges + moves) / dt, "nn_rows_evaluated": rows,
+            "nn_rows_skipped": moves * sims - rows, "nn_s_rank0": nn_ms * 1e-3,
+            "nn_tflops_rank0": fl * rows / world / (nn_ms * 1e-3) / 1e12 if nn_ms else None}
 
 
 def selfplay_guard(roots, active, noise, sims, dev, rank, world, cpu_sample=False, one_core_s=2.0):
@@ -1209,6 +1310,7 @@ def main():
             traffic = json.load(open(args.traffic_json)).get(f"{kname}_bytes_per_launch")
         except Exception:
             traffic = None
+    tr = traffic_rate(traffic_entry(args, kname), kern_ms * 1e-3)
     cycles = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
     issue = {"kernel_cycles": cycles, "longest_game_plies": longest,
              "cycles_per_ply_longest_game": cycles / max(1, longest),
@@ -1293,6 +1395,10 @@ def main():
                        "games_per_step": timed_games / args.steps, "parallelism": f"shard{world}"},
             "roofline": {"bound": "latency (per-lane chains)", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_gbs": tr["traffic_gbs"] if tr else None,
+                         "traffic_frac": tr["traffic_frac"] if tr else None,
+                         "traffic_basis": "counter bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/r06/"
+                                          "traffic.json) over this run's kernel_ms" if tr else None,
                          "kernel": kname, "kernel_ms": kern_ms, "kernel_ms_launches": K,
                          "alg_bytes_per_launch": alg_bytes, "issue_bound": issue,
                          "bound_note": "priced against HBM (peak 8 TB/s), but the launch is bound by its serial "
@@ -1628,8 +1734,10 @@ def auto_reset_leg(args, dev, rank, world, plies=MAX_PLIES, warmup=4, launches=4
     assert bad == 0, f"auto-reset leg: {bad} boards differ from the C oracle"
     alg = timed_steps * BYTES_PER_ENV_STEP + timed_games * BYTES_PER_RESET
     gbs = alg / dt / 1e9
+    tr = traffic_rate(traffic_entry(args, "k_rollout<true, false>"), dt / launches)
     return {"env_steps_per_s": timed_steps / dt, "games_per_s": timed_games / dt,
             "ms_per_launch": dt / launches * 1e3, "launches_timed": launches, "plies_per_launch": plies,
+            "traffic": tr,
             "boards": n, "kernel": "k_rollout<true, false>",
             "roofline": {"bound": "latency (per-lane chains: plies and in-kernel seeding of the next episode)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,

@@ -1173,6 +1173,24 @@ bool alloc(T **p, size_t count) {
 
 }  // namespace
 
+namespace {
+// Sum of every edge's visit count over the board's tree: each simulation
+// adds one visit to every edge of its path in back_fill (MCTS.py:220-266),
+// so this is the number of edge levels the searches walked (the path-walk
+// term of the tree's algorithmic bytes).  Wave per board, one vector atomic.
+__global__ void __launch_bounds__(kWave) k_path_edges(hz_mcts m, unsigned long long *__restrict__ out) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int ne = m.counts[(size_t)b * 4 + 1];
+  const int32_t *en = m.edge_n + (size_t)b * m.max_edges;
+  unsigned long long acc = 0;
+  for (int e = lane; e < ne; e += kWave) acc += (unsigned)en[e];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, kWave);
+  if (lane == 0 && acc) atomicAdd(out, acc);
+}
+}  // namespace
+
 extern "C" {
 
 hz_mcts *hz_mcts_create(int32_t n_boards, int32_t max_nodes, int32_t max_depth, int32_t exact_keys, void *stream) {
@@ -1402,6 +1420,12 @@ int hz_mcts_diag_stamps(uint64_t *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_exp_stamps), sizeof(g_exp_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
+
+int hz_mcts_path_edges(hz_mcts *m, int64_t *out) {
+  if (!m || !out) return -1;
+  hipLaunchKernelGGL(k_path_edges, dim3(m->n), dim3(kWave), 0, m->stream, *m, (unsigned long long *)out);
+  return launch_err();
+}
 
 int hz_mcts_leaf_ptrs(hz_mcts *m, int32_t **leaf, int32_t **leaf_gidx) {
   if (!m) return -1;

@@ -67,6 +67,7 @@ _SIGS = {
                       _c.c_int),
     "hz_mcts_stats": ([_vp, _vp], _c.c_int),
     "hz_mcts_leaf_ptrs": ([_vp, _vp, _vp], _c.c_int),
+    "hz_mcts_path_edges": ([_vp, _vp], _c.c_int),
     "hz_bias_act": ([_vp, _vp, _vp, _c.c_int64, _c.c_int32, _vp], _c.c_int),
     "hz_conv3x3_bias_act": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_heads": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),

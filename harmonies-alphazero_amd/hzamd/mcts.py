@@ -74,6 +74,11 @@ class BatchedMCTS:
         # HZ_FUSE_GATHER=0 keeps hz_mcts_gather_leaves' separate launch)
         self.fuse_gather = os.environ.get("HZ_FUSE_GATHER", "1") != "0"
         self.edges_total = torch.zeros(1, dtype=torch.int64, device=d)
+        # count_path: after each search, the edge levels its simulations
+        # walked (the sum of the tree's edge visit counts, hz_mcts_path_edges)
+        # are added on the device to path_total (one small launch per search)
+        self.count_path = False
+        self.path_total = torch.zeros(1, dtype=torch.int64, device=d)
         self._nil_pol = torch.zeros(1, ACTION_SIZE, dtype=torch.float32, device=d)
         self._nil_val = torch.zeros(1, dtype=torch.float32, device=d)
 
@@ -319,6 +324,8 @@ class BatchedMCTS:
         self.eval_rows_total += self.eval_rows
         if self.count_edges:
             self.edges_total += self.stats()[:, 1].sum(dtype=torch.int64)
+        if self.count_path:
+            nat.check(nat.lib().hz_mcts_path_edges(self._h, nat.ptr(self.path_total)), "hz_mcts_path_edges")
         visits = self.result()
         check_split_timeouts(self.device)
         return visits

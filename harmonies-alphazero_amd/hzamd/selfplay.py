@@ -100,7 +100,10 @@ class SelfPlay:
         v = self.mcts.search(self.evaluator, cfg["cpuct"], active=active, noise=noise,
                              eps=cfg["dirichlet_epsilon"], testing=testing, max_rows=max(1, bound))
         self.check_steps()  # the previous move's step, done long before this search runs
-        explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
+        if torch.is_tensor(ply):
+            explore = (ply < cfg["turns_until_tau0"]) & (not testing)
+        else:
+            explore = torch.full((n,), (not testing) and ply < cfg["turns_until_tau0"], dtype=torch.bool, device=d)
         act = choose_actions(v, explore, u)
         if self.keep_noise:
             self.noise_log.append((noise.clone(), u.clone(), act.clone()))
@@ -161,6 +164,81 @@ class SelfPlay:
         final = env.export_state()
         return {"states": states[:ply], "players": players[:ply], "visits": visits[:ply],
                 "valid": valid[:ply], "final": final, "plies": ply}
+
+    def play_steady(self, moves, reset=True, progress=None):
+        """Continuous self-play: the reference's self_play_worker
+        (trainer.py:434-541) run game after game on every board, `moves`
+        moves in all.  A board whose game ended at a move starts its next
+        game before the following move (HarmoniesGameState() after
+        random.seed(seed_base + b + (k << 32)) for its k-th game, k = 0, 1,
+        ... per board: the seeds hz_rollout(auto_reset=1) uses), so every
+        board searches at every move and no leaf batch shrinks while games
+        end.  Each move's records keep the board's game index; z comes from
+        that game's outcome once it has ended (games still running at the
+        end give no examples; compact_steady()).  progress(move) is called
+        after each move (host side only)."""
+        env, n, d = self.env, self.n, self.device
+        bidx = torch.arange(n, device=d, dtype=torch.int64)
+        base = int(self.env.seed_base)
+        game = torch.zeros(n, dtype=torch.int64, device=d)
+        ply = torch.zeros(n, dtype=torch.int64, device=d)
+        if reset:
+            env.reset(seeds=base + bidx)
+        M = int(moves)
+        states = torch.zeros(M, 6, n, dtype=torch.int64, device=d)
+        visits = torch.zeros(M, n, 143, dtype=torch.int32, device=d)
+        games = torch.zeros(M, n, dtype=torch.int32, device=d)
+        ended = torch.zeros(M, n, dtype=torch.bool, device=d)
+        outcome = torch.zeros(M, n, dtype=torch.float32, device=d)
+        plies = torch.zeros(M, n, dtype=torch.int16, device=d)
+        none = torch.zeros(n, dtype=torch.bool, device=d)
+        for m in range(M):
+            self._n_active, self._n_active_epoch = n, env.epoch
+            st, v, _ = self.move(ply, none, _bound=n)
+            states[m] = st
+            visits[m] = v
+            games[m] = game.to(torch.int32)
+            fin = env.export_state()
+            over = env.done()
+            ended[m] = over
+            outcome[m] = torch.where(over, self.outcomes(fin), torch.zeros_like(outcome[m]))
+            plies[m] = (ply + 1).to(torch.int16)
+            # the boards whose game just ended start their next one (a
+            # selected-board reset: nothing moves where over is false)
+            game = game + over.to(torch.int64)
+            ply = torch.where(over, torch.zeros_like(ply), ply + 1)
+            env.reset(sel=over, seeds=base + bidx + (game << 32))
+            if progress is not None:
+                progress(m)
+        self.check_steps()
+        players = ((states[:, 5] >> 41) & 1).to(torch.int8)
+        return {"states": states, "visits": visits, "players": players, "game": games, "ended": ended,
+                "outcome": outcome, "plies": plies, "moves": M}
+
+    def compact_steady(self, rec):
+        """play_steady's records of the games that ended inside the run, in
+        (move, board) order: as compact() (states, visits, pi, z from the
+        recorded player's side, player, board), plus each record's game
+        index, and per ended game its length (`lengths`: plies)."""
+        M, n, d = rec["moves"], self.n, self.device
+        game = rec["game"].to(torch.int64)                         # [M, n]
+        K = int(game.max().item()) + 1 if M else 1
+        key = game * n + torch.arange(n, device=d).unsqueeze(0)    # (game, board)
+        res = torch.zeros(K * n, dtype=torch.float32, device=d)
+        has = torch.zeros(K * n, dtype=torch.bool, device=d)
+        em = rec["ended"]
+        res[key[em]] = rec["outcome"][em]
+        has[key[em]] = True
+        mask = has[key]                                            # records of ended games
+        player = rec["players"].to(torch.float32)
+        out = res[key]
+        z = torch.where(player == 0, out, -out)
+        states = rec["states"].permute(0, 2, 1)[mask]
+        visits = rec["visits"][mask]
+        board_id = torch.arange(n, device=d).expand(M, n)[mask].to(torch.int32)
+        return {"states": states.contiguous(), "visits": visits, "pi": pi_from_visits(visits),
+                "z": z[mask].contiguous(), "player": rec["players"][mask], "board": board_id,
+                "game": game[mask].to(torch.int32), "lengths": rec["plies"][em].to(torch.int64)}
 
     @staticmethod
     def outcomes(final):

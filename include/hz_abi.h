@@ -273,6 +273,11 @@ int hz_root_noise(const int32_t *count, int32_t n, uint64_t seed, uint64_t board
 int hz_mcts_result(hz_mcts *mcts, int32_t *visits);
 /* per-board [nodes, edges, search generation, overflow flag] -> counts[n][4] */
 int hz_mcts_stats(hz_mcts *mcts, int32_t *counts);
+/* out[0] (device int64) += the sum of every edge's visit count over every
+ * board's current tree, i.e. the edge levels its simulations walked (each
+ * back_fill, MCTS.py:220-266, visits every edge of its path once): the
+ * path-walk term of the tree kernels' algorithmic bytes (bench.py). */
+int hz_mcts_path_edges(hz_mcts *mcts, int64_t *out);
 /* host pointers to the device arrays leaf[n] / leaf_gidx[n] (debugging) */
 int hz_mcts_leaf_ptrs(hz_mcts *mcts, int32_t **leaf, int32_t **leaf_gidx);
 

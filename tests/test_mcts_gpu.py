@@ -447,3 +447,27 @@ def test_gather_encode_equals_layered_gather():
     assert k1 == k0 and k1 > 0
     assert torch.equal(v1, v0) and torch.equal(r1, r0)
     assert torch.equal(b1, b0) and torch.equal(g1, g0)
+
+
+def test_path_edges_counts_walked_levels():
+    """hz_mcts_path_edges adds the sum of the trees' edge visit counts: every
+    simulation after the first (which expands the root) walks at least one
+    edge, the second exactly one; so after 2 simulations the sum is the
+    number of active boards, and after S it lies in [S - 1, (S - 1) * depth]
+    per board with root visits summing to S - 1."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n = 200
+    env = BatchedEnv(n, seed_base=818, device=DEV)
+    env.reset()
+    mcts = BatchedMCTS(env, 24)
+    mcts.count_path = True
+    mcts.search(stub_evaluator, 2.0, sims=2)
+    assert int(mcts.path_total.item()) == n
+    mcts.path_total.zero_()
+    v = mcts.search(stub_evaluator, 2.0, sims=24)
+    tot = int(mcts.path_total.item())
+    assert int(v.sum().item()) == 23 * n
+    assert 23 * n < tot < 23 * n * 12
+    mcts.close()
+    env.close()

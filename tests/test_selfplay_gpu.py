@@ -148,3 +148,61 @@ def test_selfplay_split_invariant(net):
         assert torch.equal(part["states"], whole["states"][:T, :, sl])
         assert torch.equal(part["visits"], whole["visits"][:T, sl])
         assert torch.equal(part["final"], whole["final"][:, sl])
+
+
+@pytest.mark.parametrize("testing", [False, True])
+def test_selfplay_steady_matches_oracle_replay(testing):
+    """play_steady (continuous self-play: a finished board starts its next
+    game, seeded seed_base + b + (k << 32), before the next move) replayed
+    board by board by the oracle across game boundaries: every recorded
+    state, game index, visit vector, move, game end and outcome; then
+    compact_steady's examples (records of ended games only) carry the z
+    of the reference's self_play_worker (trainer.py:517-527)."""
+    from hzamd.mcts import stub_evaluator
+    from hzamd.selfplay import SelfPlay
+    n, base, sims, cpuct, tau0, M = 16, 4400, 6, 2.0, 15, 150
+    cfg = {"num_simulations": sims, "cpuct": cpuct, "testing": testing, "turns_until_tau0": tau0}
+    sp = SelfPlay(n, stub_evaluator, cfg, seed_base=base, device=DEV)
+    sp.keep_noise = True
+    rec = sp.play_steady(M)
+    states, visits = rec["states"].cpu().numpy(), rec["visits"].cpu().numpy()
+    game, ended = rec["game"].cpu().numpy(), rec["ended"].cpu().numpy()
+    outc = rec["outcome"].cpu().numpy()
+    log = [tuple(t.cpu().numpy() for t in x) for x in sp.noise_log]
+    assert len(log) == M
+    z_want, lengths, n_games = {}, [], 0
+    for b in range(n):
+        k, ply = 0, 0
+        m = oracle.mt_seed(base + b)
+        s = oracle.reset(m)
+        players = []
+        for mv in range(M):
+            assert game[mv, b] == k and (unpack_ref(states[mv, :, b]) == s).all(), (b, mv)
+            noise, u, act = log[mv]
+            a, ov, _, _ = oracle.mcts_search(s, m, sims, cpuct, testing=testing, tau0=tau0, ply=ply,
+                                             u=float(u[b]), noise=noise[b])
+            assert (visits[mv, b] == ov).all() and a == act[b], (b, mv)
+            players.append((mv, int(s[72])))
+            r, s = oracle.step(s, a, m)
+            assert r == 0
+            ply += 1
+            if oracle.is_game_over(s):
+                w = int(s[75])
+                o = 1.0 if w == 0 else -1.0 if w == 1 else 0.0
+                assert ended[mv, b] and outc[mv, b] == o, (b, mv)
+                for mm, p in players:
+                    z_want[(mm, b)] = o if p == 0 else -o
+                lengths.append(ply)
+                n_games += 1
+                players, k, ply = [], k + 1, 0
+                m = oracle.mt_seed(base + b + (k << 32))
+                s = oracle.reset(m)
+            else:
+                assert not ended[mv, b], (b, mv)
+    assert n_games >= 2 * n  # every board finished at least two games
+    comp = sp.compact_steady(rec)
+    order = sorted(z_want)  # (move, board): compact's order
+    assert comp["z"].shape[0] == len(order)
+    assert np.array_equal(comp["z"].cpu().numpy(), np.array([z_want[k] for k in order], np.float32))
+    assert np.array_equal(comp["board"].cpu().numpy(), np.array([b for _, b in order]))
+    assert sorted(comp["lengths"].cpu().tolist()) == sorted(lengths)
