@@ -394,6 +394,48 @@ struct MTS {
 };
 using MT = MTS<1>;
 
+// MT with a read-ahead window, for the one-draw-per-call kernels of the
+// per-ply surface (hz_step, hz_rule_ply): at the start of a draw, prefetch()
+// twists in place up to W words past the cursor (twist_block: one round trip
+// per 8 words) and loads those W words at once; the draw's picks then pop
+// them from a register queue (shifted, never indexed: a per-lane dynamic
+// index would put the window in scratch) instead of waiting one memory round
+// trip per word.  Past the window next() is MT's.  The words read and the
+// cursor left are MT's: a turn-ending ply no longer waits ~5 dependent loads.
+template <int W>
+struct WinGMT {
+  uint32_t* w;
+  int pos, tw, left;
+  uint32_t q[W];
+
+  __device__ __forceinline__ WinGMT(uint32_t* words, int cursor)
+      : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16), left(0) {}
+  __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
+
+  __device__ __forceinline__ void prefetch() {
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    while (tw < kMT && tw < pos + W) tw += twist_block(w, 1, tw);
+    left = tw - pos < W ? tw - pos : W;
+#pragma unroll
+    for (int j = 0; j < W; j++) q[j] = j < left ? w[pos + j] : 0u;
+  }
+
+  __device__ __forceinline__ uint32_t next() {
+    if (left > 0) {
+      const uint32_t v = q[0];
+#pragma unroll
+      for (int j = 0; j + 1 < W; j++) q[j] = q[j + 1];
+      left--;
+      pos++;
+      return temper(v);
+    }
+    if (pos >= kMT) { pos = 0; tw = 0; }
+    if (pos >= tw) tw += twist_block(w, 1, tw);
+    return temper(w[pos++]);
+  }
+};
+using WinMT12 = WinGMT<12>;
+
 // Dynamic LDS of the lane-per-board kernels: the wave's 64 streams as
 // [624][65] words (word i of lane l at i*65 + l).  Addressing through this
 // __shared__ symbol keeps every access a 32-bit LDS address.

@@ -65,6 +65,17 @@ struct hz_env {
   // materialize(), before any other entry point that reads streams)
   int32_t *mt_src;           // [n]
   int lazy;                  // some board may have mt_src >= 0
+  // auto-reset episodes prepared ahead (hz_rollout with auto_reset; see
+  // ar_prep_stage): slot s of board b holds one episode's pile script,
+  // cursors and stream, tagged with the episode; mt_src = kArSrc + s while a
+  // board plays on slot s's stream
+  int ar_ahead;              // on unless HZ_AR_AHEAD=0 / hz_env_set_auto_ahead(e, 0)
+  uint32_t *ar_mt;           // [kArSlots][n][624]
+  int32_t *ar_tag;           // [kArSlots][n] episode held (-1: none)
+  uint64_t *ar_pile;         // [kArSlots][kAheadWords][n]
+  int32_t *ar_cur;           // [kArSlots][kAheadDraws + 1][n]
+  int32_t *ar_ep[2];         // [n] episode counter at the start of an auto-reset call, by call parity
+  int ar_calls, ar_primed;
   // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
   // spread over thirteen consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
@@ -262,7 +273,7 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
     return;
   }
   State s = load_state(st, n, b);
-  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
+  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
@@ -346,7 +357,7 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
     if (status) status[b] = ST_NOOP;
     return;
   }
-  StreamDraw<MT> d{MT(mt + (size_t)b * kMT, pos[b])};
+  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
@@ -877,6 +888,75 @@ __device__ __forceinline__ void draw2_stage(int blk, Ring r2, size_t nrow, uint3
   stage_mt(out_mt + (size_t)b0 * kMT, nb, tid, actmask, false);
 }
 
+// ------------------------------------------------- auto-reset chance-ahead
+// hz_rollout(auto_reset = 1) plays every board on and on, starting its next
+// episode (seed_base + b + (e << 32)) whenever a game ends: about 1.5 game
+// ends per board per 96-ply call.  Seeding a stream is a 1,246-step serial
+// chain (~60 k cycles); in-kernel, the wave of a board whose game ended had
+// to wait for it.  As with hz_play's chance-ahead, a game's chance sequence
+// does not depend on its moves, so extra blocks of each auto-reset launch
+// prepare every board's episodes e0 + 2 and e0 + 3 (e0 = the board's episode
+// counter when the call starts: it starts e0 and at most e0 + 1 in the call
+// when it takes prepared ones) into a ring of four slots by episode: the
+// stream seeded and pre-twisted, its first kAheadDraws pile draws from the
+// initial bag run into a script with the cursor after each draw, the stream
+// after them.  A board whose game ends then starts episode e from slot e & 3
+// when the slot's tag says e (prepared by an earlier call: this call's blocks
+// write slots e0 + 2, e0 + 3, never the ones it reads) and e - e0 < 2: a
+// scripted reset, no chain, no wait for the rest of the wave; otherwise it
+// seeds in place as before.  A slot is tagged only when none of its draws
+// twisted past the pre-twisted rows, so the stream as stored and every cursor
+// agree (materialize copies it to the board's own stream after the call).
+// The preparation only decides where a board's chance draws come from, never
+// what they are: results are the same with it off (hz_env_set_auto_ahead).
+constexpr int kArSlots = 4;
+constexpr int kArSrc = 16;  // mt_src codes kArSrc + slot (0, 1: pipeline 1; 2..15: pipeline 2)
+struct ArArgs {
+  uint32_t *mt;          // [kArSlots][n][624]
+  int32_t *tag;          // [kArSlots][n]
+  uint64_t *pile;        // [kArSlots][kAheadWords][n]
+  int32_t *cur;          // [kArSlots][kAheadDraws + 1][n]
+  const int32_t *ep_in;  // [n] the counters the previous call ended with (the preparing blocks' e0)
+  int on;
+};
+
+__device__ __forceinline__ void ar_prep_stage(int blk, int k, const ArArgs &ar, int n, uint64_t seed_base) {
+  __shared__ uint64_t s_ar_mask[kArSlots];
+  const int tid = threadIdx.x, lane = tid & 63, b0 = blk * kBlock, b = b0 + lane;
+  const bool act = b < n;
+  const int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  const int e = act ? ar.ep_in[b] + 2 + k : 0;
+  const int sl = e & (kArSlots - 1);
+  const bool need = act && ar.tag[(size_t)sl * n + b] != e;  // (prepared by an earlier call: kept)
+  if (tid < 64) {
+#pragma unroll
+    for (int q = 0; q < kArSlots; q++) {
+      const uint64_t m = __ballot(need && sl == q);
+      if (lane == 0) s_ar_mask[q] = m;
+    }
+    if (need) {
+      seed_in_lds(lane, episode_seed(seed_base, b, e));
+      uint64_t bag = initial_bag(), q[kAheadWords] = {};
+      int32_t *cur = ar.cur + (size_t)sl * (kAheadDraws + 1) * n + b;
+      cur[0] = kMTAhead;
+      StreamDraw<LdsMT> d{LdsMT(lane, kMTAhead)};
+      run_script(d, bag, q, cur, n, 0, kAheadDraws);
+      // the stored stream matches every cursor only if no draw twisted past
+      // the pre-twisted rows (a bag of >= 48 tiles: in practice never)
+      const bool clean = d.m.tw == kAheadTwist;
+#pragma unroll
+      for (int w = 0; w < kAheadWords; w++) ar.pile[((size_t)sl * kAheadWords + w) * n + b] = q[w];
+      ar.tag[(size_t)sl * n + b] = clean ? e : -1;
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int q = 0; q < kArSlots; q++) {
+    const uint64_t m = s_ar_mask[q];
+    if (m) stage_mt(ar.mt + ((size_t)q * n + b0) * kMT, nb, tid, m, false);
+  }
+}
+
 // AutoReset / Record are template parameters so that the common variant
 // (play to the end, no trajectory) has a plain loop: no reset path, no
 // record stores, fewer live scalar values across the ply loop.
@@ -899,7 +979,7 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
                                                     const int32_t *__restrict__ prep_ep, Ring rs, Ring r1,
                                                     Ring r2, long nrow, const uint32_t *__restrict__ ahead_rule,
                                                     uint32_t *__restrict__ prep_rule, int32_t *__restrict__ mt_src,
-                                                    int src_slot) {
+                                                    int src_slot, ArArgs ar) {
 #ifdef HZ_DIAG
   uint64_t role_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -907,6 +987,12 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     int blk = (int)blockIdx.x - nblk;
     int role = blk / nblk;
     blk -= role * nblk;
+    if constexpr (AutoReset && !Record) {
+      if (ar.on) {  // hz_rollout's auto-reset preparation: episodes e0 + 2 (role 0), e0 + 3 (role 1)
+        ar_prep_stage(blk, role, ar, n, seed_base);
+        return;
+      }
+    }
 #ifdef HZ_PREP_DELAY
     if (role < 2) __builtin_amdgcn_s_sleep(HZ_PREP_DELAY);
 #endif
@@ -1000,6 +1086,10 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     State s;
     int g_ply, games = 0, steps = 0;
     uint64_t sd, rkey;
+    // where the lane's scripted stream lives: the play slot of a prepared
+    // hz_play episode, or an auto-reset slot (set below when one is taken)
+    const int32_t *cur_b = ahead_cur ? ahead_cur + b : nullptr;
+    int src_b = src_slot;
     if (reset_first) {
       int e = ep0;
       sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
@@ -1045,6 +1135,37 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
       int n_pass = 0, n_iter = 0;
 #endif
       while (true) {
+        if constexpr (!Record) {
+          // a prepared episode (ar_prep_stage): a scripted reset at once, the
+          // lane's own, with no seeding pass for the wave to wait for
+          if (ar.on && phase_of(s.misc) == PH_OVER && !stuck && used < max_plies) {
+            const int e = episode[b];
+            const int sl = e & (kArSlots - 1);
+            if (e - ep0 < 2 && ar.tag[(size_t)sl * n + b] == e) {
+              if (score_pending(s.misc)) finish_game(s);  // the finished game is scored all the same
+              const uint64_t *pq = ar.pile + (size_t)sl * kAheadWords * n + b;
+              draw.q0 = pq[0];
+              draw.q1 = pq[(size_t)n];
+              draw.q2 = pq[(size_t)2 * n];
+              draw.q3 = pq[(size_t)3 * n];
+              draw.scripted = true;
+              draw.fell = false;
+              draw.d = 0;
+              draw.nd = kAheadDraws;
+              draw.gm = MT(ar.mt + ((size_t)sl * n + b) * kMT, 0);
+              cur_b = ar.cur + (size_t)sl * (kAheadDraws + 1) * n + b;
+              draw.cur_tail = cur_b + (size_t)kAheadDraws * n;
+              src_b = kArSrc + sl;
+              sd = seed_base + (uint64_t)b + ((uint64_t)e << 32);
+              rkey = rule_key(sd);
+              episode[b] = e + 1;
+              lds_used = false;
+              pre = false;
+              draw.scripted_reset(s);
+              g_ply = 0;
+            }
+          }
+        }
         const bool over = phase_of(s.misc) == PH_OVER;
         const bool can = !over && !stuck && used < max_plies;
 #ifdef HZ_DIAG_ROLES_ONLY
@@ -1239,8 +1360,8 @@ __global__ void __launch_bounds__(kStageThreads) k_rollout(uint64_t *__restrict_
     store_state(st, n, b, s);
     if (lds_used) pos[b] = draw.m.cursor();
     else if (draw.fell) pos[b] = draw.gm.cursor();
-    else pos[b] = ahead_cur[(size_t)draw.d * n + b];
-    mt_src[b] = lds_used ? -1 : src_slot;
+    else pos[b] = cur_b[(size_t)draw.d * n];
+    mt_src[b] = lds_used ? -1 : src_b;
     ply[b] = g_ply;
     seed[b] = sd;
 #if defined(HZ_DIAG) && !defined(HZ_DIAG_ROLES_ONLY)
@@ -2331,8 +2452,27 @@ __global__ void __launch_bounds__(64) k_mt_materialize(uint32_t *__restrict__ mt
   if (lane == 0) mt_src[b] = -1;
 }
 
+// boards whose stream lives in an auto-reset slot (mt_src = kArSrc + slot)
+__global__ void __launch_bounds__(64) k_mt_materialize_ar(uint32_t *__restrict__ mt, const uint32_t *__restrict__ ar_mt,
+                                                         int32_t *__restrict__ mt_src, int n) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int src = mt_src[b];
+  if (src < kArSrc || src >= kArSrc + kArSlots) return;
+  const uint32_t *from = ar_mt + ((size_t)(src - kArSrc) * n + b) * kMT;
+  uint32_t *to = mt + (size_t)b * kMT;
+  uint32_t v[(kMT + 63) / 64];
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++) v[k] = lane + 64 * k < kMT ? from[lane + 64 * k] : 0u;
+#pragma unroll
+  for (int k = 0; k < (kMT + 63) / 64; k++)
+    if (lane + 64 * k < kMT) to[lane + 64 * k] = v[k];
+  if (lane == 0) mt_src[b] = -1;
+}
+
 static int materialize(hz_env *e) {
   if (!e->lazy) return 0;
+  if (e->ar_mt)
+    hipLaunchKernelGGL(k_mt_materialize_ar, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ar_mt, e->mt_src, e->n);
   hipLaunchKernelGGL(k_mt_materialize, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ahead_mt[0], e->ahead_mt[1],
                      e->mt_src, e->n);
   if (e->p2_s[0]) {
@@ -2506,6 +2646,7 @@ static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32
   e->lazy = 1;
   e->calls2 = (c + 1) % (kP2Stream * kP2Ring * 2);  // (a multiple of every ring length)
   e->primed = 0;  // the other pipeline's episode prediction is stale now
+  e->ar_primed = 0;
   return 0;
 }
 
@@ -2573,6 +2714,10 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
   }
   ok = ok && hipDeviceSynchronize() == hipSuccess;
   e->seed_ahead = kAheadDraws;
+  {
+    const char *av = getenv("HZ_AR_AHEAD");
+    e->ar_ahead = av && atoi(av) == 0 ? 0 : 1;
+  }
   {  // hz_play's pipeline: 2 by default, HZ_PIPELINE=1 for the first (hz_env_set_pipeline)
     const char *pv = getenv("HZ_PIPELINE");
     e->pipeline = pv && atoi(pv) == 1 ? 1 : 2;
@@ -2618,6 +2763,12 @@ void hz_env_destroy(hz_env *e) {
     if (e->ring_cur[k]) (void)hipFree(e->ring_cur[k]);
     if (e->ring_k1[k]) (void)hipFree(e->ring_k1[k]);
   }
+  if (e->ar_mt) (void)hipFree(e->ar_mt);
+  if (e->ar_tag) (void)hipFree(e->ar_tag);
+  if (e->ar_pile) (void)hipFree(e->ar_pile);
+  if (e->ar_cur) (void)hipFree(e->ar_cur);
+  for (int k = 0; k < 2; k++)
+    if (e->ar_ep[k]) (void)hipFree(e->ar_ep[k]);
   if (e->state) (void)hipFree(e->state);
   if (e->mt) (void)hipFree(e->mt);
   if (e->pos) (void)hipFree(e->pos);
@@ -2647,6 +2798,13 @@ int hz_env_set_pipeline(hz_env *e, int32_t pipeline) {
   e->pipeline = pipeline;
   e->primed = 0;
   e->primed2 = 0;
+  return 0;
+}
+
+int hz_env_set_auto_ahead(hz_env *e, int32_t on) {
+  if (!e) return -1;
+  e->ar_ahead = on ? 1 : 0;
+  e->ar_primed = 0;
   return 0;
 }
 
@@ -2682,6 +2840,7 @@ int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   if (int err = materialize(e)) return err;  // unselected boards keep their streams
   e->primed = 0;  // episode counters move outside hz_play's plan
   e->primed2 = 0;
+  e->ar_primed = 0;
   hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
   return launch_err();
@@ -2735,6 +2894,35 @@ int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_greedy, dim3(e->n), dim3(64), 0, e->stream, e->state, e->mt, e->pos, e->n, sel, action);
   return launch_err();
+}
+
+// auto-reset preparation slots, allocated at the first auto-reset hz_rollout
+// (40 MB of streams at 4096 boards)
+static int alloc_ar(hz_env *e) {
+  if (e->ar_mt) return 0;
+  const size_t n = (size_t)e->n;
+  bool ok = hipMalloc(&e->ar_mt, kArSlots * n * kMT * sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc(&e->ar_tag, kArSlots * n * sizeof(int32_t)) == hipSuccess &&
+            hipMalloc(&e->ar_pile, kArSlots * kAheadWords * n * sizeof(uint64_t)) == hipSuccess &&
+            hipMalloc(&e->ar_cur, kArSlots * (kAheadDraws + 1) * n * sizeof(int32_t)) == hipSuccess &&
+            hipMalloc(&e->ar_ep[0], n * sizeof(int32_t)) == hipSuccess &&
+            hipMalloc(&e->ar_ep[1], n * sizeof(int32_t)) == hipSuccess &&
+            hipMemsetAsync(e->ar_tag, 0xff, kArSlots * n * sizeof(int32_t), e->stream) == hipSuccess;
+  if (!ok) {
+    auto f = [](auto *&p) {
+      if (p) (void)hipFree((void *)p);
+      p = nullptr;
+    };
+    f(e->ar_mt);
+    f(e->ar_tag);
+    f(e->ar_pile);
+    f(e->ar_cur);
+    f(e->ar_ep[0]);
+    f(e->ar_ep[1]);
+    return 1;
+  }
+  e->ar_primed = 0;
+  return 0;
 }
 
 // hz_play's chance-ahead pipeline: one launch per call c.  Blocks [0, nblk)
@@ -2793,6 +2981,26 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
     e->primed = 0;
   }
   bool rec = traj_state || traj_mask || traj_action;
+  // hz_rollout with auto-reset: episodes prepared ahead (ar_prep_stage) by
+  // 2 x nblk extra blocks; the playing blocks leave the counters they end
+  // with for the next call's preparing blocks (ep_final)
+  ArArgs ar{};
+  const bool ar_on = auto_reset && !reset_first && !rec && e->ar_ahead;
+  if (ar_on) {
+    if (alloc_ar(e)) return 1;
+    const int ar_r = e->ar_calls & 1;
+    if (!e->ar_primed) {
+      if (hipMemcpyAsync(e->ar_ep[ar_r], e->episode, (size_t)e->n * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                         e->stream))
+        return 1;
+      e->ar_primed = 1;
+    }
+    ar = ArArgs{e->ar_mt, e->ar_tag, e->ar_pile, e->ar_cur, e->ar_ep[ar_r], 1};
+    ep_final = e->ar_ep[ar_r ^ 1];
+    grid = 3 * nblk;
+  } else {
+    e->ar_primed = 0;  // episode counters move outside the auto-reset plan
+  }
   auto kern = auto_reset ? (rec ? k_rollout<true, true> : k_rollout<true, false>)
                          : (rec ? k_rollout<false, true> : k_rollout<false, false>);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos, e->ply,
@@ -2800,10 +3008,14 @@ static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int 
                      traj_mask, traj_action, games_done, steps_done, ahead_mt, ahead_tag, ahead_pile, ahead_cur,
                      e->seed_ahead, ep_final, nblk, e->ahead_mt[w], e->ahead_tag[w], e->ahead_pile[w],
                      e->ahead_cur[w], e->ep_final[w], ring(c3), ring((c3 + 2) % kRing), ring((c3 + 1) % kRing),
-                     (long)e->nrow, ahead_rule, e->ahead_rule[w], e->mt_src, ahead_mt ? r : -1);
+                     (long)e->nrow, ahead_rule, e->ahead_rule[w], e->mt_src, ahead_mt ? r : -1, ar);
   int err = launch_err();
   if (err) return err;
   if (ahead_mt) e->lazy = 1;
+  if (ar_on) {
+    e->lazy = 1;
+    e->ar_calls++;
+  }
   if (pipe) {
     e->slot_valid[w] = 1;
     e->calls++;

@@ -995,10 +995,17 @@ __device__ __forceinline__ float4 x6_ld4f(const float *p) {
   }
   return *(const float4 *)p;
 }
+// Tower: from the second block on, x and out are the same buffer (the skip
+// input is the block input, overwritten by the block's output), so they are
+// not declared __restrict__ there
+template <bool Tower>
+using X6In = std::conditional_t<Tower, const float *, const float *__restrict__>;
+template <bool Tower>
+using X6Out = std::conditional_t<Tower, float *, float *__restrict__>;
 template <bool Block, bool Cf, bool Tower>
-__device__ __forceinline__ void x6w4_body(const float *__restrict__ x, const bf16x8 *__restrict__ wp,
-                                          const float *__restrict__ bias, const float *__restrict__ res,
-                                          float *__restrict__ out, int32_t batch, const int32_t *__restrict__ live,
+__device__ __forceinline__ void x6w4_body(X6In<Tower> x, const bf16x8 *__restrict__ wp,
+                                          const float *__restrict__ bias, X6In<Tower> res,
+                                          X6Out<Tower> out, int32_t batch, const int32_t *__restrict__ live,
                                           const bf16x8 *__restrict__ wp2, const float *__restrict__ bias2,
                                           float *__restrict__ tmp) {
   constexpr int NQ = 4, kRBT = 9, NCB = 4, NG = Block ? 8 : 4;
@@ -1420,11 +1427,19 @@ struct X6Tower {
   const bf16x8 *w1[kTowerMax], *w2[kTowerMax];
   const float *b1[kTowerMax], *b2[kTowerMax];
   int32_t nblk;
+  int32_t stagger;  // A/B knob (hz_tower_x6_set_stagger): first-round start delay, units of 8,128 cycles
+  int32_t round;    // workgroups of the first round (the CU count)
 };
 template <bool Cf>
 __global__ void __launch_bounds__(256, 1)
     k_x6w4_tower(const float *__restrict__ x, float *out, int32_t batch, const int32_t *__restrict__ live,
                  float *__restrict__ tmp, X6Tower tw) {
+  // every first-round workgroup starts together, so their epilogues (a
+  // residual load and store burst of every CU at once) coincide; a start
+  // delay on every other CU of each XCD shifts half of them by part of a
+  // block (the second round inherits the shift)
+  if (tw.stagger > 0 && (int)blockIdx.x < tw.round && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < tw.stagger; i++) __builtin_amdgcn_s_sleep(127);
 #pragma unroll 1
   for (int k = 0; k < tw.nblk; k++) {
     x6w4_body<true, Cf, true>(k == 0 ? x : out, tw.w1[k], tw.b1[k], nullptr, out, batch, live, tw.w2[k], tw.b2[k],
@@ -1619,6 +1634,27 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
 // as nblk hz_resblock_x6_bias_act calls.  -2: this batch takes the
 // per-block path (hz_resblock_x6_fused(batch) == 0).
 extern "C" int32_t hz_resblock_x6_fused(int32_t batch);
+static std::atomic<int32_t> g_tower_stagger{0};
+static int32_t tower_round() {  // the device's CU count: workgroups of the tower's first round
+  static std::atomic<int32_t> cus{0};
+  int32_t v = cus.load(std::memory_order_relaxed);
+  if (!v) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      v = n;
+    else
+      v = 256;
+    cus.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+// A/B knob (no reference counterpart): the tower launch's stagger (above)
+extern "C" int hz_tower_x6_set_stagger(int32_t units) {
+  if (units < 0 || units > 1000) return -1;
+  g_tower_stagger.store(units, std::memory_order_relaxed);
+  return 0;
+}
 extern "C" int hz_tower_x6_blocks(const float *x, const void *const *w1, const float *const *b1,
                                   const void *const *w2, const float *const *b2, int32_t nblk, float *out,
                                   float *tmp, int32_t batch, const int32_t *live, void *stream) {
@@ -1635,6 +1671,8 @@ extern "C" int hz_tower_x6_blocks(const float *x, const void *const *w1, const f
     tw.b2[k] = b2[k];
   }
   tw.nblk = nblk;
+  tw.stagger = g_tower_stagger.load(std::memory_order_relaxed);
+  tw.round = tower_round();
   return x6_blk_cf() ? launch_x6w4_tower<true>(x, out, tmp, tw, batch, live, stream)
                      : launch_x6w4_tower<false>(x, out, tmp, tw, batch, live, stream);
 }
@@ -2391,7 +2429,15 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   __shared__ float4 vin[kVIn][kHS / 4];
   __shared__ float lg[kHS][kAct + 1];
   __shared__ float vpart[4][kHS];
-  __shared__ float hpart[kHS * 35 * 8][3];  // the 1x1 convs' partial sums per 16-channel group
+  // the 1x1 convs' partial sums per 16-channel group, [filter][group][state
+  // cell] with a row stride of 292 = 4 mod 32 words: the writers (item i =
+  // 8 (state cell) + group, consecutive lanes) and the readers (one state
+  // cell per lane, groups in order) both touch 32 distinct banks per 32 lanes
+  // (round 5's [item][filter] layout read at a 24-word lane stride: 8-way
+  // conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.37)
+  constexpr int kHpRow = 292;
+  static_assert(kHpRow >= kHS * 35 && kHpRow % 32 == 4, "hpart row stride");
+  __shared__ float hpart[3][8][kHpRow];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (live) batch = *live < batch ? *live : batch;
   const int s0 = blockIdx.x * kHS;
@@ -2442,9 +2488,9 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
           e1 += v[0] * q.x + v[1] * q.y + v[2] * q.z + v[3] * q.w;
           e2 += v[0] * r.x + v[1] * r.y + v[2] * r.z + v[3] * r.w;
         }
-        hpart[i][0] = e0;
-        hpart[i][1] = e1;
-        hpart[i][2] = e2;
+        hpart[0][kk][i >> 3] = e0;
+        hpart[1][kk][i >> 3] = e1;
+        hpart[2][kk][i >> 3] = e2;
       }
     }
     __syncthreads();
@@ -2454,9 +2500,9 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 8; kk++) {
-        a0 += hpart[8 * i + kk][0];
-        a1 += hpart[8 * i + kk][1];
-        a2 += hpart[8 * i + kk][2];
+        a0 += hpart[0][kk][i];
+        a1 += hpart[1][kk][i];
+        a2 += hpart[2][kk][i];
       }
       a0 += h0, a1 += h1, a2 += h2;
       ((float *)pin[cell])[sl] = a0 > 0.f ? a0 : 0.f;

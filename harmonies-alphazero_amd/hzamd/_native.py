@@ -40,6 +40,7 @@ _SIGS = {
     "hz_rollout": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_play": ([_vp, _c.c_int32, _c.c_int32, _vp, _vp, _vp, _vp, _vp], _c.c_int),
     "hz_env_set_seed_ahead": ([_vp, _c.c_int32], _c.c_int),
+    "hz_env_set_auto_ahead": ([_vp, _c.c_int32], _c.c_int),
     "hz_env_set_pipeline": ([_vp, _c.c_int32], _c.c_int),
     "hz_env_set_error_word": ([_vp, _vp], _c.c_int),
     "hz_env_set_spin_limit": ([_vp, _c.c_int32], _c.c_int),
@@ -78,6 +79,7 @@ _SIGS = {
     "hz_resblock_x6_fused": ([_c.c_int32], _c.c_int32),
     "hz_resblock_x6_set_fused": ([_c.c_int32], _c.c_int),
     "hz_resblock_x6_set_table": ([_c.c_int32], _c.c_int),
+    "hz_tower_x6_set_stagger": ([_c.c_int32], _c.c_int),
     "hz_tower_x6_blocks": ([_vp, _vp, _vp, _vp, _vp, _c.c_int32, _vp, _vp, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_resident": ([_vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),
     "hz_tower_x6_split": ([_vp, _vp, _vp, _vp, _vp, _vp, _c.c_int32, _c.c_int32, _vp, _vp], _c.c_int),

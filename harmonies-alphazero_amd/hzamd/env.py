@@ -65,6 +65,11 @@ class BatchedEnv:
         `draws` pile draws) on/off; results are identical either way."""
         nat.check(nat.lib().hz_env_set_seed_ahead(self._h, int(draws) if enable else 0), "hz_env_set_seed_ahead")
 
+    def set_auto_ahead(self, enable):
+        """hz_rollout(auto_reset)'s episodes prepared ahead on/off
+        (hz_env_set_auto_ahead); results are identical either way."""
+        nat.check(nat.lib().hz_env_set_auto_ahead(self._h, int(bool(enable))), "hz_env_set_auto_ahead")
+
     def set_pipeline(self, pipeline):
         """hz_play's pipeline: 2 (the default) = every game spread over thirteen
         consecutive calls (k_play2), 1 = chance-ahead (k_rollout); results

@@ -155,6 +155,14 @@ int hz_env_set_seed_ahead(hz_env *env, int32_t draws);
  * auto_reset = 0, no trajectory outputs and max_plies >= 96 (others take
  * pipeline 1).  Returns -1 for a value other than 1 or 2. */
 int hz_env_set_pipeline(hz_env *env, int32_t pipeline);
+/* hz_rollout with auto_reset: on != 0 (the default, unless HZ_AR_AHEAD=0
+ * at hz_env_create) lets each such call's extra blocks prepare every board's
+ * episodes two and three ahead of its counter (seeded stream, pile script of
+ * the first 24 draws, cursors), so that a board whose game ends starts the
+ * next one from its script instead of seeding in place
+ * (harmonies_engine.py:66-79 + :120-137 restated ahead of time; a game's
+ * chance sequence does not depend on its moves).  Same results either way. */
+int hz_env_set_auto_ahead(hz_env *env, int32_t on);
 /* Both hz_play pipelines hand rows from one wave to another inside a block
  * through an LDS progress counter; a waiting wave spins at most spin_limit
  * s_sleep rounds.  A wait that gives up ORs a bit into the env's error word
@@ -341,6 +349,11 @@ int hz_resblock_x6_set_table(int32_t cf);
 int hz_tower_x6_blocks(const float *x, const void *const *w1, const float *const *b1, const void *const *w2,
                        const float *const *b2, int32_t nblk, float *out, float *tmp, int32_t batch,
                        const int32_t *live, void *stream);
+/* A/B knob (no reference counterpart): hz_tower_x6_blocks' first-round
+ * workgroups on every other CU of each XCD start `units` x 8,128 cycles late
+ * (0, the default: none), so the blocks' epilogue bursts of all CUs stop
+ * coinciding.  Results are the same bits either way. */
+int hz_tower_x6_set_stagger(int32_t units);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
  * 38 -> 128 channels, padding 1): board NCHW [batch][38][5][7] as the

@@ -517,3 +517,60 @@ def test_rule_ply_equals_three_calls():
     assert bool(envs[1].done().all())
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("plies", [96, 40, 250])
+def test_auto_reset_prepared_episodes_equal_in_place_seeding(Env, plies):
+    """hz_rollout(auto_reset) with episodes prepared ahead (the default) and
+    with every new game seeded in place (hz_env_set_auto_ahead(0)): the same
+    states, CPython streams (exported mid-run and at the end: boards then
+    play on streams copied back from the preparation slots), game and step
+    counts, on a partial block of boards; 250 plies per call ends up to four
+    games per board per call (only the first two may come from the slots);
+    and the final states and game counts equal the oracle's auto-reset
+    restatement."""
+    n, base, calls = 1000, 4242, 7
+    outs = []
+    for on in (True, False):
+        env = Env(n, seed_base=base, device=DEV)
+        env.set_auto_ahead(on)
+        env.reset()
+        games = torch.zeros(calls, n, dtype=torch.int32, device=DEV)
+        steps = torch.zeros(calls, n, dtype=torch.int32, device=DEV)
+        mid = None
+        for c in range(calls):
+            env.rollout(plies, auto_reset=True, games_done=games[c], steps_done=steps[c])
+            if c == 3:
+                mid = tuple(t.clone() for t in env.export_state(with_mt=True))
+        fin = env.export_state(with_mt=True)
+        env.check_errors()
+        outs.append([t.cpu() for t in (*mid, *fin, games.sum(0), steps.sum(0))])
+        env.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    total, finals, ref_games, _ = oracle.play_rule_auto(n, base, calls * plies, ep0=0, nthreads=8)
+    st = outs[0][3].numpy()
+    g = outs[0][6].numpy()
+    bad = [b for b in range(n) if not ((unpack_ref(st[:, b]) == finals[b]).all() and g[b] == ref_games[b])]
+    assert not bad, bad[:8]
+    assert int(outs[0][7].sum()) == total
+
+
+def test_auto_reset_then_per_ply_steps_continue_the_streams(Env):
+    """After auto-reset calls that left boards on prepared slots, the per-ply
+    surface (hz_rule_ply) continues every board's game and stream exactly as
+    after in-place seeding (the slots' streams materialised first)."""
+    n, base = 700, 77
+    outs = []
+    for on in (True, False):
+        env = Env(n, seed_base=base, device=DEV)
+        env.set_auto_ahead(on)
+        env.reset()
+        for _ in range(5):
+            env.rollout(96, auto_reset=True)
+        for _ in range(30):
+            env.rule_ply()
+        outs.append([t.cpu() for t in env.export_state(with_mt=True)])
+        env.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
