@@ -763,15 +763,14 @@ def selfplay_probe(args, dev, rank, world):
                                            "ranks, over the slowest rank's time",
                         "game": game})
             out["exchange"] = game.get("exchange")
-        out["steady"] = steady
-        if steady is not None:
-            out["steady_games_per_s"] = steady["games_per_s"]
         else:
             out.update({"env_steps_per_s": env_all / elapsed,
                         "env_steps_basis": "per-move leg: expansion children + real moves",
                         "games_per_s": world * n / (per_move * MEAN_SELFPLAY_PLIES),
                         "games_per_s_basis": f"estimate: ms per move x mean game length {MEAN_SELFPLAY_PLIES} "
                                              "plies (--sp-games 0)", "exchange": None})
+        out["steady"] = steady
+        out["steady_games_per_s"] = steady["games_per_s"] if steady is not None else None
         if guard.get("cpu_baseline") is not None:
             out["cpu_baseline"] = guard["cpu_baseline"]
     sp.mcts.close()
@@ -1376,6 +1375,7 @@ def main():
                               "and selfplay_games_per_s",
             "selfplay_env_steps_per_s": (sp or {}).get("env_steps_per_s"),
             "selfplay_games_per_s": (sp or {}).get("games_per_s"),
+            "selfplay_steady_games_per_s": (sp or {}).get("steady_games_per_s"),
             "env_games_per_s": games_per_s,
             "env_games_basis": "rule-driven env games (config 2, no MCTS) per second; the self-play games/s "
                                "is selfplay.games_per_s",

@@ -365,6 +365,37 @@ __device__ __forceinline__ int twist_block(Ptr w, int S, int start) {
   return k;
 }
 
+// twist_block for a board-major stream in global memory with 16-B accesses:
+// a wave's dword loads of 64 streams touch 64 lines each, so the vector
+// form moves the same lines with a quarter of the instructions.  start is a
+// multiple of 8 (the cursor's tw); the far words of block start are 8
+// consecutive words at 1 mod 4 (i + 397 or i - 227), except for start = 224
+// (they wrap from word 623 to 0: dword loads there).
+__device__ __forceinline__ int twist_block_vec(uint32_t* w, int start) {
+  const uint4 c0 = *(const uint4*)(w + start), c1 = *(const uint4*)(w + start + 4);
+  const uint32_t c8 = w[start + 8 < kMT ? start + 8 : 0];
+  uint32_t far[8];
+  if (start == 224) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int i = start + j;
+      far[j] = w[i < 227 ? i + 397 : i - 227];
+    }
+  } else {
+    const int f0 = start < 227 ? start + 397 : start - 227;  // = 1 mod 4
+    const uint4 a = *(const uint4*)(w + f0 - 1), b = *(const uint4*)(w + f0 + 3), c = *(const uint4*)(w + f0 + 7);
+    far[0] = a.y; far[1] = a.z; far[2] = a.w; far[3] = b.x;
+    far[4] = b.y; far[5] = b.z; far[6] = b.w; far[7] = c.x;
+  }
+  const uint32_t cur[9] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c8};
+  uint32_t o[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) o[j] = twist_word(cur[j], cur[j + 1], far[j]);
+  *(uint4*)(w + start) = make_uint4(o[0], o[1], o[2], o[3]);
+  *(uint4*)(w + start + 4) = make_uint4(o[4], o[5], o[6], o[7]);
+  return 8;
+}
+
 // A board's stream in global memory (board-major, contiguous): used by the
 // one-draw-per-call kernels (hz_step, hz_end_turn, ...) and the MCTS chance
 // replay.  Cursor = pos | tw << 16: pos = CPython's index, tw = words of the
@@ -406,21 +437,37 @@ template <int W>
 struct WinGMT {
   uint32_t* w;
   int pos, tw, left;
+  bool fresh;  // the window was fetched and nothing popped since (an early prefetch: the draw's is a no-op)
   uint32_t q[W];
 
   __device__ __forceinline__ WinGMT(uint32_t* words, int cursor)
-      : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16), left(0) {}
+      : w(words), pos(cursor & 0xFFFF), tw(cursor >> 16), left(0), fresh(false) {}
   __device__ __forceinline__ int cursor() const { return pos | (tw << 16); }
 
   __device__ __forceinline__ void prefetch() {
+    static_assert(W % 4 == 0, "window of whole 16-B loads");
+    if (fresh) return;
+    fresh = true;
     if (pos >= kMT) { pos = 0; tw = 0; }
-    while (tw < kMT && tw < pos + W) tw += twist_block(w, 1, tw);
+    while (tw < kMT && tw < pos + W) tw += twist_block_vec(w, tw);
     left = tw - pos < W ? tw - pos : W;
+    // words [pos, pos + W) from W / 4 + 1 aligned 16-B loads (a load past
+    // the stream's end rereads its last four words: positions >= 624 are
+    // never used), shifted by pos & 3 with selects (no dynamic index)
+    const int a = pos & ~3, sh = pos & 3;
+    uint32_t f[W + 4];
 #pragma unroll
-    for (int j = 0; j < W; j++) q[j] = j < left ? w[pos + j] : 0u;
+    for (int k = 0; k < W / 4 + 1; k++) {
+      const int o = a + 4 * k <= kMT - 4 ? a + 4 * k : kMT - 4;
+      const uint4 v = *(const uint4*)(w + o);
+      f[4 * k] = v.x; f[4 * k + 1] = v.y; f[4 * k + 2] = v.z; f[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < W; j++) q[j] = sh == 0 ? f[j] : sh == 1 ? f[j + 1] : sh == 2 ? f[j + 2] : f[j + 3];
   }
 
   __device__ __forceinline__ uint32_t next() {
+    fresh = false;
     if (left > 0) {
       const uint32_t v = q[0];
 #pragma unroll

@@ -341,6 +341,12 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
   State s = load_state(st, n, b);
+  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
+  // a third placement ends the turn, whose refill draws: the stream's
+  // read-ahead window (and the twist it may need) is fetched now, under the
+  // legal-mask and rule work, instead of after them (the draw then finds it)
+  const bool early = phase_of(s.misc) == PH_P3 && !game_done(s.misc);
+  if (early) d.m.prefetch();
   uint64_t m[3];
   int c = legal_mask(s, m);
   if (game_done(s.misc)) { m[0] = m[1] = m[2] = 0; c = 0; }
@@ -354,16 +360,18 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
   const int a = c > 0 ? kth_action(m, rule_pick(seed[b], p, c)) : -1;
   if (action) action[b] = (int16_t)a;
   if (a < 0) {
+    // (the early prefetch may have twisted words in place: its cursor, the
+    // same stream position, goes back with them)
+    if (early) pos[b] = d.m.cursor();
     if (status) status[b] = ST_NOOP;
     return;
   }
-  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
-    pos[b] = d.m.cursor();
     ply[b] = p + 1;
   }
+  if (r == ST_OK || early) pos[b] = d.m.cursor();
   if (status) status[b] = r;
 }
 

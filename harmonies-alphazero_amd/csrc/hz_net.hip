@@ -1634,7 +1634,13 @@ extern "C" int hz_resblock_x6_bias_act(const float *x, const void *w1, const flo
 // as nblk hz_resblock_x6_bias_act calls.  -2: this batch takes the
 // per-block path (hz_resblock_x6_fused(batch) == 0).
 extern "C" int32_t hz_resblock_x6_fused(int32_t batch);
-static std::atomic<int32_t> g_tower_stagger{0};
+// the default stagger (4 units, ~33 k cycles): 0.3-0.6 % per 4096-row forward
+// against none, bit-identical (tools/tower_stagger_ab.py, profiles/r06/s6d,
+// s6e); HZ_TOWER_STAGGER overrides it
+static std::atomic<int32_t> g_tower_stagger{[] {
+  const char *e = getenv("HZ_TOWER_STAGGER");
+  return e ? (int32_t)atoi(e) : (int32_t)4;
+}()};
 static int32_t tower_round() {  // the device's CU count: workgroups of the tower's first round
   static std::atomic<int32_t> cus{0};
   int32_t v = cus.load(std::memory_order_relaxed);

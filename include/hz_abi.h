@@ -351,8 +351,8 @@ int hz_tower_x6_blocks(const float *x, const void *const *w1, const float *const
                        const int32_t *live, void *stream);
 /* A/B knob (no reference counterpart): hz_tower_x6_blocks' first-round
  * workgroups on every other CU of each XCD start `units` x 8,128 cycles late
- * (0, the default: none), so the blocks' epilogue bursts of all CUs stop
- * coinciding.  Results are the same bits either way. */
+ * (default 4, HZ_TOWER_STAGGER overrides; 0: none), so the blocks' epilogue
+ * bursts of all CUs stop coinciding.  Results are the same bits either way. */
 int hz_tower_x6_set_stagger(int32_t units);
 
 /* out = relu(conv3x3(board, w) + bias[co]) for the stem (model.py:328-330,
