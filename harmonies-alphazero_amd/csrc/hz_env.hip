@@ -76,6 +76,14 @@ struct hz_env {
   int32_t *ar_cur;           // [kArSlots][kAheadDraws + 1][n]
   int32_t *ar_ep[2];         // [n] episode counter at the start of an auto-reset call, by call parity
   int ar_calls, ar_primed;
+  // per-ply draw windows (k_step / k_ply; see PlyWin): 12 stream words per
+  // board saved by the ply before a turn end, tagged with the cursor and
+  // the stream epoch, which every other entry point that can move or
+  // rewrite streams bumps
+  uint32_t *pw_words;        // [kPlyWin][nrow]
+  int32_t *pw_tag;           // [nrow] cursor the words start at (-1: none)
+  int32_t *pw_ep;            // [nrow] stream epoch of the words
+  int32_t mt_epoch;
   // pipeline 2 (hz_env_set_pipeline(e, 2); see k_play2): every board's game
   // spread over thirteen consecutive hz_play calls, one stage per call
   int pipeline;              // 1: chance-ahead (k_rollout's roles), 2: k_play2
@@ -261,10 +269,82 @@ __global__ void __launch_bounds__(kBlock) k_legal(const uint64_t *__restrict__ s
   if (count) count[b] = c;
 }
 
+// ---------------------------------------------------- per-ply draw windows
+// A turn end draws one pile (harmonies_engine.py:301-329 -> :132-137):
+// ~4 stream words, a twist of the generation in place every other time.
+// The per-ply kernels (k_step, k_ply) spread that memory work over the turn
+// instead of putting it on the turn-ending ply: the ply that makes a turn's
+// first placement twists the stream ahead until 12 words past the cursor
+// are twisted; the ply that makes the second saves those 12 words in the
+// board's slot (word-major, so the turn-ending ply loads them coalesced,
+// with its state, in the same round trip), tagged with the cursor and the
+// env's stream epoch.  The turn-ending ply draws from the slot when both
+// tags match (WinGMT's window, marked fresh: no load), from memory
+// otherwise.  The words are the stream's own and every other entry point
+// that can move or rewrite a stream bumps the epoch, so results never
+// depend on the slot.
+constexpr int kPlyWin = 12;
+static_assert(kPlyWin == 12, "WinMT12's window");
+struct PlyWin {
+  uint32_t *w;   // [kPlyWin][nrow]
+  int32_t *tag;  // [nrow]
+  int32_t *ep;   // [nrow]
+  long nrow;
+  int32_t epoch;
+};
+struct PlyWinIn {  // a board's slot, loaded with its state
+  uint32_t q[kPlyWin];
+  int32_t tag, ep;
+};
+__device__ __forceinline__ PlyWinIn win_load(const PlyWin &pw, int b) {
+  PlyWinIn in;
+#pragma unroll
+  for (int j = 0; j < kPlyWin; j++) in.q[j] = pw.w[(size_t)j * pw.nrow + b];
+  in.tag = pw.tag[b];
+  in.ep = pw.ep[b];
+  return in;
+}
+// the turn-ending ply: draw from the saved words when they are this cursor's
+__device__ __forceinline__ void win_take(const PlyWin &pw, const PlyWinIn &in, WinMT12 &m, int cursor) {
+  if (in.tag == cursor && in.ep == pw.epoch) {
+#pragma unroll
+    for (int j = 0; j < kPlyWin; j++) m.q[j] = in.q[j];
+    m.left = kPlyWin;
+    m.fresh = true;
+  }
+}
+// after a successful non-drawing step: twist ahead (a first placement made),
+// or save the next 12 words (a second placement made: the next ply ends the
+// turn).  m's cursor may move tw only (written back by the caller).
+__device__ __forceinline__ void win_prepare(const PlyWin &pw, WinMT12 &m, int b, int phase_after) {
+  if (phase_after != PH_P2 && phase_after != PH_P3) return;
+  if (m.pos >= kMT) return;  // (a generation's end: the draw's own prefetch handles it)
+  while (m.tw < kMT && m.tw < m.pos + kPlyWin) m.tw += twist_block_vec(m.w, m.tw);
+  if (phase_after != PH_P3) return;
+  if (m.tw - m.pos < kPlyWin) {  // the generation ends inside the window
+    pw.tag[b] = -1;
+    return;
+  }
+  const int a = m.pos & ~3, sh = m.pos & 3;
+  uint32_t f[kPlyWin + 4];
+#pragma unroll
+  for (int k = 0; k < kPlyWin / 4 + 1; k++) {
+    const int o = a + 4 * k <= kMT - 4 ? a + 4 * k : kMT - 4;
+    const uint4 v = *(const uint4 *)(m.w + o);
+    f[4 * k] = v.x; f[4 * k + 1] = v.y; f[4 * k + 2] = v.z; f[4 * k + 3] = v.w;
+  }
+#pragma unroll
+  for (int j = 0; j < kPlyWin; j++)
+    pw.w[(size_t)j * pw.nrow + b] = sh == 0 ? f[j] : sh == 1 ? f[j + 1] : sh == 2 ? f[j + 2] : f[j + 3];
+  pw.tag[b] = m.cursor();
+  pw.ep[b] = pw.epoch;
+}
+
 // ------------------------------------------------------------------- step
 __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                  int32_t *__restrict__ pos, int32_t *__restrict__ ply, int n,
-                                                 const int16_t *__restrict__ action, int32_t *__restrict__ status) {
+                                                 const int16_t *__restrict__ action, int32_t *__restrict__ status,
+                                                 PlyWin pw) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
   int a = action[b];
@@ -273,10 +353,14 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
     return;
   }
   State s = load_state(st, n, b);
-  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
+  const int c0 = pos[b];
+  const PlyWinIn win = win_load(pw, b);
+  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, c0)};
+  if (phase_of(s.misc) == PH_P3) win_take(pw, win, d.m, c0);
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
+    win_prepare(pw, d.m, b, phase_of(s.misc));
     pos[b] = d.m.cursor();
     ply[b] += 1;
   }
@@ -337,16 +421,22 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
                                                 int32_t *__restrict__ pos, int32_t *__restrict__ ply,
                                                 const uint64_t *__restrict__ seed, int n,
                                                 uint64_t *__restrict__ mask, int32_t *__restrict__ count,
-                                                int16_t *__restrict__ action, int32_t *__restrict__ status) {
+                                                int16_t *__restrict__ action, int32_t *__restrict__ status,
+                                                PlyWin pw) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
   State s = load_state(st, n, b);
-  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, pos[b])};
-  // a third placement ends the turn, whose refill draws: the stream's
-  // read-ahead window (and the twist it may need) is fetched now, under the
-  // legal-mask and rule work, instead of after them (the draw then finds it)
+  const int c0 = pos[b];
+  const PlyWinIn win = win_load(pw, b);
+  StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, c0)};
+  // a third placement ends the turn, whose refill draws: from the words the
+  // previous ply saved (PlyWin), or else the stream's read-ahead window (and
+  // the twist it may need) fetched now, under the legal-mask and rule work
   const bool early = phase_of(s.misc) == PH_P3 && !game_done(s.misc);
-  if (early) d.m.prefetch();
+  if (early) {
+    win_take(pw, win, d.m, c0);
+    d.m.prefetch();  // (a no-op after win_take)
+  }
   uint64_t m[3];
   int c = legal_mask(s, m);
   if (game_done(s.misc)) { m[0] = m[1] = m[2] = 0; c = 0; }
@@ -369,6 +459,7 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
   int r = step_state(s, a, d);
   if (r == ST_OK) {
     store_state(st, n, b, s);
+    win_prepare(pw, d.m, b, phase_of(s.misc));
     ply[b] = p + 1;
   }
   if (r == ST_OK || early) pos[b] = d.m.cursor();
@@ -2477,8 +2568,11 @@ __global__ void __launch_bounds__(64) k_mt_materialize_ar(uint32_t *__restrict__
   if (lane == 0) mt_src[b] = -1;
 }
 
+static PlyWin ply_win(hz_env *e) { return PlyWin{e->pw_words, e->pw_tag, e->pw_ep, (long)e->nrow, e->mt_epoch}; }
+
 static int materialize(hz_env *e) {
   if (!e->lazy) return 0;
+  e->mt_epoch++;  // streams rewritten (PlyWin's saved words are stale)
   if (e->ar_mt)
     hipLaunchKernelGGL(k_mt_materialize_ar, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ar_mt, e->mt_src, e->n);
   hipLaunchKernelGGL(k_mt_materialize, dim3(e->n), dim3(64), 0, e->stream, e->mt, e->ahead_mt[0], e->ahead_mt[1],
@@ -2590,6 +2684,7 @@ static int alloc_p2(hz_env *e) {
 // hashes in rings of kP2Ring (read by play stage st st + 1 calls later).  Every slot written by call c is read by call c + 1 or later,
 // so launch order on the stream is the only synchronisation.
 static int launch_play2(hz_env *e, int32_t max_plies, int32_t *games_done, int32_t *steps_done) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (alloc_p2(e)) return 1;
   const int c = e->calls2, r = c & 1, w = r ^ 1;
   if (!e->primed2) {
@@ -2741,6 +2836,12 @@ hz_env *hz_env_create(int32_t n_boards, uint64_t seed_base, void *stream) {
         c[0] % 4 == 0 && c[1] % 4 == 0 && c[2] % 4 == 0)
       for (int k = 0; k < 3; k++) e->p2_cut[k] = c[k];
   }
+  ok = ok && hipMalloc(&e->pw_words, e->nrow * kPlyWin * sizeof(uint32_t)) == hipSuccess &&
+       hipMalloc(&e->pw_tag, e->nrow * sizeof(int32_t)) == hipSuccess &&
+       hipMalloc(&e->pw_ep, e->nrow * sizeof(int32_t)) == hipSuccess &&
+       hipMemset(e->pw_tag, 0xff, e->nrow * sizeof(int32_t)) == hipSuccess &&
+       hipMemset(e->pw_ep, 0, e->nrow * sizeof(int32_t)) == hipSuccess;
+  e->mt_epoch = 1;
   ok = ok && hipMalloc(&e->wait_err_own, sizeof(int32_t)) == hipSuccess &&
        hipMemset(e->wait_err_own, 0, sizeof(int32_t)) == hipSuccess;
   e->wait_err = e->wait_err_own;
@@ -2771,6 +2872,9 @@ void hz_env_destroy(hz_env *e) {
     if (e->ring_cur[k]) (void)hipFree(e->ring_cur[k]);
     if (e->ring_k1[k]) (void)hipFree(e->ring_k1[k]);
   }
+  if (e->pw_words) (void)hipFree(e->pw_words);
+  if (e->pw_tag) (void)hipFree(e->pw_tag);
+  if (e->pw_ep) (void)hipFree(e->pw_ep);
   if (e->ar_mt) (void)hipFree(e->ar_mt);
   if (e->ar_tag) (void)hipFree(e->ar_tag);
   if (e->ar_pile) (void)hipFree(e->ar_pile);
@@ -2825,9 +2929,14 @@ int hz_env_set_stream(hz_env *e, void *stream) {
 uint64_t *hz_env_state_ptr(hz_env *e) { return e ? e->state : nullptr; }
 uint32_t *hz_env_mt_ptr(hz_env *e) {  // the streams are made current first (materialize)
   if (!e || materialize(e)) return nullptr;
+  e->mt_epoch++;  // the caller may move or rewrite streams (PlyWin)
   return e->mt;
 }
-int32_t *hz_env_mt_pos_ptr(hz_env *e) { return e ? e->pos : nullptr; }
+int32_t *hz_env_mt_pos_ptr(hz_env *e) {
+  if (!e) return nullptr;
+  e->mt_epoch++;
+  return e->pos;
+}
 int32_t *hz_env_ply_ptr(hz_env *e) { return e ? e->ply : nullptr; }
 uint64_t *hz_env_seed_ptr(hz_env *e) { return e ? e->seed : nullptr; }
 
@@ -2844,6 +2953,7 @@ int hz_env_set_seed_ahead(hz_env *e, int32_t draws) {
 }
 
 int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e) return -1;
   if (int err = materialize(e)) return err;  // unselected boards keep their streams
   e->primed = 0;  // episode counters move outside hz_play's plan
@@ -2864,7 +2974,7 @@ int hz_step(hz_env *e, const int16_t *action, int32_t *status) {
   if (!e || !action) return -1;
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_step, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
-                     e->n, action, status);
+                     e->n, action, status, ply_win(e));
   return launch_err();
 }
 
@@ -2872,7 +2982,7 @@ int hz_rule_ply(hz_env *e, uint64_t *mask, int32_t *count, int16_t *action, int3
   if (!e) return -1;
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_ply, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->ply,
-                     e->seed, e->n, mask, count, action, status);
+                     e->seed, e->n, mask, count, action, status, ply_win(e));
   return launch_err();
 }
 
@@ -2898,6 +3008,7 @@ int hz_rule_actions(hz_env *e, const uint64_t *mask, const int32_t *count, int16
 }
 
 int hz_greedy_actions(hz_env *e, const uint8_t *sel, int16_t *action) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e || !action) return -1;
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_greedy, dim3(e->n), dim3(64), 0, e->stream, e->state, e->mt, e->pos, e->n, sel, action);
@@ -2948,6 +3059,7 @@ static int alloc_ar(hz_env *e) {
 // ep_final from the counters.
 static int launch_rollout(hz_env *e, int32_t max_plies, int32_t auto_reset, int reset_first, uint64_t *traj_state,
                           uint64_t *traj_mask, int16_t *traj_action, int32_t *games_done, int32_t *steps_done) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e || max_plies < 0) return -1;
   e->primed2 = 0;  // (pipeline 2's episode prediction is stale after this launch)
   // hz_rollout continues the current games on their streams; hz_play starts
@@ -3061,6 +3173,7 @@ int hz_export_state(hz_env *e, uint64_t *state, uint32_t *mt, int32_t *mt_index)
 }
 
 int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const int32_t *mt_index) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e) return -1;
   if ((mt == nullptr) != (mt_index == nullptr)) return -2;
   size_t n = (size_t)e->n;
@@ -3076,6 +3189,7 @@ int hz_import_state(hz_env *e, const uint64_t *state, const uint32_t *mt, const 
 }
 
 int hz_replenish(hz_env *e, const uint8_t *sel) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e) return -1;
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,
@@ -3084,6 +3198,7 @@ int hz_replenish(hz_env *e, const uint8_t *sel) {
 }
 
 int hz_end_turn(hz_env *e, const uint8_t *sel) {
+  if (e) e->mt_epoch++;  // (may move or rewrite streams: PlyWin)
   if (!e) return -1;
   if (int err = materialize(e)) return err;
   hipLaunchKernelGGL(k_turn_op, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->mt, e->pos, e->n, sel,

@@ -574,3 +574,62 @@ def test_auto_reset_then_per_ply_steps_continue_the_streams(Env):
         env.close()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_ply_window_slots_never_change_results(Env, fused):
+    """hz_rule_ply / hz_step keep 12 stream words per board from the ply
+    before a turn end (PlyWin, tagged with the cursor and the stream epoch
+    that every stream-rewriting entry point bumps).  Boards whose streams are
+    replaced mid-turn by hz_import_state at the same CPython index, then
+    played on, match a fresh env given the same states and streams: every
+    state and stream after 12 more plies; and a run that crosses turn ends
+    uninterrupted matches the oracle's rule games."""
+    n = 300
+
+    def ply(env):
+        if fused:
+            env.rule_ply()
+        else:
+            mask, count = env.legal_mask()
+            env.step(env.rule_actions(mask, count))
+
+    a = Env(n, seed_base=5, device=DEV)
+    a.reset()
+    for _ in range(7):  # plies 0-6: windows saved after plies 2 and 6 (turn ends at 3, 7)
+        ply(a)
+    st, _, idx = a.export_state(with_mt=True)
+    other = Env(n, seed_base=91, device=DEV)
+    other.reset()
+    _, mt2, _ = other.export_state(with_mt=True)
+    a.import_state(st, mt2, idx)  # other words at the same cursors
+    for _ in range(12):
+        ply(a)
+    got = states_of(a)
+    _, mt, mi = a.export_state(with_mt=True)
+    mt, mi = mt.cpu().numpy().view(np.uint32), mi.cpu().numpy()
+    st, mt2, idx = st.cpu().numpy(), mt2.cpu().numpy().view(np.uint32), idx.cpu().numpy()
+    for b in range(0, n, 7):  # the oracle from the imported state and stream (rule seed 5 + b, ply 7)
+        s = unpack_ref(st[:, b])
+        m = oracle.mt_from_words(mt2[b], idx[b])
+        for p in range(7, 19):
+            if oracle.is_game_over(s):
+                break
+            mask = oracle.legal(s)
+            L = int(mask.sum())
+            act = np.flatnonzero(mask)[((oracle.rule(5 + b, p) >> 32) * L) >> 32]
+            s = oracle.step(s, int(act), m)[1]
+        assert (got[b] == s).all(), b
+        assert oracle.mt_next32(oracle.mt_from_words(mt[b], mi[b])) == oracle.mt_next32(m), b
+    # uninterrupted: whole rule games, turn ends drawing from saved words
+    d = Env(n, seed_base=17, device=DEV)
+    d.reset()
+    for _ in range(96):
+        ply(d)
+    _, finals, _, nxt = oracle.play_rule_games(n, 17, nthreads=8)
+    got = states_of(d)
+    _, mt, mi = d.export_state(with_mt=True)
+    mt, mi = mt.cpu().numpy().view(np.uint32), mi.cpu().numpy()
+    for b in range(n):
+        assert (got[b] == finals[b]).all(), b
+        assert oracle.mt_next32(oracle.mt_from_words(mt[b], mi[b])) == nxt[b], b
