@@ -32,6 +32,7 @@ pred = BatchedPredictor(net)
 class Rec:
     device_rows = True
     capturable = False
+    row_independent = True
 
     def __init__(self):
         self.calls = []
