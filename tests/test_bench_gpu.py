@@ -100,6 +100,7 @@ def test_bench_two_ranks_rehearsal():
     assert x["records"] == sp["game"]["moves"] and x["bytes_per_rank_received"] == x["records"] * 336
     assert 2 * 256 * 40 <= x["records"] <= 2 * 256 * 100
     assert sp["games_per_s_basis"].startswith("complete games") and sp["game"]["games"] == 2 * 256
+    assert sp["steady"]["games_ended"] >= 2 * 256  # both ranks' continuous legs, summed
     # every rank checked its own boards against the C twin and the oracle
     assert sp["parity"].startswith("512/512 boards bit-exact vs C twin")
     assert "8192/8192 boards bit-exact vs C oracle" in d["parity"]
@@ -133,6 +134,16 @@ def test_bench_single_rank_contract():
     assert sp["sims"] == 256 * 16 * 2 and 0 < sp["nn_rows_evaluated"] <= sp["sims"]
     assert 0 < sp["nn_roofline"]["frac"] < 1 and sp["nn_roofline"]["fp32_mfma_frac"] > 0
     assert sp["parity"].startswith("256/256 boards bit-exact vs C twin")
+    # continuous self-play: every board's first game ends inside the 80 moves
+    st = sp["steady"]
+    assert st["games_ended"] >= 256 and 40 <= st["mean_game_plies"] <= 100 and st["games_per_s"] > 0
+    assert sp["steady_games_per_s"] == st["games_per_s"] == d["selfplay_steady_games_per_s"]
+    # the caller-facing loop and the counter-derived rates
+    assert "replayed by the C oracle" in d["api_caller"]["parity"] and d["api_caller"]["env_steps_per_s"] > 0
+    assert d["auto_reset"]["env_steps_per_s"] > 0 and "bit-exact" in d["auto_reset"]["parity"]
+    if d["roofline"]["traffic_gbs"] is not None:
+        assert 0 < d["roofline"]["traffic_frac"] < 1
+    assert sp["tree_roofline"]["path_edge_levels"] >= sp["sims"] // 2
     assert sp["games_per_s_basis"].startswith("complete games") and sp["game"]["games"] == 256
     assert "load_checkpoint" in sp["network"]
     for k in ("value", "unit", "cores", "kind", "sample", "nn_cpu_ms_per_eval"):
