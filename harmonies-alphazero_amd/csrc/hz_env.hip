@@ -340,6 +340,35 @@ __device__ __forceinline__ void win_prepare(const PlyWin &pw, WinMT12 &m, int b,
   pw.ep[b] = pw.epoch;
 }
 
+// the same masks unpacked to one byte per action (bool [n][143], what
+// BatchedEnv.legal_actions() hands a caller): each lane unpacks its board's
+// three words into LDS, then the block writes its 64 boards' 9,152
+// contiguous bytes with 16-B stores (a byte store per action and lane
+// would touch 64 lines per instruction)
+__global__ void __launch_bounds__(kBlock) k_legal_bytes(const uint64_t *__restrict__ st, int n,
+                                                        uint8_t *__restrict__ out, int32_t *__restrict__ count) {
+  __shared__ uint4 s_out[kBlock * kActions / 16];
+  const int lane = threadIdx.x, b0 = blockIdx.x * kBlock, b = b0 + lane;
+  const int nb = n - b0 < kBlock ? n - b0 : kBlock;
+  uint64_t m[3] = {0, 0, 0};
+  int c = 0;
+  if (b < n) {
+    const State s = load_state(st, n, b);
+    c = legal_mask(s, m);
+    if (game_done(s.misc)) { m[0] = m[1] = m[2] = 0; c = 0; }
+    if (count) count[b] = c;
+  }
+  uint8_t *o = reinterpret_cast<uint8_t *>(s_out) + lane * kActions;
+#pragma unroll 8
+  for (int a = 0; a < kActions; a++) o[a] = (uint8_t)((m[a >> 6] >> (a & 63)) & 1);
+  __syncthreads();
+  const int total = nb * kActions;  // bytes of this block's boards
+  uint8_t *dst = out + (size_t)b0 * kActions;
+  // (out + b0 * 143 is 16-B aligned only when b0 is: 64 * 143 = 9,152 = 572 x 16 keeps it so from an aligned base)
+  for (int q = lane; q < total / 16; q += kBlock) reinterpret_cast<uint4 *>(dst)[q] = s_out[q];
+  for (int i = total / 16 * 16 + lane; i < total; i += kBlock) dst[i] = reinterpret_cast<const uint8_t *>(s_out)[i];
+}
+
 // ------------------------------------------------------------------- step
 __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint32_t *__restrict__ mt,
                                                  int32_t *__restrict__ pos, int32_t *__restrict__ ply, int n,
@@ -2961,6 +2990,12 @@ int hz_reset(hz_env *e, const uint8_t *sel, const uint64_t *seeds) {
   e->ar_primed = 0;
   hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kStageThreads), kResetLds, e->stream, e->state, e->mt, e->pos,
                      e->ply, e->episode, e->seed, e->n, e->seed_base, sel, seeds);
+  return launch_err();
+}
+
+int hz_legal_actions(hz_env *e, uint8_t *legal, int32_t *count) {
+  if (!e || !legal || ((uintptr_t)legal & 15)) return -1;
+  hipLaunchKernelGGL(k_legal_bytes, dim3(grid_for(e->n)), dim3(kBlock), 0, e->stream, e->state, e->n, legal, count);
   return launch_err();
 }
 

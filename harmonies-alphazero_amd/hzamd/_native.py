@@ -29,6 +29,7 @@ _SIGS = {
     "hz_env_seed_ptr": ([_vp], _vp),
     "hz_reset": ([_vp, _vp, _vp], _c.c_int),
     "hz_legal_mask": ([_vp, _vp, _vp], _c.c_int),
+    "hz_legal_actions": ([_vp, _vp, _vp], _c.c_int),
     "hz_step": ([_vp, _vp, _vp], _c.c_int),
     "hz_score": ([_vp, _vp, _vp], _c.c_int),
     "hz_replenish": ([_vp, _vp], _c.c_int),

@@ -111,10 +111,15 @@ class BatchedEnv:
         nat.check(nat.lib().hz_legal_mask(self._h, nat.ptr(out), nat.ptr(count)), "hz_legal_mask")
         return out, count
 
-    def legal_actions(self):
-        """Boolean [n, 143] view of legal_mask (unpacked on the device)."""
-        mask, _ = self.legal_mask()
-        return unpack_mask(mask)
+    def legal_actions(self, out=None, count=None):
+        """Boolean [n, 143] legal-action mask (get_legal_moves through
+        get_action_index, one launch: hz_legal_actions) and the legal counts
+        int32 [n]."""
+        self._sync_stream()
+        out = torch.empty(self.n, ACTION_SIZE, dtype=torch.bool, device=self.device) if out is None else out
+        count = self._count if count is None else count
+        nat.check(nat.lib().hz_legal_actions(self._h, nat.ptr(out), nat.ptr(count)), "hz_legal_actions")
+        return out
 
     def step(self, actions, status=None):
         """apply_move per board (actions int16 [n], <0 = no-op); int32 status."""

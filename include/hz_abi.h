@@ -69,6 +69,10 @@ int hz_reset(hz_env *env, const uint8_t *sel, const uint64_t *seeds);
  * board, mask[b*3 + w] bit i = action 64*w + i.  count[b] = #legal (may be
  * NULL).  A finished board has an empty mask. */
 int hz_legal_mask(hz_env *env, uint64_t *mask, int32_t *count);
+/* the same legal moves as one byte per action: legal[b*143 + a] = 1 when
+ * action a is legal on board b (a bool [n][143] tensor; legal 16-B aligned),
+ * count as above.  One launch for BatchedEnv.legal_actions(). */
+int hz_legal_actions(hz_env *env, uint8_t *legal, int32_t *count);
 
 /* step: apply_move (harmonies_engine.py:210-298) in place, including
  * _end_turn_actions (:301-329) and chance draws.  action[b] < 0 = no-op.

@@ -633,3 +633,25 @@ def test_ply_window_slots_never_change_results(Env, fused):
     for b in range(n):
         assert (got[b] == finals[b]).all(), b
         assert oracle.mt_next32(oracle.mt_from_words(mt[b], mi[b])) == nxt[b], b
+
+
+def test_legal_actions_bytes_equal_unpacked_mask(Env):
+    """hz_legal_actions (BatchedEnv.legal_actions: one byte per action, one
+    launch) equals the packed hz_legal_mask unpacked bit by bit, counts
+    included, on a partial block of boards spread over the game (finished
+    boards: all false)."""
+    from hzamd.env import unpack_mask
+    n = 1000
+    env = Env(n, seed_base=303, device=DEV)
+    env.reset()
+    plies = torch.arange(n, device=DEV) % 75
+    for p in range(75):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+    mask, count = env.legal_mask()
+    want, want_c = unpack_mask(mask).clone(), count.clone()
+    got = env.legal_actions()
+    assert got.dtype == torch.bool and got.shape == (n, 143)
+    assert torch.equal(got, want) and torch.equal(env._count, want_c)
+    assert bool((got.sum(1) == want_c).all()) and bool((want_c == 0).any())
