@@ -1610,7 +1610,7 @@ def api_caller_leg(args, dev, rank, world, plies=MAX_PLIES, reps=5):
     """The caller-facing batched loop (harmonies_engine.py:145-298 through
     process_game_state.py:156-179's action index), as a Python caller drives
     it: reset every board with its episode's seed, then per ply
-    BatchedEnv.legal_actions() (the 143-bit masks, unpacked on the device)
+    BatchedEnv.legal_actions() (bool [n, 143], one hz_legal_actions launch)
     -> the caller's own move, chosen OUTSIDE the env kernels with PyTorch ops
     on a device tensor (uniform over the legal moves: a seeded device
     generator's scores, masked, arg-max) -> BatchedEnv.step().  Eager launches
@@ -1675,9 +1675,9 @@ def api_caller_leg(args, dev, rank, world, plies=MAX_PLIES, reps=5):
     gbs = alg / dt / 1e9
     return {"env_steps_per_s": steps / dt, "games_per_s": resets / dt, "ms_per_batch": dt / reps * 1e3,
             "boards": n, "plies_per_batch": plies, "batches_timed": reps,
-            "launches_per_ply": "hz_legal_mask + unpack (3) + rand + masked_fill + any + argmax + where + copy "
-                                "+ hz_step (~10 eager launches)",
-            "roofline": {"bound": "launch (a Python loop of ~10 eager launches per ply)",
+            "launches_per_ply": "hz_legal_actions + rand + masked_fill + any + argmax + where + copy + hz_step "
+                                "(~8 eager launches)",
+            "roofline": {"bound": "launch (a Python loop of ~8 eager launches per ply)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                          "alg_bytes_per_batch": alg / reps / world,
                          "basis": f"{BYTES_PER_ENV_STEP} B per env step + {BYTES_PER_RESET} B per reset over the "
