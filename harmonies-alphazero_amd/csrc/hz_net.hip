@@ -2430,7 +2430,12 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
                                                   float *__restrict__ logits, float *__restrict__ probs,
                                                   float *__restrict__ value, int32_t batch,
                                                   const int32_t *__restrict__ live) {
-  __shared__ float4 w4[3][32];
+  // the 1x1 convs' weights, [filter][group][4 float4 + 1 pad]: a lane reads
+  // its group kk's float4 k4, and the eight groups of a wave sit 20 words
+  // apart (8 distinct 4-bank quads); unpadded, groups kk and kk + 2 were 32
+  // words apart, the same banks: 4-way conflicts on 108 ds_read_b128 per
+  // thread, most of the kernel's SQ_LDS_BANK_CONFLICT (ratio 0.379 in round 6)
+  __shared__ float4 w4[3][8][5];
   __shared__ float4 pin[kPIn][kHS / 4];
   __shared__ float4 vin[kVIn][kHS / 4];
   __shared__ float lg[kHS][kAct + 1];
@@ -2439,8 +2444,8 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   // cell] with a row stride of 292 = 4 mod 32 words: the writers (item i =
   // 8 (state cell) + group, consecutive lanes) and the readers (one state
   // cell per lane, groups in order) both touch 32 distinct banks per 32 lanes
-  // (round 5's [item][filter] layout read at a 24-word lane stride: 8-way
-  // conflicts, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.37)
+  // (round 5's [item][filter] layout read at a 24-word lane stride; the
+  // measured conflict ratio stayed at 0.379 without it: the w4 reads above)
   constexpr int kHpRow = 292;
   static_assert(kHpRow >= kHS * 35 && kHpRow % 32 == 4, "hpart row stride");
   __shared__ float hpart[3][8][kHpRow];
@@ -2451,7 +2456,7 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
   const int ns = batch - s0 < kHS ? batch - s0 : kHS;
   HZ_HSTAMP(0)
   HZ_HSTAMP_RT(8)
-  if (t < 96) w4[t >> 5][t & 31] = ((const float4 *)hw)[t];
+  if (t < 96) w4[t >> 5][(t >> 2) & 7][t & 3] = ((const float4 *)hw)[t];
   for (int i = t; i < kHS * kGlob; i += 256) {
     const int sl = i / kGlob, g = i - kGlob * sl;
     const float v = glob[(size_t)(s0 + (sl < ns ? sl : ns - 1)) * kGlob + g];
@@ -2487,9 +2492,8 @@ __global__ void __launch_bounds__(256) k_heads_fc(const float *__restrict__ x, c
         float e0 = 0.f, e1 = 0.f, e2 = 0.f;
 #pragma unroll
         for (int k4 = 0; k4 < 4; k4++) {
-          const int k = 4 * kk + k4;
           const f32x4 v = u[it][k4];
-          const float4 p = w4[0][k], q = w4[1][k], r = w4[2][k];
+          const float4 p = w4[0][kk][k4], q = w4[1][kk][k4], r = w4[2][kk][k4];
           e0 += v[0] * p.x + v[1] * p.y + v[2] * p.z + v[3] * p.w;
           e1 += v[0] * q.x + v[1] * q.y + v[2] * q.z + v[3] * q.w;
           e2 += v[0] * r.x + v[1] * r.y + v[2] * r.z + v[3] * r.w;
