@@ -535,21 +535,29 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, CS == 4 ? 
   // splitting it in place, but every staged value of an encoder board is then
   // a bf16 value, which lets the chunk skip the A pieces' products (below).
   // Slots past 39 stage as zeros.
+  // The second chunk stages slots 32-39 in every K slice pair (part p as
+  // part p & 1): its tap-packed K-steps read slice 0 in lane groups kg = 0, 2
+  // and the copy in slice 1 in kg = 1, 3 (aoff_tp), so the 16 lanes of an
+  // LDS cycle (positions {0-3, 12-15} of one group, {4-11} of the next: the
+  // class table's pairing) fall in even and odd bank slots; all reading
+  // slice 0 put them on the even slots only: 2-way conflicts on a third of
+  // the stem's A reads (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.236)
   auto stem_load = [&](int it, int q) -> f32x4 {
     f32x4 v;
     int f = it * kThreads + t;
     f = f < kRowsT * 8 ? f : kRowsT * 8 - 1;
-    const int c0 = 32 * q + 4 * (f & 7);
+    const int part = f & 7, pe = q == 1 ? (part & 1) : part;
+    const int c0 = 32 * q + 4 * pe, src = gsrc[it] + 4 * (pe - part) * 35;
     if (c0 == 36) {
-      v[0] = x[gsrc[it] + (32 * q) * 35];
-      const float p = x[gsrc[it] + (32 * q + 1) * 35];
+      v[0] = x[src + (32 * q) * 35];
+      const float p = x[src + (32 * q + 1) * 35];
       const float h = bf16_value(bf16_bits(p)), r = p - h, m = bf16_value(bf16_bits(r));
       v[1] = h;
       v[2] = m;
       v[3] = bf16_value(bf16_bits(r - m));
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC - 1 ? x[gsrc[it] + (32 * q + j) * 35] : 0.f;
+      for (int j = 0; j < 4; j++) v[j] = c0 + j < kBoardC - 1 ? x[src + (32 * q + j) * 35] : 0.f;
     }
     return v;
   };
@@ -648,7 +656,7 @@ __global__ void __launch_bounds__((CS == 8 ? 2 : 1) * (8 / NCB) * 64, CS == 4 ? 
   // (zero past tap 8): 3 K-steps instead of 9 (weights packed to match,
   // hzamd/infer.py pack_stem_x6)
   auto aoff_tp = [&](int rb, int st) -> int {
-    const int tap = 4 * st + kg, base = cbase[rb] - 16 * kg;
+    const int tap = 4 * st + kg, base = cbase[rb] - 16 * kg + 16 * (kg & 1);  // slice 0 or its copy in 1
     if (tap >= 9) return kZero + (base & 255);
     const int a = base + ((tap / 3 - 1) * 7 + (tap % 3 - 1)) * kX6Cell;
     return (valid[rb] >> tap) & 1 ? a : kZero + (a & 255);
