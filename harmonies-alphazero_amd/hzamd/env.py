@@ -44,6 +44,19 @@ class BatchedEnv:
     def _sync_stream(self):
         nat.lib().hz_env_set_stream(self._h, nat.stream_ptr(self.device))
 
+    def _out(self, t, shape, dtype, name):
+        """A caller-supplied buffer the kernels write: checked before its
+        pointer goes to the library (which trusts the size), None passes."""
+        if t is None:
+            return None
+        dev = t.device if isinstance(t, torch.Tensor) else None
+        if (dev is None or dev.type != "cuda" or (self.device.index is not None and dev.index != self.device.index)
+                or t.dtype != dtype or tuple(t.shape) != tuple(shape) or not t.is_contiguous()):
+            got = f"{t.dtype} {tuple(t.shape)} on {dev}" if dev is not None else type(t).__name__
+            raise ValueError(f"{name}: expected a contiguous {dtype} tensor of shape {tuple(shape)} on "
+                             f"{self.device}, got {got}")
+        return t
+
     def close(self):
         if getattr(self, "_h", None):
             torch.cuda.synchronize(self.device)
@@ -106,8 +119,8 @@ class BatchedEnv:
         """143-bit legal-action mask per board, int64 [n, 3] (bit i of word w
         = action 64*w + i) and the number of legal actions int32 [n]."""
         self._sync_stream()
-        out = self._mask if out is None else out
-        count = self._count if count is None else count
+        out = self._mask if out is None else self._out(out, (self.n, 3), torch.int64, "out")
+        count = self._count if count is None else self._out(count, (self.n,), torch.int32, "count")
         nat.check(nat.lib().hz_legal_mask(self._h, nat.ptr(out), nat.ptr(count)), "hz_legal_mask")
         return out, count
 
@@ -116,8 +129,9 @@ class BatchedEnv:
         get_action_index, one launch: hz_legal_actions) and the legal counts
         int32 [n]."""
         self._sync_stream()
-        out = torch.empty(self.n, ACTION_SIZE, dtype=torch.bool, device=self.device) if out is None else out
-        count = self._count if count is None else count
+        out = (torch.empty(self.n, ACTION_SIZE, dtype=torch.bool, device=self.device) if out is None
+               else self._out(out, (self.n, ACTION_SIZE), torch.bool, "out"))
+        count = self._count if count is None else self._out(count, (self.n,), torch.int32, "count")
         nat.check(nat.lib().hz_legal_actions(self._h, nat.ptr(out), nat.ptr(count)), "hz_legal_actions")
         return out
 
@@ -125,7 +139,7 @@ class BatchedEnv:
         """apply_move per board (actions int16 [n], <0 = no-op); int32 status."""
         self._sync_stream()
         actions = actions.to(device=self.device, dtype=torch.int16).contiguous()
-        status = self._status if status is None else status
+        status = self._status if status is None else self._out(status, (self.n,), torch.int32, "status")
         nat.check(nat.lib().hz_step(self._h, nat.ptr(actions), nat.ptr(status)), "hz_step")
         return status
 
@@ -158,7 +172,10 @@ class BatchedEnv:
         self._sync_stream()
         if mask is None:
             mask, count = self.legal_mask()
-        out = torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None else out
+        mask = self._out(mask, (self.n, 3), torch.int64, "mask")
+        count = self._out(count, (self.n,), torch.int32, "count")
+        out = (torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None
+               else self._out(out, (self.n,), torch.int16, "out"))
         nat.check(nat.lib().hz_rule_actions(self._h, nat.ptr(mask), nat.ptr(count), nat.ptr(out)),
                   "hz_rule_actions")
         return out
@@ -168,6 +185,10 @@ class BatchedEnv:
         (hz_rule_ply); the given output tensors get what the three calls
         would write."""
         self._sync_stream()
+        mask = self._out(mask, (self.n, 3), torch.int64, "mask")
+        count = self._out(count, (self.n,), torch.int32, "count")
+        action = self._out(action, (self.n,), torch.int16, "action")
+        status = self._out(status, (self.n,), torch.int32, "status")
         nat.check(nat.lib().hz_rule_ply(self._h, nat.ptr(mask), nat.ptr(count), nat.ptr(action), nat.ptr(status)),
                   "hz_rule_ply")
 
@@ -179,7 +200,8 @@ class BatchedEnv:
         self._sync_stream()
         if sel is not None:
             sel = sel.to(device=self.device, dtype=torch.uint8).contiguous()
-        out = torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None else out
+        out = (torch.empty(self.n, dtype=torch.int16, device=self.device) if out is None
+               else self._out(out, (self.n,), torch.int16, "out"))
         nat.check(nat.lib().hz_greedy_actions(self._h, nat.ptr(sel), nat.ptr(out)), "hz_greedy_actions")
         return out
 
@@ -193,8 +215,10 @@ class BatchedEnv:
             traj = (torch.zeros(max_plies, WORDS, self.n, dtype=torch.int64, device=self.device),
                     torch.zeros(max_plies, self.n, 3, dtype=torch.int64, device=self.device),
                     torch.full((max_plies, self.n), -1, dtype=torch.int16, device=self.device))
-        games_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if games_done is None else games_done
-        steps_done = torch.zeros(self.n, dtype=torch.int32, device=self.device) if steps_done is None else steps_done
+        games_done = (torch.zeros(self.n, dtype=torch.int32, device=self.device) if games_done is None
+                      else self._out(games_done, (self.n,), torch.int32, "games_done"))
+        steps_done = (torch.zeros(self.n, dtype=torch.int32, device=self.device) if steps_done is None
+                      else self._out(steps_done, (self.n,), torch.int32, "steps_done"))
         ts, tm, ta = traj if traj else (None, None, None)
         fn = nat.lib().hz_play if reset else nat.lib().hz_rollout
         nat.check(fn(self._h, int(max_plies), int(bool(auto_reset)), nat.ptr(ts), nat.ptr(tm), nat.ptr(ta),

@@ -655,3 +655,29 @@ def test_legal_actions_bytes_equal_unpacked_mask(Env):
     assert got.dtype == torch.bool and got.shape == (n, 143)
     assert torch.equal(got, want) and torch.equal(env._count, want_c)
     assert bool((got.sum(1) == want_c).all()) and bool((want_c == 0).any())
+
+
+@pytest.mark.gpu
+def test_caller_buffers_are_checked_before_launch(Env):
+    """A caller-supplied output buffer of the wrong shape, dtype or device is
+    refused with ValueError before its pointer reaches the library (the
+    kernels write n rows whatever the buffer holds); correct ones are used."""
+    n = 130
+    env = Env(n, seed_base=5, device=DEV)
+    env.reset()
+    bad = [
+        lambda: env.legal_actions(out=torch.zeros(n - 1, 143, dtype=torch.bool, device=DEV)),
+        lambda: env.legal_actions(out=torch.zeros(n, 143, dtype=torch.uint8, device=DEV)),
+        lambda: env.legal_actions(out=torch.zeros(n, 2 * 143, dtype=torch.bool, device=DEV)[:, ::2]),
+        lambda: env.legal_mask(out=torch.zeros(n, 3, dtype=torch.int64)),
+        lambda: env.legal_mask(count=torch.zeros(n, dtype=torch.int64, device=DEV)),
+        lambda: env.step(torch.zeros(n, dtype=torch.int16, device=DEV), status=torch.zeros(n - 2, dtype=torch.int32,
+                                                                                            device=DEV)),
+        lambda: env.rule_ply(torch.zeros(n, 2, dtype=torch.int64, device=DEV)),
+        lambda: env.rollout(4, games_done=torch.zeros(n // 2, dtype=torch.int32, device=DEV)),
+    ]
+    for f in bad:
+        with pytest.raises(ValueError):
+            f()
+    out = torch.ones(n, 143, dtype=torch.bool, device=DEV)
+    assert env.legal_actions(out=out) is out and int(out.sum()) == int(env._count.sum()) > 0
