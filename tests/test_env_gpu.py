@@ -681,3 +681,44 @@ def test_caller_buffers_are_checked_before_launch(Env):
             f()
     out = torch.ones(n, 143, dtype=torch.bool, device=DEV)
     assert env.legal_actions(out=out) is out and int(out.sum()) == int(env._count.sum()) > 0
+
+
+@pytest.mark.gpu
+def test_large_ragged_batch_vs_oracle(Env):
+    """16x the BASELINE batch plus a ragged tail (65,573 boards: 1,025 blocks
+    of 64, the last with 37 boards; many rounds of blocks per launch): the
+    thirteen-stage hz_play pipeline once full (episodes 12, 13), the
+    auto-reset rollout and the per-ply hz_rule_ply path, every board's final
+    state, ply / step counts and a sample of streams bit-exact vs the C
+    oracle."""
+    n, base = 65_573, 90_001
+    env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(2)
+    for ep in range(14):
+        _, steps, _ = env.rollout(200, reset=True)
+        if ep >= 12:
+            total, finals, plies, nxt = oracle.play_rule_games(n, base, nthreads=8, episode=ep)
+            assert (states_of(env) == finals).all(), ep
+            assert (steps.cpu().numpy() == plies).all() and int(steps.sum()) == total, ep
+            _, mt, idx = env.export_state(with_mt=True)
+            mt, idx = mt.cpu().numpy().view(np.uint32), idx.cpu().numpy()
+            for b in list(range(0, n, 4099)) + [n - 1]:
+                assert oracle.mt_next32(oracle.mt_from_words(mt[b], idx[b])) == nxt[b], (ep, b)
+    env.check_errors()
+    env.close()
+
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    games, steps, _ = env.rollout(96, auto_reset=True)
+    total, finals, g_want, ep_want = oracle.play_rule_auto(n, base, 96, ep0=0, nthreads=8)
+    assert int(steps.sum()) == total and (games.cpu().numpy() == g_want).all()
+    assert (states_of(env) == finals).all()
+    env.close()
+
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    for _ in range(96):
+        env.rule_ply()
+    total, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=0)
+    assert (states_of(env) == finals).all()
+    env.close()
