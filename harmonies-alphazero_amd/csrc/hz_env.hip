@@ -376,14 +376,22 @@ __global__ void __launch_bounds__(kBlock) k_step(uint64_t *__restrict__ st, uint
                                                  PlyWin pw) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
-  int a = action[b];
+  // every load of the step issued with the action's (one memory round trip;
+  // a no-op board's loads go unused)
+  const int a = action[b];
+  State s = load_state(st, n, b);
+  const int c0 = pos[b];
+  const PlyWinIn win = win_load(pw, b);
+  // (the compiler would sink these loads past the no-op branch: a second
+  // round trip; naming them here keeps all of them in the first)
+  asm volatile("" ::"v"(s.pl[0]), "v"(s.pl[1]), "v"(s.pl[2]), "v"(s.pl[3]), "v"(s.piles), "v"(s.misc), "v"(c0),
+               "v"(win.tag), "v"(win.ep), "v"(win.q[0]), "v"(win.q[1]), "v"(win.q[2]), "v"(win.q[3]), "v"(win.q[4]),
+               "v"(win.q[5]), "v"(win.q[6]), "v"(win.q[7]), "v"(win.q[8]), "v"(win.q[9]), "v"(win.q[10]),
+               "v"(win.q[11]));
   if (a < 0) {
     if (status) status[b] = ST_NOOP;
     return;
   }
-  State s = load_state(st, n, b);
-  const int c0 = pos[b];
-  const PlyWinIn win = win_load(pw, b);
   StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, c0)};
   if (phase_of(s.misc) == PH_P3) win_take(pw, win, d.m, c0);
   int r = step_state(s, a, d);
@@ -457,6 +465,10 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
   State s = load_state(st, n, b);
   const int c0 = pos[b];
   const PlyWinIn win = win_load(pw, b);
+  // the rule's inputs loaded with the state: read after the mask stores, they
+  // were a second dependent memory round trip on every ply
+  const int p = ply[b];
+  const uint64_t sd = seed[b];
   StreamDraw<WinMT12> d{WinMT12(mt + (size_t)b * kMT, c0)};
   // a third placement ends the turn, whose refill draws: from the words the
   // previous ply saved (PlyWin), or else the stream's read-ahead window (and
@@ -475,8 +487,7 @@ __global__ void __launch_bounds__(kBlock) k_ply(uint64_t *__restrict__ st, uint3
     mask[(size_t)b * 3 + 2] = m[2];
   }
   if (count) count[b] = c;
-  const int p = ply[b];
-  const int a = c > 0 ? kth_action(m, rule_pick(seed[b], p, c)) : -1;
+  const int a = c > 0 ? kth_action(m, rule_pick(sd, p, c)) : -1;
   if (action) action[b] = (int16_t)a;
   if (a < 0) {
     // (the early prefetch may have twisted words in place: its cursor, the
