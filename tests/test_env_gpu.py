@@ -722,3 +722,43 @@ def test_large_ragged_batch_vs_oracle(Env):
     total, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=8, episode=0)
     assert (states_of(env) == finals).all()
     env.close()
+
+
+@pytest.mark.gpu
+def test_single_board_every_path(Env):
+    """One board (a block with 63 idle lanes in every role): the thirteen-stage
+    hz_play until fully pipelined, the chance-ahead pipeline, the auto-reset
+    rollout, the per-ply surface and the byte mask, each bit-exact vs the
+    oracle."""
+    n, base = 1, 61
+    env = Env(n, seed_base=base, device=DEV)
+    env.set_pipeline(2)
+    for ep in range(15):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+    env.set_pipeline(1)
+    for ep in range(15, 19):
+        _, steps, _ = env.rollout(200, reset=True)
+        _check_episode(env, base, ep, steps)
+    env.check_errors()
+    env.close()
+
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    games, steps, _ = env.rollout(300, auto_reset=True)
+    total, finals, g_want, _ = oracle.play_rule_auto(n, base, 300, ep0=0, nthreads=1)
+    assert int(steps.sum()) == total and (games.cpu().numpy() == g_want).all()
+    assert (states_of(env) == finals).all()
+    env.close()
+
+    env = Env(n, seed_base=base, device=DEV)
+    env.reset()
+    while not bool(env.done().all()):
+        legal = env.legal_actions()
+        mask, count = env.legal_mask()
+        from hzamd.env import unpack_mask
+        assert torch.equal(legal, unpack_mask(mask)) and int(legal.sum()) == int(count[0])
+        env.rule_ply()
+    total, finals, plies, _ = oracle.play_rule_games(n, base, nthreads=1, episode=0)
+    assert (states_of(env) == finals).all()
+    env.close()
