@@ -11,18 +11,19 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "harmonies-alphazero_amd")]
 
 import torch  # noqa: E402
 
-from hzamd.infer import FoldedNet  # noqa: E402
+from hzamd.infer import FoldedNet, split_max_batch  # noqa: E402
 from hzamd.net import HarmoniesNet  # noqa: E402
 
 torch.manual_seed(0)
 fnet = FoldedNet(HarmoniesNet().eval().cuda())
 out = {}
+cap = split_max_batch(torch.device("cuda:0"))  # the split tower's co-residency limit on this device
 for batch in [int(b) for b in sys.argv[1:]] or (1, 16, 64, 256, 384, 512, 768, 1024):
     board = (torch.rand(batch, 38, 5, 7, device="cuda") > 0.8).float()
     glob = torch.rand(batch, 42, device="cuda")
     row = {}
-    for name, rmax, smax in (("split", 1 << 30, 32), ("resident", 1 << 30, 0), ("layered", 0, 0)):
-        if name == "split" and batch > 32:
+    for name, rmax, smax in (("split", 1 << 30, batch), ("resident", 1 << 30, 0), ("layered", 0, 0)):
+        if name == "split" and batch > cap:
             continue
         fnet.resident_max, fnet.split_max = rmax, smax
         for _ in range(5):
@@ -37,4 +38,4 @@ for batch in [int(b) for b in sys.argv[1:]] or (1, 16, 64, 256, 384, 512, 768, 1
         torch.cuda.synchronize()
         row[name] = round(e0.elapsed_time(e1) * 1e3 / n, 1)
     out[batch] = row
-print(json.dumps({"us_per_predict": out}))
+print(json.dumps({"split_max_batch": cap, "us_per_predict": out}))
