@@ -471,3 +471,41 @@ def test_path_edges_counts_walked_levels():
     assert 23 * n < tot < 23 * n * 12
     mcts.close()
     env.close()
+
+
+@pytest.mark.parametrize("sims", [1, 2, 3])
+def test_mcts_few_simulations_vs_oracle(sims):
+    """The smallest searches (one simulation: the root's expansion alone; two
+    and three: the first select steps below it) on a ragged batch of 130
+    boards at assorted positions: visits, tree sizes and the next MT word of
+    every board vs the C oracle."""
+    from hzamd.env import BatchedEnv
+    from hzamd.mcts import BatchedMCTS, stub_evaluator
+    n, base, cpuct = 130, 4100 + sims, 1.25
+    env = BatchedEnv(n, seed_base=base, device=DEV)
+    env.reset()
+    plies = torch.arange(n, device=DEV) % 67
+    for p in range(67):
+        mask, count = env.legal_mask()
+        act = env.rule_actions(mask, count)
+        env.step(torch.where(plies > p, act, torch.full_like(act, -1)))
+    st0, mt0, idx0 = env.export_state(with_mt=True)
+    st0, mt0, idx0 = st0.cpu().numpy(), mt0.cpu().numpy().view(np.uint32), idx0.cpu().numpy()
+    active = torch.from_numpy(np.array([not oracle.is_game_over(unpack_ref(st0[:, b])) for b in range(n)]))
+    assert int(active.sum()) > 0
+    mcts = BatchedMCTS(env, sims)
+    visits = mcts.search(stub_evaluator, cpuct, active=active).cpu().numpy()
+    counts = mcts.stats().cpu().numpy()
+    _, mt1, idx1 = env.export_state(with_mt=True)
+    mt1, idx1 = mt1.cpu().numpy().view(np.uint32), idx1.cpu().numpy()
+    for b in range(n):
+        if not active[b]:
+            assert visits[b].sum() == 0
+            continue
+        m = oracle.mt_from_words(mt0[b], idx0[b])
+        _, ov, nn, ne = oracle.mcts_search(unpack_ref(st0[:, b]), m, sims, cpuct, testing=True)
+        assert (visits[b] == ov).all(), b
+        assert (counts[b, 0], counts[b, 1]) == (nn, ne), b
+        assert oracle.mt_next32(oracle.mt_from_words(mt1[b], idx1[b])) == oracle.mt_next32(m), b
+    mcts.close()
+    env.close()
