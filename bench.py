@@ -699,7 +699,12 @@ def selfplay_probe(args, dev, rank, world):
     # does not take (select, expand, backup, gather + encode, noise, choice)
     edges = int(ev.edges.item())
     path = int(ev.path_edges.item())
-    tree_s = elapsed - nn_ms * 1e-3
+    # both from the instrumented pass: the network's event-timed share and
+    # that pass's own move time (the uninstrumented pass's time minus the
+    # instrumented pass's network time mixed two passes' clocks: 9.7-18.1 ms
+    # per move across boxes for the same code, against 12.6-12.9 this way;
+    # the event records, ~2 per simulation, count as tree time here)
+    tree_s = elapsed_i - nn_ms * 1e-3
     tree_bytes = rows * (BYTES_PER_ENCODE + TREE_BYTES_POLICY) + edges * TREE_BYTES_CHILD + path * TREE_BYTES_PATH
     tree_gbs = tree_bytes / tree_s / 1e9 if tree_s > 0 else None
     tree_roofline = {"bound": "latency (a wave per board walks, expands and backs up one path per simulation)",
@@ -710,8 +715,8 @@ def selfplay_probe(args, dev, rank, world):
                               f"evaluated leaf ({rows} rows), {TREE_BYTES_CHILD} B per expansion child (state, key "
                               f"digest, edge, hash slot; {edges} children), {TREE_BYTES_PATH} B per edge level "
                               f"walked (select's read + backup's N/W update; {path} levels = the sum of the trees' "
-                              "edge visit counts, hz_mcts_path_edges), over the timed moves' time minus the "
-                              "network's",
+                              "edge visit counts, hz_mcts_path_edges), over the instrumented pass's move time "
+                              "minus its event-timed network time",
                      "path_edge_levels": path, "mean_path_depth": path / max(1, board_moves * sims),
                      "traffic": traffic_rate(traffic_entry(args, "k_expand_backup<4, true, true, 16>"))}
     # the network's numerics in the measured run: rows of a timed leaf batch
@@ -733,11 +738,13 @@ def selfplay_probe(args, dev, rank, world):
                "sims_per_s": sims_all / elapsed, "nn_evals_per_s": rows_all / elapsed,
                "env_steps_per_s_per_move_leg": env_all / elapsed,
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
-               "tree_ms_per_move": per_move * 1e3 - nn_ms / args.sp_moves,
+               "tree_ms_per_move": (elapsed_i - nn_ms * 1e-3) / args.sp_moves * 1e3,
                "ms_per_move_instrumented": elapsed_i / args.sp_moves * 1e3,
                "per_move_basis": "ms_per_move: the timed moves alone; nn_ms_per_move: the same moves replayed from "
                                  "the same positions with a HIP event pair around every leaf evaluation "
-                                 "(ms_per_move_instrumented is that pass's move time); tree = the difference",
+                                 "(ms_per_move_instrumented is that pass's move time); tree_ms_per_move = "
+                                 "ms_per_move_instrumented - nn_ms_per_move (one pass: the event records count "
+                                 "as tree time)",
                "nn_rows_evaluated": rows, "sims": sims_done,
                "nn_roofline": {"bound": "mfma", "achieved": nn_tf, "peak": emu_peak, "unit": "TFLOP/s",
                                "frac": nn_tf / emu_peak if nn_tf else None,
