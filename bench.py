@@ -739,6 +739,7 @@ def selfplay_probe(args, dev, rank, world):
                "env_steps_per_s_per_move_leg": env_all / elapsed,
                "ms_per_move": per_move * 1e3, "nn_ms_per_move": nn_ms / args.sp_moves,
                "tree_ms_per_move": (elapsed_i - nn_ms * 1e-3) / args.sp_moves * 1e3,
+               "tree_ms_per_move_two_pass": per_move * 1e3 - nn_ms / args.sp_moves,
                "ms_per_move_instrumented": elapsed_i / args.sp_moves * 1e3,
                "per_move_basis": "ms_per_move: the timed moves alone; nn_ms_per_move: the same moves replayed from "
                                  "the same positions with a HIP event pair around every leaf evaluation "
