@@ -628,6 +628,12 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XSTAMP(k)
 #define HZ_XFLAG(k, v)
 #endif
+#ifdef HZ_KEYCHECK
+// diagnostic build only (tools/Makefile libhz_kc.so): children whose key
+// differs from canon_key of their state, leaves whose stored key differs from
+// canon_key of their stored state, children checked
+__device__ unsigned long long g_kc[3];
+#endif
 static_assert(kChildLds >= kMaxChildren, "child arrays hold every legal move");
 // 9.8 KB (was 12.3 KB, 19.5 KB before that): 16 waves fit a CU.  The turn-end
 // stream copy and the children's states share their bytes (the stream is
@@ -681,6 +687,19 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
   // (loaded now, used at the end)
   const int in_edge = d > 0 ? path[d - 1] : -1;
   State ls = load_node(m.node_state + (nb + leaf) * 6);
+  // the leaf's stored key (same round trip): its children's keys are built
+  // from it (canon_key_child); wave-uniform, kept in scalar registers
+  CKey lk;
+  {
+    const uint64_t *lkp = m.node_key + (nb + leaf) * 8;
+    uint64_t v[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) v[w] = lkp[w];
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+      lk.w[w] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v[w] >> 32)) << 32 |
+                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v[w]);
+  }
   int leaf_player = player_of(ls.misc);
   // policy/value row of this board: its own (per-board batch) or its row in
   // the gathered batch (hz_mcts_gather_leaves)
@@ -759,7 +778,15 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
           State ch = ls;
           ScriptDraw sd{turn_end ? L.script[c] : ~0ull};
           step_state(ch, a, sd);
-          CKey k = canon_key(ch, !m.exact_keys);
+          CKey k = canon_key_child(lk, ls, ch, a, !m.exact_keys);
+#ifdef HZ_KEYCHECK
+          {
+            const CKey want = canon_key(ch, !m.exact_keys), lw = canon_key(ls, !m.exact_keys);
+            if (!key_eq(want, k)) atomicAdd(&g_kc[0], 1ull);
+            if (!key_eq(lw, lk)) atomicAdd(&g_kc[1], 1ull);
+            atomicAdd(&g_kc[2], 1ull);
+          }
+#endif
 #pragma unroll
           for (int w = 0; w < 8; w++) L.key[c][w] = k.w[w];
 #pragma unroll
@@ -1435,3 +1462,9 @@ int hz_mcts_leaf_ptrs(hz_mcts *m, int32_t **leaf, int32_t **leaf_gidx) {
 }
 
 }  // extern "C"
+
+#ifdef HZ_KEYCHECK
+extern "C" int hz_keycheck_counts(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kc), sizeof(g_kc)) == hipSuccess ? 0 : 1;
+}
+#endif
