@@ -810,12 +810,24 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
       for (int s = lane; s < kDedupSlots; s += kWave) L.dslot[s] = 0u;  // empty (no entry is 0, see below)
       uint64_t *ht = m.ht + (size_t)b * m.hcap;
       uint64_t hmask = (uint64_t)(m.hcap - 1);
-      for (int c = lane; c < kChildSlots; c += kWave) {
+      // the free slot each probe ended on and the word it held: a new child's
+      // insertion (below) swaps its entry in there with one atomic, instead
+      // of reloading the slot first (a sibling may have taken it meanwhile:
+      // the swap then fails and the insertion probes on)
+      uint32_t fslot[2] = {0u, 0u};
+      uint64_t fold[2] = {0ull, 0ull};
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const int c = lane + r * kWave;
         if (c >= nl) continue;
         uint64_t h = L.hash[c];
         for (uint64_t slot = h & hmask;; slot = (slot + 1) & hmask) {
           uint64_t e = ht[slot];
-          if ((int)(e >> 32) != gen) break;
+          if ((int)(e >> 32) != gen) {
+            fslot[r] = (uint32_t)slot;
+            fold[r] = e;
+            break;
+          }
           int nid = (int)(uint32_t)e;
           // the node's stored canonical key against the child's (one memory
           // round trip after the table's; no key is rebuilt from a state)
@@ -953,12 +965,20 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
             for (int w = 0; w < 8; w++) m.node_key[(nb + node_id) * 8 + w] = L.key[c][w];
             m.node_e0[nb + node_id] = 0;
             m.node_ne[nb + node_id] = game_done(L.state[c][5]) ? -1 : 0;  // -1: terminal (never expanded)
-            for (uint64_t slot = L.hash[c] & hmask;; slot = (slot + 1) & hmask) {
-              unsigned long long old = ht[slot];
-              if ((int)(old >> 32) == gen) continue;
-              unsigned long long prev =
+            // the probe's free slot first (the word it held is the expected
+            // value); a failed swap names the slot's new word: taken by a
+            // sibling (this generation) -> the next slot, loaded
+            uint64_t slot = fslot[r];
+            unsigned long long old = fold[r];
+            for (;;) {
+              const unsigned long long prev =
                   atomicCAS((unsigned long long *)&ht[slot], old, (unsigned long long)ht_entry(gen, node_id));
               if (prev == old) break;
+              old = prev;
+              while ((int)(old >> 32) == gen) {
+                slot = (slot + 1) & hmask;
+                old = ht[slot];
+              }
             }
           }
           if (f != 2) {
