@@ -606,8 +606,11 @@ __device__ __forceinline__ int turn_end_draws_parallel(uint32_t *w, int cursor, 
 // ---------------------------------------------------------- expand + backup
 #ifdef HZ_DIAG
 // diagnostic build only (tools/expand_phases.py): per board, s_memtime at the
-// phase boundaries of k_expand_backup + flags; written to this buffer alone
-__device__ uint64_t g_exp_stamps[16384][12];
+// phase boundaries of k_expand_backup + flags; written to this buffer alone,
+// by the fused launches only (Sel: the search's simulations 1..S-1), so the
+// buffer holds the last fused launch's stamps; slots 12-14: after the next
+// simulation's select, after its leaf's encode, after the row-slot barriers
+__device__ uint64_t g_exp_stamps[16384][16];
 // one asm statement fenced by scheduling barriers, so the stamp stays where it
 // is written (cdna_hip_programming.md §7, in-kernel stamps)
 __device__ __forceinline__ uint64_t xstamp() {
@@ -620,10 +623,10 @@ __device__ __forceinline__ uint64_t xstamp() {
 #define HZ_XSTAMP(k) \
   {                                                          \
     const uint64_t t_ = xstamp();                            \
-    if (lane == 0 && b < 16384) g_exp_stamps[b][k] = t_;     \
+    if (dg && lane == 0 && b < 16384) g_exp_stamps[b][k] = t_; \
   }
 #define HZ_XFLAG(k, v) \
-  if (lane == 0 && b < 16384) g_exp_stamps[b][k] = (uint64_t)(v);
+  if (dg && lane == 0 && b < 16384) g_exp_stamps[b][k] = (uint64_t)(v);
 #else
 #define HZ_XSTAMP(k)
 #define HZ_XFLAG(k, v)
@@ -674,7 +677,9 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
                                                     const float *__restrict__ value,
                                                     const double *__restrict__ noise, double eps,
                                                     float one_minus_eps, int testing,
-                                                    const int32_t *__restrict__ row_of, int prio, int b, int lane) {
+                                                    const int32_t *__restrict__ row_of, int prio, int b, int lane,
+                                                    bool dg) {
+  (void)dg;  // (HZ_DIAG: stamp this launch)
   HZ_XSTAMP(0)
   HZ_XFLAG(10, 0)
   int leaf = m.leaf[b];
@@ -688,17 +693,13 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
   const int in_edge = d > 0 ? path[d - 1] : -1;
   State ls = load_node(m.node_state + (nb + leaf) * 6);
   // the leaf's stored key (same round trip): its children's keys are built
-  // from it (canon_key_child); wave-uniform, kept in scalar registers
-  CKey lk;
+  // from it (canon_key_child); wave-uniform, moved to scalar registers where
+  // the children start (the wait for these loads is not taken before then)
+  uint64_t lkv[8];
   {
     const uint64_t *lkp = m.node_key + (nb + leaf) * 8;
-    uint64_t v[8];
 #pragma unroll
-    for (int w = 0; w < 8; w++) v[w] = lkp[w];
-#pragma unroll
-    for (int w = 0; w < 8; w++)
-      lk.w[w] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v[w] >> 32)) << 32 |
-                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v[w]);
+    for (int w = 0; w < 8; w++) lkv[w] = lkp[w];
   }
   int leaf_player = player_of(ls.misc);
   // policy/value row of this board: its own (per-board batch) or its row in
@@ -765,6 +766,11 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
         wave_lds_sync();  // the stream copy is read before the children's states overwrite it
       }
       HZ_XSTAMP(2)
+      CKey lk;
+#pragma unroll
+      for (int w = 0; w < 8; w++)
+        lk.w[w] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(lkv[w] >> 32)) << 32 |
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)lkv[w]);
       // the children's priors are loaded here, their latency hidden under
       // the children's rule work
       // children: lane handles child c = lane and lane + 64 (one at a time:
@@ -1052,7 +1058,10 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
 // boards take their rows with one atomic add (16 boards: 256 adds per
 // simulation at 4096 boards instead of 4096 to one address, which cost ~20
 // us of same-address serialisation at L2).
-template <int Waves, bool Sel, bool Gather = false, int BPW = 1>  // Waves: minimum waves per SIMD the register allocation must allow (3: none forced)
+// WaveSlot (BPW > 1): each wave takes its row with its own atomic add as
+// soon as its walk is done, instead of the workgroup's one add after a
+// barrier that waits for the workgroup's slowest wave (A/B: HZ_SLOT_WAVE)
+template <int Waves, bool Sel, bool Gather = false, int BPW = 1, bool WaveSlot = false>  // Waves: minimum waves per SIMD the register allocation must allow (3: none forced)
 __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_eu(Waves, 8))) k_expand_backup(hz_mcts m, uint32_t *__restrict__ mtw,
                                                          int32_t *__restrict__ mtcur,
                                                          const float *__restrict__ policy,
@@ -1074,7 +1083,8 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
   const int b = (int)blockIdx.x * BPW + w;
   const bool live = BPW == 1 || b < m.n;
   if (live)
-    expand_backup_board(L, m, mtw, mtcur, policy, value, noise, eps, one_minus_eps, testing, row_of, prio, b, lane);
+    expand_backup_board(L, m, mtw, mtcur, policy, value, noise, eps, one_minus_eps, testing, row_of, prio, b, lane,
+                        Sel);
   if (Sel) {
     __builtin_amdgcn_s_setprio(0);
     // the walk reads N and W past L1: the backup's adds were done at L2 (the
@@ -1086,13 +1096,17 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
     // rest on same-address requests reaching L2 in issue order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     const int g = live ? select_board<true>(m, b, lane, active, cpuct) : -1;
+#ifdef HZ_DIAG
+    const bool dg = live;
+#endif
+    HZ_XSTAMP(12)
     if constexpr (Gather) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (add_prev && m.eval_ctr) m.eval_ctr[0] += *count_prev;  // final: its batch was evaluated
         *count_prev = 0;
       }
       int slot = -1;
-      if constexpr (BPW > 1) {
+      if constexpr (BPW > 1 && !WaveSlot) {
         if (lane == 0) s_need[w] = g >= 0;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1111,6 +1125,7 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
         slot = __builtin_amdgcn_readfirstlane(slot);
       }
       if (slot >= m.n) slot = -1;  // (count_out was not zero: never with the host's protocol)
+      HZ_XSTAMP(14)
       if (live && lane == 0) {
         m.slot[b] = slot;
         if (slot >= 0) {
@@ -1126,6 +1141,10 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
         encode_one(m.node_state + (size_t)g * 6, board + (size_t)slot * kBoardFloats,
                    glob + (size_t)slot * kGlobFloats, lane, smask, sval);
       }
+#ifdef HZ_DIAG
+      __builtin_amdgcn_s_waitcnt(0);
+#endif
+      HZ_XSTAMP(13)
     }
   }
 }
@@ -1393,14 +1412,19 @@ static int expand_backup(hz_mcts *m, hz_env *env, const float *policy, const flo
     const char *e = getenv("HZ_EXPAND_PRIO");
     return e && atoi(e) == 0 ? 0 : 1;
   }();
-#define HZ_EXPAND_LAUNCH(W, S, G, BP)                                                                           \
-  hipLaunchKernelGGL((k_expand_backup<W, S, G, BP>), dim3((m->n + (BP) - 1) / (BP)), dim3(kWave * (BP)),        \
+  static const bool wave_slot = [] {
+    const char *e = getenv("HZ_SLOT_WAVE");
+    return e && atoi(e) == 1;
+  }();
+#define HZ_EXPAND_LAUNCH(W, S, G, BP, ...)                                                                      \
+  hipLaunchKernelGGL((k_expand_backup<W, S, G, BP, ##__VA_ARGS__>), dim3((m->n + (BP) - 1) / (BP)), dim3(kWave * (BP)), \
                      0, m->stream, *m, hz_env_mt_ptr(env),                                                        \
                      hz_env_mt_pos_ptr(env), policy, value, noise, eps, ome, testing, slot, prio, active, cpuct,     \
                      board, glob, rows, count_out, count_prev, add_prev)
   const bool gat = sel && count_out;
   if (waves == 4) {
     if (gat && gather_bpw() == 8) HZ_EXPAND_LAUNCH(4, true, true, 8);
+    else if (gat && wave_slot) HZ_EXPAND_LAUNCH(4, true, true, kGatherBPW, true);
     else if (gat) HZ_EXPAND_LAUNCH(4, true, true, kGatherBPW);
     else if (sel) HZ_EXPAND_LAUNCH(4, true, false, 1);
     else HZ_EXPAND_LAUNCH(4, false, false, 1);

@@ -4,7 +4,9 @@ evaluator), one search of `sims` simulations; the stamps of the last
 simulation's expansion, per board: start, after the leaf's legal mask, after
 the turn-end chance replay, after the children, after the transposition
 probes, after the sibling dedup/ids, after the node/edge writes, after the
-backup.  Prints medians / 95th percentiles / maxima in cycles, by kind of
+backup; then the next simulation's select, the row-slot barriers and the
+leaf's encode.  The stamps are the last fused launch's (k_expand_backup with
+Sel: simulations 1..S-1; the search's final expansion does not stamp).  Prints medians / 95th percentiles / maxima in cycles, by kind of
 expansion, and the span of the launch.
 Usage (GPU box, repo root): HZ_LIB=tools/libhz_diag.so python tools/expand_phases.py [sims] [moves]"""
 import ctypes
@@ -35,7 +37,7 @@ torch.cuda.synchronize()
 done = sp.env.done()
 sp.mcts.search(stub_evaluator, 2.0, active=~done, testing=True)
 torch.cuda.synchronize()
-st = np.zeros((16384, 12), dtype=np.uint64)
+st = np.zeros((16384, 16), dtype=np.uint64)
 assert L.hz_mcts_diag_stamps(st.ctypes.data) == 0
 st = st[:n].astype(np.int64)
 flag = st[:, 10]
@@ -68,18 +70,24 @@ for kind, sel in (("turn_end", expanded & turn_end), ("other_expand", expanded &
         d["copy_in"] = summ(s[:, 8] - s[:, 1])
         d["draws"] = summ(s[:, 9] - s[:, 8])
         d["write_back"] = summ(s[:, 2] - s[:, 9])
+    d["backup->select"] = summ(s[:, 12] - s[:, 7])
+    d["select->slot_barriers"] = summ(s[:, 14] - s[:, 12])
+    d["slot_barriers->encoded"] = summ(s[:, 13] - s[:, 14])
+    d["whole_wave"] = summ(s[:, 13] - s[:, 0])
     res["wave_cycles"][kind] = d
 # s_memtime counters are per XCD (not synchronised across them): spans are
-# taken within an XCD (workgroup b runs on XCD b % 8)
-res["span_cycles_per_xcd"] = [int(st[x::8, 7].max() - st[x::8, 0].min()) for x in range(8)]
+# taken within an XCD (the fused launch: 16 boards per workgroup, workgroup
+# w on XCD w % 8)
+xcd = (np.arange(n) // 16) % 8
+res["span_cycles_per_xcd"] = [int(st[xcd == x, 13].max() - st[xcd == x, 0].min()) for x in range(8)]
 q = (0, 0.25, 0.5, 0.75, 0.95, 1)
 live = st[:, 7] >= st[:, 0]
 res["per_xcd"] = []
 for x in range(8):
-    sx = st[x::8][live[x::8]]
+    sx = st[(xcd == x) & live]
     t0x = sx[:, 0].min()
     res["per_xcd"].append({"start": [int(np.quantile(sx[:, 0] - t0x, v)) for v in q],
-                           "end": [int(np.quantile(sx[:, 7] - t0x, v)) for v in q]})
+                           "end": [int(np.quantile(sx[:, 13] - t0x, v)) for v in q]})
 starts = np.sort(st[:, 0] - t0)
 res["start_quantiles"] = [float(np.quantile(starts, q)) for q in (0, 0.25, 0.5, 0.75, 1)]
 print(json.dumps(res, indent=1))
