@@ -165,7 +165,10 @@ def test_gpu_train_step_matches_reference_fixture(graphed):
     weights: all but 1 % of the elements within 1e-5 (measured 0.37 % above:
     Adam divides each gradient by its own scale, so a gradient that is zero
     up to rounding takes either sign on the two devices and moves its weight
-    by ~lr either way), every element within three Adam steps (3 x lr)."""
+    by ~lr either way), every element within twice three Adam steps: an
+    Adam step moves an element by at most ~1.0014 lr here (beta 0.9 / 0.999),
+    and the two devices may move it in opposite directions at each of the
+    three steps (one box measured 3.05 lr: two sign disagreements)."""
     import numpy as np
     from hzamd.train import GraphedStep
     from test_manager_cpu import TRAIN_CFG, fixture, state
@@ -193,5 +196,5 @@ def test_gpu_train_step_matches_reference_fixture(graphed):
     print(f"graphed={graphed}: loss diff {d_loss:.3g}, weight diff max {d.max().item():.3g}, "
           f"median {d.median().item():.3g}, fraction > 1e-5 {far:.3g}")
     assert d_loss <= 1e-4, d_loss
-    assert far <= 1e-2 and d.max().item() <= 3 * lr * 1.01, (far, d.max().item())
+    assert far <= 1e-2 and d.max().item() <= 2 * 3 * lr * 1.01, (far, d.max().item())
     assert d.median().item() <= 1e-7
