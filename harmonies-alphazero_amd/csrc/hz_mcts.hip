@@ -195,17 +195,21 @@ template <bool Fresh = false>
 __device__ __forceinline__ int select_board(const hz_mcts &m, int b, int lane, const uint8_t *__restrict__ active,
                                             float cpuct) {
   int32_t *cnt = m.counts + (size_t)b * 4;
-  if ((active && !active[b]) || cnt[0] == 0) {
+  size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
+  // the board's flags and its root's edges in one memory round trip (the
+  // root's words are in bounds whether or not the board has a tree)
+  const bool act = !active || active[b];
+  const int n_nodes = cnt[0];
+  int ne = m.node_ne[nb], e0 = m.node_e0[nb];  // the root
+  if (!act || n_nodes == 0) {
     if (lane == 0) {
       m.leaf[b] = -1;
       m.leaf_gidx[b] = -1;
     }
     return -1;
   }
-  size_t nb = (size_t)b * m.max_nodes, eb = (size_t)b * m.max_edges;
   int node = 0, d = 0;
   int32_t *path = m.path + (size_t)b * m.max_depth;
-  int ne = m.node_ne[nb], e0 = m.node_e0[nb];  // the root
   bool term = false;                           // an active board's root is not terminal
   bool known = true;                           // ne came from the node itself
   for (;;) {
@@ -1096,6 +1100,15 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
     // rest on same-address requests reaching L2 in issue order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     const int g = live ? select_board<true>(m, b, lane, active, cpuct) : -1;
+    // Gather: the leaf's six state words, loaded before the row-slot
+    // barriers (their latency under the wait), encoded after them
+    uint64_t lsw[6] = {0, 0, 0, 0, 0, 0};
+    if constexpr (Gather) {
+      if (g >= 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) lsw[k] = m.node_state[(size_t)g * 6 + k];
+      }
+    }
 #ifdef HZ_DIAG
     const bool dg = live;
 #endif
@@ -1134,12 +1147,9 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
         }
       }
       if (slot >= 0) {
-        // the leaf's words are in L2 (the walk just read its edges; the node
-        // state was written by an earlier expansion)
         uint64_t *smask = &L.key[0][0];
         float *sval = reinterpret_cast<float *>(&L.key[40][0]);
-        encode_one(m.node_state + (size_t)g * 6, board + (size_t)slot * kBoardFloats,
-                   glob + (size_t)slot * kGlobFloats, lane, smask, sval);
+        encode_one(lsw, board + (size_t)slot * kBoardFloats, glob + (size_t)slot * kGlobFloats, lane, smask, sval);
       }
 #ifdef HZ_DIAG
       __builtin_amdgcn_s_waitcnt(0);
