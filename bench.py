@@ -56,6 +56,15 @@ PIPELINE_DEPTH = {1: 4, 2: 13}
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 X6_PRODUCTS = 6                # bf16 MFMAs per fp32 product block in the x6 kernels
+# bf16 MFMA FLOP the 4096-row forward's kernels issue per state (8-state
+# workgroups; v_mfma_f32_16x16x32_bf16 = 16,384 FLOP): the tower's 16 convs x
+# 4 chunks x 132 block-taps (the tap classes skip off-board taps: 132 of 162)
+# x 8 column blocks x 6 products, and the stem's chunk 0 (132 block-taps x 8
+# x 3: an encoder board's values are bf16 values, so only the A plane h
+# issues) and its tap-packed chunk 1 (3 K-steps x 18 blocks x 8 x 3), per
+# workgroup / 8 (hz_net.hip kX6ClassTaps, k_conv3x3_x6, x6w4_body)
+MFMA_FLOP = 16384
+X6_ISSUED_FLOP_PER_STATE = (16 * 4 * 132 * 8 * 6 + 132 * 8 * 3 + 3 * 18 * 8 * 3) * MFMA_FLOP / 8
 CLOCK_GHZ = 2.4            # MI355X peak engine clock (cycle figures of the issue-bound view)
 MT_SEED_STEPS = 1246       # init_by_array's two 623-step passes: the seeding chain per reset
 MT_STEP_FLOOR_CYCLES = 17  # tools/alu_chain.py: the bare MT recurrence per step
@@ -751,6 +760,18 @@ def selfplay_probe(args, dev, rank, world):
                                "frac": nn_tf / emu_peak if nn_tf else None,
                                "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS,
                                "fp32_mfma_frac": nn_tf / FP32_MFMA_PEAK_TFLOPS if nn_tf else None,
+                               "mfma_issued": {
+                                   "bf16_flop_per_eval": X6_ISSUED_FLOP_PER_STATE,
+                                   "achieved": (X6_ISSUED_FLOP_PER_STATE * rows / (nn_ms * 1e-3) / 1e12
+                                                if nn_ms else None),
+                                   "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                   "frac": (X6_ISSUED_FLOP_PER_STATE * rows / (nn_ms * 1e-3) / 1e12
+                                            / BF16_MFMA_PEAK_TFLOPS if nn_ms else None),
+                                   "basis": "bf16 MFMA FLOP the stem and tower kernels issue per state (the tap "
+                                            "classes skip off-board taps, the stem's bf16-exact inputs issue one "
+                                            "A plane) over the same event time, against the bf16 dense peak: the "
+                                            "matrix pipes' delivered rate, where frac above credits the dense fp32 "
+                                            "conv"},
                                "flop_per_eval": fl,
                                "basis": "fp32 FLOP of the whole leaf-eval forward at the 4096-row batch (HIP events "
                                         "around each call, incl. the heads) over the emulated-fp32 roof: the stem "
