@@ -826,26 +826,55 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
       // the swap then fails and the insertion probes on)
       uint32_t fslot[2] = {0u, 0u};
       uint64_t fold[2] = {0ull, 0ull};
+      // the lane's two children (c = lane, lane + 64) probe in lockstep, so
+      // a wide expansion's second child adds no chain of round trips of its
+      // own: each step loads both table words, then both candidates' keys
+      uint64_t pslot[2];
+      bool open[2];
 #pragma unroll
       for (int r = 0; r < 2; r++) {
         const int c = lane + r * kWave;
-        if (c >= nl) continue;
-        uint64_t h = L.hash[c];
-        for (uint64_t slot = h & hmask;; slot = (slot + 1) & hmask) {
-          uint64_t e = ht[slot];
-          if ((int)(e >> 32) != gen) {
-            fslot[r] = (uint32_t)slot;
-            fold[r] = e;
-            break;
+        open[r] = c < nl;
+        pslot[r] = open[r] ? L.hash[c] & hmask : 0;
+      }
+      while (open[0] || open[1]) {
+        uint64_t e[2] = {0ull, 0ull};
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+          if (open[r]) e[r] = ht[pslot[r]];
+        bool cand[2];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          cand[r] = open[r] && (int)(e[r] >> 32) == gen;
+          if (open[r] && !cand[r]) {  // a free slot: the child is not in the tree
+            fslot[r] = (uint32_t)pslot[r];
+            fold[r] = e[r];
+            open[r] = false;
           }
-          int nid = (int)(uint32_t)e;
-          // the node's stored canonical key against the child's (one memory
-          // round trip after the table's; no key is rebuilt from a state)
-          const uint64_t *nk = m.node_key + (nb + nid) * 8;
-          const int nne = m.node_ne[nb + nid], ne0 = m.node_e0[nb + nid];  // (same round trip)
+        }
+        // the candidate nodes' stored canonical keys against the children's
+        // (one memory round trip after the table's; no key is rebuilt from a
+        // state), with their edges and terminal marks
+        uint64_t nk[2][8];
+        int nne[2] = {0, 0}, ne0[2] = {0, 0};
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          if (cand[r]) {
+            const int nid = (int)(uint32_t)e[r];
+            const uint64_t *kp = m.node_key + (nb + nid) * 8;
+#pragma unroll
+            for (int w = 0; w < 8; w++) nk[r][w] = kp[w];
+            nne[r] = m.node_ne[nb + nid];
+            ne0[r] = m.node_e0[nb + nid];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          if (!cand[r]) continue;
+          const int c = lane + r * kWave, nid = (int)(uint32_t)e[r];
           bool eq = true;
 #pragma unroll
-          for (int w = 0; w < 8; w++) eq = eq && nk[w] == L.key[c][w];
+          for (int w = 0; w < 8; w++) eq = eq && nk[r][w] == L.key[c][w];
           if (eq) {
             L.flag[c] = nid == leaf ? 2 : 1;
             L.child[c] = nid;
@@ -853,8 +882,11 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
             // stored state decides, as the reference's Node does: equal keys
             // do not imply equal game_over); kept in the child's hash word,
             // which only new children read from here on
-            L.hash[c] = (uint64_t)(uint32_t)edge_hint_of(nne > 0 ? ne0 : 0, nne > 0 ? nne : 0, nne < 0);
-            break;
+            L.hash[c] = (uint64_t)(uint32_t)edge_hint_of(nne[r] > 0 ? ne0[r] : 0, nne[r] > 0 ? nne[r] : 0,
+                                                         nne[r] < 0);
+            open[r] = false;
+          } else {
+            pslot[r] = (pslot[r] + 1) & hmask;
           }
         }
       }
