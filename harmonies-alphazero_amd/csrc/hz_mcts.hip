@@ -705,6 +705,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
 #pragma unroll
     for (int w = 0; w < 8; w++) lkv[w] = lkp[w];
   }
+  const int leaf_ne = m.node_ne[nb + leaf];  // (same round trip) 0: not expanded yet
   int leaf_player = player_of(ls.misc);
   // policy/value row of this board: its own (per-board batch) or its row in
   // the gathered batch (hz_mcts_gather_leaves)
@@ -721,8 +722,19 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
     int nl = legal_mask(ls, mk);
     bool noisy = leaf == 0 && !testing && noise;
     HZ_XSTAMP(1)
-    if (nl > 0 && nl <= kMaxChildren && m.node_ne[nb + leaf] == 0) {
+    if (nl > 0 && nl <= kMaxChildren && leaf_ne == 0) {
       bool turn_end = phase_of(ls.misc) == PH_P3;
+      // the children's actions and priors (lane's c = lane, lane + 64): the
+      // policy row is read now, its latency under the chance replay and the
+      // rule work of the first child
+      int cact[2];
+      float cpri[2];
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const int c = lane + r * kWave;
+        cact[r] = c < nl ? kth_action(mk, c) : 0;
+        cpri[r] = c < nl ? policy[row * kActions + cact[r]] : 0.f;
+      }
       // the launch lasts as long as its slowest waves, the turn-end
       // expansions (chance replay + ~21 children: ~58 k cycles median against
       // ~41 k for the others, profiles/r03/expand_phases_spec_draws.json);
@@ -775,16 +787,14 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
       for (int w = 0; w < 8; w++)
         lk.w[w] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(lkv[w] >> 32)) << 32 |
                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)lkv[w]);
-      // the children's priors are loaded here, their latency hidden under
-      // the children's rule work
       // children: lane handles child c = lane and lane + 64 (one at a time:
       // the rule work of two children at once held 38 more registers than fit)
 #pragma unroll 1
       for (int r = 0; r < 2; r++) {
         const int c = lane + r * kWave;
         if (c < nl) {
-          int a = kth_action(mk, c);
-          L.prior[c] = policy[row * kActions + a];
+          const int a = r == 0 ? cact[0] : cact[1];
+          L.prior[c] = r == 0 ? cpri[0] : cpri[1];
           State ch = ls;
           ScriptDraw sd{turn_end ? L.script[c] : ~0ull};
           step_state(ch, a, sd);
@@ -1024,7 +1034,7 @@ __device__ __forceinline__ void expand_backup_board(ExpandLds &L, const hz_mcts 
             }
           }
           if (f != 2) {
-            int a = kth_action(mk, c);
+            const int a = cact[r];
             float p = L.prior[c];
             if (noisy) p = __double2float_rn(__dadd_rn((double)__fmul_rn(one_minus_eps, p),
                                                        __dmul_rn(eps, noise[(size_t)b * kMaxChildren + c])));
