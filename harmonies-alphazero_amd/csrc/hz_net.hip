@@ -1588,6 +1588,17 @@ static bool x6_blk_cf() {
 // 4-state form (k_conv3x3_x6<4, false, 4, 2>: two 4-wave workgroups per CU,
 // each one's epilogue and staging free to overlap the other's MFMAs;
 // A/B measurements)
+// the stem above the one-state forms in 4-state workgroups (64 KB of LDS:
+// two per CU, one's loads and stores under the other's MFMAs) instead of 8:
+// 47.8 vs 49.6 us at 4,096 encoder rows, bit-identical (tools/stem_ab.py,
+// alternating processes, profiles/r06/stem_cs4); HZ_STEM_CS4=0: 8 states
+static bool stem_cs4() {
+  static const bool v = [] {
+    const char *e = getenv("HZ_STEM_CS4");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
 static bool x6_cs4() {
   static const bool v = [] {
     const char *e = getenv("HZ_X6_CS4");
@@ -1600,6 +1611,8 @@ template <int NQ, bool Stem>
 static int launch_x6(const float *x, const void *wpack6, const float *bias, const float *res, float *out,
                      int32_t batch, const int32_t *live, void *stream) {
   if (batch <= x6_tiny_max()) return launch_x6_cs<NQ, Stem, 1, 1>(x, wpack6, bias, res, out, batch, live, stream);
+  if constexpr (Stem)
+    if (batch > x6_small_max() && stem_cs4()) return launch_x6_cs<NQ, Stem, 4, 2>(x, wpack6, bias, res, out, batch, live, stream);
   if constexpr (NQ == 4 && !Stem)
     if (batch > x6_small_max() && x6_cs4()) return launch_x6_cs<NQ, Stem, 4, 2>(x, wpack6, bias, res, out, batch, live, stream);
   if constexpr (NQ == 4 && !Stem)

@@ -23,7 +23,8 @@ import numpy as np
 KEEP = ("k_play2", "k_rollout", "k_conv3x3_x6w4", "k_conv3x3_x6<", "k_stem", "k_heads_fc", "k_expand_backup",
         "k_select", "k_gather_encode", "k_ply", "k_legal", "k_step", "k_rule", "k_score", "k_tower_x6", "k_x6w4_tower")
 # the full-batch leaf-eval forward: the residual tower in one launch, the stem, the fused head
-NN_KERNELS = ("k_x6w4_tower<true>", "k_conv3x3_x6<2, true, 8, 2>", "k_heads_fc")
+# (the stem: 4-state workgroups since round 6, 8 before; whichever ran)
+NN_KERNELS = ("k_x6w4_tower<true>", ("k_conv3x3_x6<2, true, 4, 2>", "k_conv3x3_x6<2, true, 8, 2>"), "k_heads_fc")
 
 
 def short(name):
@@ -83,8 +84,10 @@ def main():
             out["selfplay_line"]["nn_roofline_frac"] = nr.get("frac")
             # the same roofline from the profile: the forward's kernels'
             # median dispatches (most dispatches are full 4,096-row batches)
-            if nr.get("flop_per_eval") and all(kn2 in kernels for kn2 in NN_KERNELS):
-                fwd_us = sum(kernels[kn2]["median_us"] for kn2 in NN_KERNELS)
+            found = [next((a for a in (kn2 if isinstance(kn2, tuple) else (kn2,)) if a in kernels), None)
+                     for kn2 in NN_KERNELS]
+            if nr.get("flop_per_eval") and all(found):
+                fwd_us = sum(kernels[kn2]["median_us"] for kn2 in found)
                 rows = sp.get("boards") or 4096
                 out["selfplay_line"]["nn_forward_us_from_median"] = fwd_us
                 out["selfplay_line"]["nn_roofline_frac_from_median"] = (
