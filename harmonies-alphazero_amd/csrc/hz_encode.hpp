@@ -193,8 +193,12 @@ __device__ __forceinline__ void encode_pair(const uint64_t *__restrict__ st, lon
 // row's 665 float2 are written contiguously.  The same masks, values and
 // element order as encode_pair (so the same bits).  The MCTS kernel that
 // selects a leaf encodes it with this in place of a separate gather launch.
-__device__ __forceinline__ void encode_one(const uint64_t *__restrict__ ns, float *__restrict__ board_row,
-                                           float *__restrict__ glob_row, int lane, uint64_t *smask, float *sval) {
+// In two parts: encode_one_values builds the row in the lane's registers
+// (its 11 float2 of the board row, its global), encode_one_store writes it;
+// the MCTS kernel builds before it knows the row's batch slot.
+constexpr int kEncQ = (665 + 63) / 64;  // float2 of the board row per lane
+__device__ __forceinline__ void encode_one_values(const uint64_t *__restrict__ ns, int lane, uint64_t *smask,
+                                                  float *sval, float2 (&vals)[kEncQ], float &gv_out) {
   if (lane < 38) {
     const int ch = lane;
     uint64_t mask;
@@ -241,19 +245,37 @@ __device__ __forceinline__ void encode_one(const uint64_t *__restrict__ ns, floa
   // float2 q = elements 2 q, 2 q + 1: channel c0, position y0 (q advances by
   // 64: elements by 128 = 3 channels + 23 positions)
   int c0 = (2 * lane) / 35, y0 = 2 * lane - 35 * c0;
-  for (int q = lane; q < 665; q += 64) {
-    const uint64_t ma = smask[c0], mb = smask[c0 + 1 < 38 ? c0 + 1 : c0];
-    const float va = sval[c0], vb = sval[c0 + 1 < 38 ? c0 + 1 : c0];
-    const float v0 = ((ma >> y0) & 1) ? va : 0.f;
-    const bool nxt = y0 + 1 >= 35;
-    const int p1 = nxt ? 0 : y0 + 1;
-    const float v1 = (((nxt ? mb : ma) >> p1) & 1) ? (nxt ? vb : va) : 0.f;
-    reinterpret_cast<float2 *>(board_row)[q] = make_float2(v0, v1);
+#pragma unroll
+  for (int k = 0; k < kEncQ; k++) {
+    float v0 = 0.f, v1 = 0.f;
+    if (lane + 64 * k < 665) {
+      const uint64_t ma = smask[c0], mb = smask[c0 + 1 < 38 ? c0 + 1 : c0];
+      const float va = sval[c0], vb = sval[c0 + 1 < 38 ? c0 + 1 : c0];
+      v0 = ((ma >> y0) & 1) ? va : 0.f;
+      const bool nxt = y0 + 1 >= 35;
+      const int p1 = nxt ? 0 : y0 + 1;
+      v1 = (((nxt ? mb : ma) >> p1) & 1) ? (nxt ? vb : va) : 0.f;
+    }
+    vals[k] = make_float2(v0, v1);
     c0 += 3;
     y0 += 23;
     if (y0 >= 35) { y0 -= 35; c0++; }
   }
+  gv_out = gv;
+}
+__device__ __forceinline__ void encode_one_store(float *__restrict__ board_row, float *__restrict__ glob_row, int lane,
+                                                 const float2 (&vals)[kEncQ], float gv) {
+#pragma unroll
+  for (int k = 0; k < kEncQ; k++)
+    if (lane + 64 * k < 665) reinterpret_cast<float2 *>(board_row)[lane + 64 * k] = vals[k];
   if (lane < 42) glob_row[lane] = gv;
+}
+__device__ __forceinline__ void encode_one(const uint64_t *__restrict__ ns, float *__restrict__ board_row,
+                                           float *__restrict__ glob_row, int lane, uint64_t *smask, float *sval) {
+  float2 vals[kEncQ];
+  float gv;
+  encode_one_values(ns, lane, smask, sval, vals, gv);
+  encode_one_store(board_row, glob_row, lane, vals, gv);
 }
 
 template <bool Glob>

@@ -1142,13 +1142,18 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
     // rest on same-address requests reaching L2 in issue order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     const int g = live ? select_board<true>(m, b, lane, active, cpuct) : -1;
-    // Gather: the leaf's six state words, loaded before the row-slot
-    // barriers (their latency under the wait), encoded after them
-    uint64_t lsw[6] = {0, 0, 0, 0, 0, 0};
+    // Gather: the leaf's six state words loaded and its row built in the
+    // lane's registers (encode_one_values) before the row-slot barriers,
+    // under the wait for the workgroup's slowest wave; after them only the
+    // row's stores remain
+    float2 evals[kEncQ];
+    float egv = 0.f;
     if constexpr (Gather) {
       if (g >= 0) {
+        uint64_t lsw[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) lsw[k] = m.node_state[(size_t)g * 6 + k];
+        encode_one_values(lsw, lane, &L.key[0][0], reinterpret_cast<float *>(&L.key[40][0]), evals, egv);
       }
     }
 #ifdef HZ_DIAG
@@ -1189,9 +1194,7 @@ __global__ void __launch_bounds__(kWave * BPW) __attribute__((amdgpu_waves_per_e
         }
       }
       if (slot >= 0) {
-        uint64_t *smask = &L.key[0][0];
-        float *sval = reinterpret_cast<float *>(&L.key[40][0]);
-        encode_one(lsw, board + (size_t)slot * kBoardFloats, glob + (size_t)slot * kGlobFloats, lane, smask, sval);
+        encode_one_store(board + (size_t)slot * kBoardFloats, glob + (size_t)slot * kGlobFloats, lane, evals, egv);
       }
 #ifdef HZ_DIAG
       __builtin_amdgcn_s_waitcnt(0);
