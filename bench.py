@@ -727,7 +727,7 @@ def selfplay_probe(args, dev, rank, world):
                               "edge visit counts, hz_mcts_path_edges), over the instrumented pass's move time "
                               "minus its event-timed network time",
                      "path_edge_levels": path, "mean_path_depth": path / max(1, board_moves * sims),
-                     "traffic": traffic_rate(traffic_entry(args, "k_expand_backup<4, true, true, 16>"))}
+                     "traffic": traffic_rate(traffic_entry(args, "k_expand_backup<4, true, true, 16, false>"))}
     # the network's numerics in the measured run: rows of a timed leaf batch
     # against the checkpoint's network in float64 on the CPU
     nn_parity = nn_guard(ev, dev)

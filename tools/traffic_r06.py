@@ -3,7 +3,7 @@ passes (FETCH_SIZE, WRITE_SIZE: each its own run of the same command) and
 each kernel's mean duration from a kernel-trace pass of that command, for
 the kernels bench.py prices: k_play2 (config 2), k_rollout<true, false>
 (the auto-reset leg), k_x6w4_tower<true> (the leaf-eval tower) and
-k_expand_backup<4, true, true, 16> (the tree).  Bytes = (2 x FETCH_SIZE +
+k_expand_backup<4, true, true, 16, false> (the tree).  Bytes = (2 x FETCH_SIZE +
 WRITE_SIZE) x 1024: on gfx950 FETCH_SIZE counts half the bytes of wide
 streaming reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact.
 
@@ -17,7 +17,7 @@ import os
 import re
 import sys
 
-KERNELS = ("k_play2", "k_rollout<true, false>", "k_x6w4_tower<true>", "k_expand_backup<4, true, true, 16>")
+KERNELS = ("k_play2", "k_rollout<true, false>", "k_x6w4_tower<true>", "k_expand_backup<4, true, true, 16, false>")
 
 
 def short(name):
